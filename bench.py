@@ -1,0 +1,316 @@
+"""Benchmark of the GeePS gradient-update reduction path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Workload (BASELINE.json north-star target / configs[2]): a 1M-row x 1024 fp32
+parameter table, 8 synthetic clients, the table row-range sharded over the N
+GPUs as N server shards (src/client/clientlib-viter.cpp:674-682).  Client c is
+hosted on rank c % N; its delta buffer is uniform in [-0.5, 0.5) (seed 1000+c).
+
+A *step* is one device-resident N-way reduction: each shard adds the 8 client
+buckets for its rows into its master copy in client order 0..7 with one
+gp_bucket_sum_apply launch (the reference's TabletStorage::apply_updates x 8,
+src/server/tablet-server.cpp:119-134).  At N > 1 the buckets were first moved
+to their shard by RCCL all-to-all (untimed here; the exchange-inclusive step
+exchange + apply + all-gather refresh is timed separately and reported as
+`exchange_inclusive`).  Total work is fixed as N grows: scaling "strong".
+
+value = gradient (delta) bytes reduced per second, whole job:
+        clients * rows * width * 4 B / max-over-ranks step time.
+roofline.achieved = algorithmic HBM bytes of one launch ((clients + 2) * shard
+        bytes: 8 bucket reads + master read + master write) / its average
+        duration from HIP events on the launch stream.
+cpu_baseline = the oracle's restatement of the reference server arithmetic
+        (sequential vsAdd per client, gcc -O3) on rank 0's host cores, on a
+        bounded 128K-row sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roofline"
+KERNEL_NAME = "bucket_sum_vec_kernel"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--rows", type=int, default=1 << 20)
+    p.add_argument("--width", type=int, default=1024)
+    p.add_argument("--clients", type=int, default=8)
+    p.add_argument("--exchange", choices=["a2a", "rs"], default="a2a")
+    p.add_argument("--exchange-steps", type=int, default=5)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-inclusive", action="store_true")
+    p.add_argument("--cpu-rows", type=int, default=1 << 17)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    return p.parse_args()
+
+
+def init_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != n_gpus:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return (dist.get_rank() if world > 1 else 0), world, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_deltas(hosted, n, dev):
+    g = torch.Generator(device=dev)
+    out = []
+    for c in hosted:
+        g.manual_seed(1000 + c)
+        d = torch.rand(n, generator=g, device=dev)
+        d.sub_(0.5)
+        out.append(d)
+    return out
+
+
+def timed_apply(red, steps, warmup, world, dev):
+    """Device-resident reduction: K launches, HIP events around each one on the
+    launch stream, wall clock bracketed by barrier + synchronize."""
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        red.apply()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        red.apply()
+        b.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    return wall, kernel_ms
+
+
+def timed_exchange(red, deltas, steps, warmup, world):
+    for _ in range(warmup):
+        red.step(deltas)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        red.step(deltas)
+    barrier(world)
+    return time.perf_counter() - t0
+
+
+def host_inclusive(rows, W, clients, dev, steps=3):
+    """The path starts and ends in host memory: H2D of the arriving client
+    buckets (pinned), the N-way sum, D2H of the refreshed shard.  Measured on a
+    1/8-size table (128K rows) so the pinned staging stays small."""
+    from geeps_amd import rowops
+    n = rows * W
+    host = [torch.empty(n, dtype=torch.float32).pin_memory() for _ in range(clients)]
+    for c, h in enumerate(host):
+        h.uniform_(-0.5, 0.5)
+    out = torch.empty(n, dtype=torch.float32).pin_memory()
+    dbuf = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(clients)]
+    master = torch.zeros(n, dtype=torch.float32, device=dev)
+    copy = torch.cuda.Stream()
+    comp = torch.cuda.current_stream()
+
+    def one():
+        # H2D on a copy stream, bucket k's arrival overlapped with nothing else
+        # to keep it simple and honest: all copies, then the sum, then D2H.
+        with torch.cuda.stream(copy):
+            for h, d in zip(host, dbuf):
+                d.copy_(h, non_blocking=True)
+        comp.wait_stream(copy)
+        rowops.bucket_sum_apply(master, dbuf)
+        out.copy_(master, non_blocking=True)
+        torch.cuda.synchronize()
+
+    one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = (time.perf_counter() - t0) / steps
+    return {"rows": rows, "width": W, "clients": clients,
+            "ms_per_step": dt * 1e3,
+            "delta_GBps": clients * n * 4 / dt / 1e9,
+            "note": "pinned H2D of all client buckets + one N-way sum + D2H of the shard"}
+
+
+def cpu_baseline(rows, W, clients, seconds):
+    """The oracle's restatement of the reference server arithmetic, timed on the
+    host (bounded sample).  1 thread = the reference's one server thread per
+    channel (src/client/clientlib.cpp:102-105)."""
+    import numpy as np
+    from oracle import oracle
+    n = rows * W
+    ups = [oracle.synthetic_delta(c, n) for c in range(clients)]
+    master = np.zeros(n, np.float32)
+    oracle.apply_updates(master, ups)  # warm the pages
+    rounds, t0 = 0, time.perf_counter()
+    while True:
+        oracle.apply_updates(master, ups)
+        rounds += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    per = dt / rounds
+    res = {"value": clients * n * 4 / per / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": f"{rows} rows x {W} fp32, {clients} clients applied sequentially "
+                     f"(oracle_apply_updates, gcc -O3), {rounds} rounds in {dt:.1f} s"}
+    threads = min(16, os.cpu_count() or 1)
+    if threads > 1:
+        t0, r2 = time.perf_counter(), 0
+        while time.perf_counter() - t0 < seconds / 3:
+            oracle.apply_updates(master, ups, threads=threads)
+            r2 += 1
+        per2 = (time.perf_counter() - t0) / r2
+        res["all_cores"] = {"value": clients * n * 4 / per2 / 1e9, "cores": threads,
+                            "note": "row range split over threads = num_comm_channels "
+                                    "server threads (clientlib.cpp:216-224)"}
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+        res["cpu_model"] = model
+        res["nproc"] = os.cpu_count()
+    except OSError:
+        pass
+    return res
+
+
+def load_traffic(workload_key):
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        entry = data.get(workload_key)
+        return None if entry is None else float(entry["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    args = parse()
+    rank, world, dev = init_dist(args.gpus)
+    import geeps_amd
+    from geeps_amd.shard import ShardedReducer
+    geeps_amd.lib()  # the HIP library must be there; no fallback
+
+    R, W, C = args.rows, args.width, args.clients
+    red = ShardedReducer(R, W, C, dev, exchange=args.exchange)
+    L = red.layout
+    log(f"[rank {rank}] shard rows [{L.row_start}, {L.row_start + L.local_rows}) "
+        f"hosting clients {red.hosted}")
+    deltas = make_deltas(red.hosted, R * W, dev)
+    red.push(deltas)  # buckets resident on their shard
+    torch.cuda.synchronize()
+
+    wall, kernel_ms = timed_apply(red, args.steps, args.warmup, world, dev)
+    wall = max_over_ranks(wall, world, dev)
+    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    avg_kernel_ms_max = max_over_ranks(avg_kernel_ms, world, dev)
+    step_s = wall / args.steps
+    delta_bytes = C * R * W * 4
+    value = delta_bytes / step_s / 1e9
+    shard_bytes = L.local_vals * 4
+    algo_bytes = (C + 2) * shard_bytes           # per launch on this rank
+    achieved = algo_bytes / (avg_kernel_ms / 1e3) / 1e9
+    achieved_min = max_over_ranks(-achieved, world, dev) * -1  # slowest rank
+
+    workload_key = f"r{R}_w{W}_c{C}_g{world}"
+    result_exchange = None
+    if world > 1 and args.exchange_steps > 0:
+        ex = timed_exchange(red, deltas, args.exchange_steps, 1, world)
+        ex = max_over_ranks(ex, world, dev) / args.exchange_steps
+        result_exchange = {"ms_per_step": ex * 1e3, "value": delta_bytes / ex / 1e9,
+                           "unit": "GB/s", "exchange": args.exchange,
+                           "note": "RCCL exchange of the buckets + N-way sum + all-gather refresh"}
+
+    host_inc = None
+    cpu = None
+    if rank == 0 and world == 1:
+        del deltas
+        red = None
+        torch.cuda.empty_cache()
+        if not args.no_host_inclusive:
+            log("[rank 0] host-inclusive leg")
+            host_inc = host_inclusive(R // 8, W, C, dev)
+        if not args.no_cpu_baseline:
+            log("[rank 0] cpu baseline leg")
+            cpu = cpu_baseline(min(args.cpu_rows, R), W, C, args.cpu_seconds)
+
+    if rank == 0:
+        traffic = load_traffic(workload_key)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (uniform [-0.5,0.5) deltas, seed 1000+client)",
+            "config": {"workload": f"{C}-way fp32 row reduction into the master table, "
+                                   f"{R} rows x {W} fp32, {world} server shard(s), "
+                                   f"device-resident (BASELINE.json north-star / configs[2])",
+                       "rows": R, "row_width": W, "clients": C, "shards": world,
+                       "exchange": args.exchange if world > 1 else "none (resident)",
+                       "parallelism": f"row-range shards x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_min, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved_min / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel": KERNEL_NAME,
+                         "avg_kernel_ms": round(avg_kernel_ms_max, 4),
+                         "algorithmic_bytes_per_launch": algo_bytes},
+            "hbm_GBps_algorithmic": round((C + 2) * R * W * 4 / step_s / 1e9, 1),
+            "cpu_baseline": cpu,
+        }
+        if result_exchange:
+            line["exchange_inclusive"] = result_exchange
+        if host_inc:
+            line["host_inclusive"] = host_inc
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

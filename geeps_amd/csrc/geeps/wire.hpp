@@ -1,0 +1,73 @@
+#ifndef GEEPS_AMD_WIRE_HPP_
+#define GEEPS_AMD_WIRE_HPP_
+
+// Wire layout of the update push and the shard refresh (the two ends of the
+// reduction path).  Byte-compatible with the reference's
+// src/common/wire-protocol.hpp:42-131 so that frames produced by either side
+// decode on the other: the 24-byte headers, RowKey (16 B) and the Command
+// numbering are identical (checked by tests/test_layout.py).
+//
+// A CLOCK_WITH_UPDATES_BATCH frame is [header][RowKey x n][RowOpVal x n]
+// (src/client/encoder-decoder.cpp:105-150); a READ_ROW_BATCH reply is
+// [sc_read_row_batch_msg_t][RowKey x n][RowData x n]
+// (src/server/server-encoder-decoder.cpp:228-250).
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "geeps-user-defined-types.hpp"
+
+// Clock value of a table nobody has clocked yet, and the largest clock
+// (src/common/internal-config.hpp:34-36).
+#define BIG_ITER 10000000
+#define MAX_CLOCK BIG_ITER
+#define INITIAL_DATA_AGE -BIG_ITER
+
+enum Command {
+  FIND_ROW,
+  READ_ROW_BATCH,
+  CLOCK,
+  CLOCK_WITH_UPDATES_BATCH,
+  ADD_ACCESS_INFO,
+  GET_STATS,
+  SHUTDOWN
+};
+
+struct RowKey {
+  table_id_t table;
+  row_idx_t row;
+  RowKey(table_id_t t = 0, row_idx_t r = 0) : table(t), row(r) {}
+};
+typedef std::vector<RowKey> RowKeys;
+
+// client -> server: one clock's summed deltas for the server's row range.
+struct cs_clock_with_updates_batch_msg_t {
+  command_t cmd;
+  uint32_t client_id;
+  iter_t clock;
+  uint32_t table_id;
+  int update_branch_id;
+  int read_branch_id;
+};
+
+// client -> server: clock with no updates.
+struct cs_clock_msg_t {
+  command_t cmd;
+  uint32_t client_id;
+  iter_t clock;
+  uint32_t table_id;
+  int read_branch_id;
+};
+
+// server -> client: the refreshed shard.
+struct sc_read_row_batch_msg_t {
+  command_t cmd;
+  uint32_t server_id;
+  iter_t data_age;
+  iter_t self_clock;
+  uint32_t table_id;
+  int branch_id;
+};
+
+#endif  // GEEPS_AMD_WIRE_HPP_

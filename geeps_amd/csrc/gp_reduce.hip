@@ -1,0 +1,529 @@
+// gp_reduce.hip — gfx950 (MI355X / CDNA4) kernels of the GeePS gradient-update
+// reduction path, behind the C-ABI declared in include/gp_reduce.h.
+//
+// Two kernel families, both HBM-bandwidth bound (elementwise fp32 add; no
+// MFMA — there is no contraction here):
+//
+//  * bucket_sum_kernel  — the server's N-way sum of client delta buckets into
+//    the master shard (reference: TabletStorage::apply_updates,
+//    src/server/tablet-server.cpp:119-134, applied once per client message).
+//    The reference makes N sequential passes over the shard (3 streams x 4 B
+//    per element per client); here one pass reads master + N buckets once and
+//    writes master once, summing in bucket order so every element is
+//    bit-identical to the sequential form.
+//
+//  * row_op_kernel — the row-indexed scatter-add / gather / scatter-assign
+//    over a DoubleIndex (reference: src/common/row-op-util.cu:39-142).  The
+//    reference launches one thread per ELEMENT with a 64-bit div/mod and a
+//    16-B index load per element; here a group of LPR lanes owns a row, the
+//    row's index is loaded once per row, and each lane moves 16 B per access
+//    (dwordx4), RPG rows per group in flight.
+//
+// Wave64 throughout: 256-thread workgroups = 4 waves, one per SIMD.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "gp_reduce.h"
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;
+// A block-stride grid of this many blocks per CU saturates HBM on 256 CUs
+// while keeping launch cost flat for any problem size.
+constexpr int kBlocksPerCU = 8;
+constexpr int kMaxBucketsPerLaunch = 8;
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define GP_HIP_TRY(expr)                                                    \
+  do {                                                                      \
+    hipError_t e_ = (expr);                                                 \
+    if (e_ != hipSuccess) {                                                 \
+      return set_error(GP_ERR_HIP, std::string(#expr) + ": " +             \
+                                       hipGetErrorString(e_));             \
+    }                                                                       \
+  } while (0)
+
+int g_num_cus = 0;
+
+int num_cus() {
+  // Cached per process (the device's CU count never changes); a race here is
+  // benign (both writers store the same value).
+  if (g_num_cus == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                              dev) != hipSuccess ||
+        cus <= 0) {
+      cus = 256;
+    }
+    g_num_cus = cus;
+  }
+  return g_num_cus;
+}
+
+size_t grid_cap() { return (size_t)num_cus() * kBlocksPerCU; }
+
+inline bool aligned16(const void *p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+// ---------------------------------------------------------------------------
+// N-way bucket sum: out[i] = ((in[i] + b0[i]) + b1[i]) + ... + b{NB-1}[i]
+// ---------------------------------------------------------------------------
+
+struct BucketPtrs {
+  const float *p[kMaxBucketsPerLaunch];
+};
+
+__device__ __forceinline__ f4 ld_stream(const f4 *p) {
+  // Each bucket byte is read exactly once: non-temporal keeps the stream
+  // from evicting anything useful from L2 / Infinity Cache.
+  return __builtin_nontemporal_load(p);
+}
+
+// UNROLL consecutive block-strides per thread: (NB + 1) * UNROLL independent
+// 16-B loads are in flight per lane before the first add.
+template <int NB, int UNROLL>
+__global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
+    f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4) {
+  const size_t tile = (size_t)kBlock * UNROLL;
+  const size_t stride = (size_t)gridDim.x * tile;
+  const f4 *bp[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) bp[k] = reinterpret_cast<const f4 *>(b.p[k]);
+
+  size_t base = (size_t)blockIdx.x * tile + threadIdx.x;
+  // Full tiles: no bounds checks inside.
+  for (; base + (UNROLL - 1) * kBlock < n4; base += stride) {
+    f4 acc[UNROLL];
+    f4 v[NB][UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) acc[u] = in[base + u * kBlock];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) v[k][u] = ld_stream(bp[k] + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc[u] += v[k][u];  // bucket order 0..NB-1
+      out[base + u * kBlock] = acc[u];
+    }
+  }
+  // Ragged last tile.
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const size_t i = base + u * kBlock;
+    if (i < n4) {
+      f4 acc = in[i];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc += ld_stream(bp[k] + i);
+      out[i] = acc;
+    }
+  }
+}
+
+// Scalar form: unaligned pointers and the < 4-float tail.
+template <int NB>
+__global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
+    float *__restrict__ out, const float *__restrict__ in, BucketPtrs b,
+    size_t n) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    float acc = in[i];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) acc += b.p[k][i];
+    out[i] = acc;
+  }
+}
+
+template <int NB>
+int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
+                         size_t n, hipStream_t s) {
+  bool vec = aligned16(out) && aligned16(in);
+  for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
+  size_t done = 0;
+  if (vec && n >= 4) {
+    constexpr int U = NB <= 2 ? 4 : (NB <= 5 ? 2 : 1);
+    const size_t n4 = n / 4;
+    const size_t tiles = (n4 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
+    const size_t grid = tiles < grid_cap() ? tiles : grid_cap();
+    hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out),
+                       reinterpret_cast<const f4 *>(in), b, n4);
+    done = n4 * 4;
+  }
+  if (done < n) {
+    BucketPtrs t;
+    for (int k = 0; k < NB; ++k) t.p[k] = b.p[k] + done;
+    const size_t rem = n - done;
+    size_t grid = (rem + kBlock - 1) / kBlock;
+    if (grid > grid_cap()) grid = grid_cap();
+    hipLaunchKernelGGL((bucket_sum_scalar_kernel<NB>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, out + done, in + done, t, rem);
+  }
+  GP_HIP_TRY(hipGetLastError());
+  return GP_OK;
+}
+
+int launch_bucket_sum(float *out, const float *in, const float *const *bk,
+                      int nb, size_t n, hipStream_t s) {
+  BucketPtrs b = {};
+  for (int k = 0; k < nb; ++k) b.p[k] = bk[k];
+  switch (nb) {
+    case 1: return launch_bucket_sum_nb<1>(out, in, b, n, s);
+    case 2: return launch_bucket_sum_nb<2>(out, in, b, n, s);
+    case 3: return launch_bucket_sum_nb<3>(out, in, b, n, s);
+    case 4: return launch_bucket_sum_nb<4>(out, in, b, n, s);
+    case 5: return launch_bucket_sum_nb<5>(out, in, b, n, s);
+    case 6: return launch_bucket_sum_nb<6>(out, in, b, n, s);
+    case 7: return launch_bucket_sum_nb<7>(out, in, b, n, s);
+    case 8: return launch_bucket_sum_nb<8>(out, in, b, n, s);
+    default: return set_error(GP_ERR_INVALID, "bucket count out of range");
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row-indexed ops over a DoubleIndex.
+// ---------------------------------------------------------------------------
+
+enum RowOp : int {
+  kAddFrom = 0,     // y[id1] += x[id0], guard on the x index
+  kAssignTo = 1,    // y[id0]  = x[id1], guard on the y index
+  kAssignFrom = 2,  // y[id1]  = x[id0], guard on the x index
+};
+
+template <int OP>
+__device__ __forceinline__ void row_endpoints(const gp_double_index &ix,
+                                              uint64_t off0, uint64_t off1,
+                                              uint64_t &from, uint64_t &to) {
+  if (OP == kAssignTo) {
+    from = ix.id1 + off1;
+    to = ix.id0 + off0;
+  } else {
+    from = ix.id0 + off0;
+    to = ix.id1 + off1;
+  }
+}
+
+// T = f4 (VEC 4) or float (VEC 1).  A group of LPR consecutive lanes owns a
+// row; each group handles RPG rows per iteration, all their loads issued
+// before the first store.  `vw` = row_size / VEC (vectors per row).
+template <typename T, int VEC, int OP, int LPR, int RPG>
+__global__ __launch_bounds__(kBlock) void row_op_kernel(
+    float *__restrict__ y, const float *__restrict__ x,
+    const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
+    uint64_t off1, size_t row_size, size_t vw, size_t limit) {
+  constexpr int kGroups = kBlock / LPR;
+  const int lane = threadIdx.x % LPR;
+  const size_t group = (size_t)blockIdx.x * kGroups + threadIdx.x / LPR;
+  const size_t gstride = (size_t)gridDim.x * kGroups * RPG;
+  T *yv = reinterpret_cast<T *>(y);
+  const T *xv = reinterpret_cast<const T *>(x);
+
+  for (size_t r0 = group * RPG; r0 < num_rows; r0 += gstride) {
+    uint64_t from[RPG], to[RPG];
+    bool live[RPG], whole[RPG];
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+      const size_t r = r0 + k;
+      live[k] = r < num_rows;
+      from[k] = to[k] = 0;
+      whole[k] = false;
+      if (live[k]) {
+        const gp_double_index ix = index[r];
+        row_endpoints<OP>(ix, off0, off1, from[k], to[k]);
+        const uint64_t guarded = (OP == kAssignTo) ? to[k] : from[k];
+        whole[k] = (guarded + 1) * row_size <= limit;
+      }
+    }
+    bool all_whole = true;
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) all_whole = all_whole && (whole[k] || !live[k]);
+
+    if (all_whole) {
+      for (size_t j = lane; j < vw; j += LPR) {
+        T xs[RPG], ys[RPG];
+#pragma unroll
+        for (int k = 0; k < RPG; ++k)
+          if (live[k]) xs[k] = xv[from[k] * vw + j];
+        if (OP == kAddFrom) {
+#pragma unroll
+          for (int k = 0; k < RPG; ++k)
+            if (live[k]) ys[k] = yv[to[k] * vw + j];
+        }
+#pragma unroll
+        for (int k = 0; k < RPG; ++k) {
+          if (live[k]) {
+            if (OP == kAddFrom)
+              yv[to[k] * vw + j] = ys[k] + xs[k];
+            else
+              yv[to[k] * vw + j] = xs[k];
+          }
+        }
+      }
+    } else {
+      // Rows straddling num_vals_limit: element-wise guard, scalar accesses
+      // (nothing past the limit is touched, as in the reference).
+#pragma unroll 1
+      for (int k = 0; k < RPG; ++k) {
+        if (!live[k]) continue;
+        const uint64_t guarded = (OP == kAssignTo) ? to[k] : from[k];
+        for (size_t e = lane; e < row_size; e += LPR) {
+          if (guarded * row_size + e < limit) {
+            const float xv1 = x[from[k] * row_size + e];
+            if (OP == kAddFrom)
+              y[to[k] * row_size + e] += xv1;
+            else
+              y[to[k] * row_size + e] = xv1;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int VEC, int OP, int LPR>
+void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
+                       size_t n, uint64_t off0, uint64_t off1, size_t row_size,
+                       size_t limit, hipStream_t s) {
+  // Keep ~8 independent 16-B loads per lane in flight.
+  constexpr int RPG = (OP == kAddFrom) ? 4 : 8;
+  constexpr int kGroups = kBlock / LPR;
+  const size_t groups = (n + RPG - 1) / RPG;
+  size_t grid = (groups + kGroups - 1) / kGroups;
+  if (grid > grid_cap()) grid = grid_cap();
+  hipLaunchKernelGGL((row_op_kernel<T, VEC, OP, LPR, RPG>), dim3((unsigned)grid),
+                     dim3(kBlock), 0, s, y, x, idx, n, off0, off1, row_size,
+                     row_size / VEC, limit);
+}
+
+template <typename T, int VEC, int OP>
+void launch_row_op_t(float *y, const float *x, const gp_double_index *idx,
+                     size_t n, uint64_t off0, uint64_t off1, size_t row_size,
+                     size_t limit, hipStream_t s) {
+  const size_t vw = row_size / VEC;
+  // Lanes per row: the smallest power of two covering the row, capped at a
+  // wave; short rows (64 / 128 floats) pack 4 / 2 rows into one wave.
+  if (vw <= 1)
+    launch_row_op_lpr<T, VEC, OP, 1>(y, x, idx, n, off0, off1, row_size, limit, s);
+  else if (vw <= 2)
+    launch_row_op_lpr<T, VEC, OP, 2>(y, x, idx, n, off0, off1, row_size, limit, s);
+  else if (vw <= 4)
+    launch_row_op_lpr<T, VEC, OP, 4>(y, x, idx, n, off0, off1, row_size, limit, s);
+  else if (vw <= 8)
+    launch_row_op_lpr<T, VEC, OP, 8>(y, x, idx, n, off0, off1, row_size, limit, s);
+  else if (vw <= 16)
+    launch_row_op_lpr<T, VEC, OP, 16>(y, x, idx, n, off0, off1, row_size, limit, s);
+  else if (vw <= 32)
+    launch_row_op_lpr<T, VEC, OP, 32>(y, x, idx, n, off0, off1, row_size, limit, s);
+  else
+    launch_row_op_lpr<T, VEC, OP, 64>(y, x, idx, n, off0, off1, row_size, limit, s);
+}
+
+template <int OP>
+int launch_row_op(float *y, const float *x, const gp_double_index *idx,
+                  size_t n, gp_double_index off, size_t row_size, size_t limit,
+                  hipStream_t s) {
+  if (n == 0) return GP_OK;
+  if (!y || !x || !idx) return set_error(GP_ERR_INVALID, "null pointer");
+  if (row_size == 0) return set_error(GP_ERR_INVALID, "row_size == 0");
+  if (row_size % 4 == 0 && aligned16(y) && aligned16(x))
+    launch_row_op_t<f4, 4, OP>(y, x, idx, n, off.id0, off.id1, row_size, limit, s);
+  else
+    launch_row_op_t<float, 1, OP>(y, x, idx, n, off.id0, off.id1, row_size, limit, s);
+  GP_HIP_TRY(hipGetLastError());
+  return GP_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int gp_abi_version(void) { return GP_ABI_VERSION; }
+
+const char *gp_last_error(void) { return g_last_error.c_str(); }
+
+int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
+                        size_t num_rows, gp_double_index offset,
+                        size_t row_size, size_t num_vals_limit, gp_stream s) {
+  return launch_row_op<kAddFrom>(y, x, index, num_rows, offset, row_size,
+                                 num_vals_limit, (hipStream_t)s);
+}
+
+int gp_gather_rows(float *y, const float *x, const gp_double_index *index,
+                   size_t num_rows, gp_double_index offset, size_t row_size,
+                   size_t num_vals_limit, gp_stream s) {
+  return launch_row_op<kAssignTo>(y, x, index, num_rows, offset, row_size,
+                                  num_vals_limit, (hipStream_t)s);
+}
+
+int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
+                    size_t num_rows, gp_double_index offset, size_t row_size,
+                    size_t num_vals_limit, gp_stream s) {
+  return launch_row_op<kAssignFrom>(y, x, index, num_rows, offset, row_size,
+                                    num_vals_limit, (hipStream_t)s);
+}
+
+int gp_bucket_sum_apply(float *master, const float *const *buckets,
+                        int num_buckets, size_t num_vals, gp_stream s) {
+  if (num_buckets == 0 || num_vals == 0) return GP_OK;
+  if (num_buckets < 0) return set_error(GP_ERR_INVALID, "num_buckets < 0");
+  if (!master || !buckets) return set_error(GP_ERR_INVALID, "null pointer");
+  for (int k = 0; k < num_buckets; ++k)
+    if (!buckets[k]) return set_error(GP_ERR_INVALID, "null bucket pointer");
+  // More than kMaxBucketsPerLaunch buckets: consecutive launches over the
+  // same master, each continuing the bucket order where the last stopped.
+  for (int k0 = 0; k0 < num_buckets; k0 += kMaxBucketsPerLaunch) {
+    const int nb = num_buckets - k0 < kMaxBucketsPerLaunch
+                       ? num_buckets - k0
+                       : kMaxBucketsPerLaunch;
+    const int rc = launch_bucket_sum(master, master, buckets + k0, nb,
+                                     num_vals, (hipStream_t)s);
+    if (rc != GP_OK) return rc;
+  }
+  return GP_OK;
+}
+
+int gp_add(size_t n, const float *a, const float *b, float *y, gp_stream s) {
+  if (n == 0) return GP_OK;
+  if (!a || !b || !y) return set_error(GP_ERR_INVALID, "null pointer");
+  const float *bk[1] = {b};
+  return launch_bucket_sum(y, a, bk, 1, n, (hipStream_t)s);
+}
+
+int gp_zero(float *y, size_t num_vals, gp_stream s) {
+  if (num_vals == 0) return GP_OK;
+  if (!y) return set_error(GP_ERR_INVALID, "null pointer");
+  GP_HIP_TRY(hipMemsetAsync(y, 0, num_vals * sizeof(float), (hipStream_t)s));
+  return GP_OK;
+}
+
+// ---- runtime helpers -------------------------------------------------------
+
+int gp_device_count(int *count) {
+  if (!count) return set_error(GP_ERR_INVALID, "null pointer");
+  GP_HIP_TRY(hipGetDeviceCount(count));
+  return GP_OK;
+}
+
+int gp_set_device(int device) {
+  GP_HIP_TRY(hipSetDevice(device));
+  g_num_cus = 0;
+  return GP_OK;
+}
+
+int gp_get_device(int *device) {
+  if (!device) return set_error(GP_ERR_INVALID, "null pointer");
+  GP_HIP_TRY(hipGetDevice(device));
+  return GP_OK;
+}
+
+int gp_malloc_device(void **ptr, size_t bytes) {
+  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
+  *ptr = nullptr;
+  if (bytes == 0) return GP_OK;
+  GP_HIP_TRY(hipMalloc(ptr, bytes));
+  return GP_OK;
+}
+
+int gp_free_device(void *ptr) {
+  if (ptr) GP_HIP_TRY(hipFree(ptr));
+  return GP_OK;
+}
+
+int gp_malloc_host(void **ptr, size_t bytes) {
+  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
+  *ptr = nullptr;
+  if (bytes == 0) return GP_OK;
+  GP_HIP_TRY(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
+  return GP_OK;
+}
+
+int gp_free_host(void *ptr) {
+  if (ptr) GP_HIP_TRY(hipHostFree(ptr));
+  return GP_OK;
+}
+
+int gp_memcpy_async(void *dst, const void *src, size_t bytes, gp_stream s) {
+  if (bytes == 0) return GP_OK;
+  if (!dst || !src) return set_error(GP_ERR_INVALID, "null pointer");
+  GP_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)s));
+  return GP_OK;
+}
+
+int gp_memset_async(void *dst, int value, size_t bytes, gp_stream s) {
+  if (bytes == 0) return GP_OK;
+  if (!dst) return set_error(GP_ERR_INVALID, "null pointer");
+  GP_HIP_TRY(hipMemsetAsync(dst, value, bytes, (hipStream_t)s));
+  return GP_OK;
+}
+
+int gp_stream_create(gp_stream *s) {
+  if (!s) return set_error(GP_ERR_INVALID, "null pointer");
+  hipStream_t st = nullptr;
+  GP_HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  *s = (gp_stream)st;
+  return GP_OK;
+}
+
+int gp_stream_destroy(gp_stream s) {
+  if (s) GP_HIP_TRY(hipStreamDestroy((hipStream_t)s));
+  return GP_OK;
+}
+
+int gp_stream_synchronize(gp_stream s) {
+  GP_HIP_TRY(hipStreamSynchronize((hipStream_t)s));
+  return GP_OK;
+}
+
+int gp_device_synchronize(void) {
+  GP_HIP_TRY(hipDeviceSynchronize());
+  return GP_OK;
+}
+
+int gp_event_create(gp_event *e) {
+  if (!e) return set_error(GP_ERR_INVALID, "null pointer");
+  hipEvent_t ev = nullptr;
+  GP_HIP_TRY(hipEventCreate(&ev));
+  *e = (gp_event)ev;
+  return GP_OK;
+}
+
+int gp_event_destroy(gp_event e) {
+  if (e) GP_HIP_TRY(hipEventDestroy((hipEvent_t)e));
+  return GP_OK;
+}
+
+int gp_event_record(gp_event e, gp_stream s) {
+  GP_HIP_TRY(hipEventRecord((hipEvent_t)e, (hipStream_t)s));
+  return GP_OK;
+}
+
+int gp_event_synchronize(gp_event e) {
+  GP_HIP_TRY(hipEventSynchronize((hipEvent_t)e));
+  return GP_OK;
+}
+
+int gp_event_elapsed_ms(float *ms, gp_event start, gp_event stop) {
+  if (!ms) return set_error(GP_ERR_INVALID, "null pointer");
+  GP_HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+  return GP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,199 @@
+"""Row operations and the server's N-way sum on device tensors.
+
+Host-side mirror of the reference's row-op interface, same names and argument
+meaning, each call one C-ABI launch (include/gp_reduce.h) on the caller's
+current HIP stream:
+
+=================================  ===============================================
+this module                        reference
+=================================  ===============================================
+add_rows_from_double_index_gpu     src/common/row-op-util.hpp:151-155 / .cu:109-142
+assign_rows_to_double_index_gpu    src/common/row-op-util.hpp:141-145 / .cu:39-72
+assign_rows_from_double_index_gpu  src/common/row-op-util.hpp:146-150 / .cu:74-107
+add_row_batch_gpu                  src/common/row-op-util.hpp:72-79 (y += x)
+gpu_add                            cpu_add, src/common/gpu-util/math_functions.hpp:60-61
+zerofy_data_gpu                    DataStorage::zerofy_data_gpu, common-util.hpp:445-456
+apply_updates                      TabletStorage::apply_updates x N in arrival order,
+                                   src/server/tablet-server.cpp:119-134
+=================================  ===============================================
+
+Differences from the reference (deliberate, documented in DESIGN.md): launches
+are asynchronous (the reference syncs after each, row-op-util.cu:141); sizes are
+64-bit; errors raise ``GpError`` instead of aborting.
+
+Tensors: values are float32 CUDA tensors addressed as flat arrays of
+``row_size``-float rows; a DoubleIndex is an int64 CUDA tensor of shape (n, 2)
+holding (id0, id1) per row.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from . import native
+from .native import DoubleIndex, check
+
+ROW_DATA_SIZE = 128  # include/geeps-user-defined-types.hpp
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def _dev_f32(t: torch.Tensor, name: str) -> None:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA (HIP) tensor")
+    if t.dtype != torch.float32:
+        raise ValueError(f"{name} must be float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _as_offset(off) -> DoubleIndex:
+    if off is None:
+        return DoubleIndex(0, 0)
+    if isinstance(off, DoubleIndex):
+        return off
+    a, b = off
+    return DoubleIndex(int(a), int(b))
+
+
+def _row_op(kind: str, rows_y, rows_x, index, num_rows, index_offset, row_size,
+            num_vals_limit, stream, validate) -> None:
+    _dev_f32(rows_y, "rows_y")
+    _dev_f32(rows_x, "rows_x")
+    if num_rows is None:
+        num_rows = 0 if index is None else int(index.shape[0])
+    if num_rows == 0:
+        return
+    if not (index.is_cuda and index.dtype == torch.int64 and index.dim() == 2
+            and index.shape[1] == 2 and index.is_contiguous()):
+        raise ValueError("index must be a contiguous int64 CUDA tensor of shape (n, 2)")
+    if num_rows > index.shape[0]:
+        raise ValueError("num_rows exceeds index length")
+    if row_size <= 0:
+        raise ValueError("row_size must be positive")
+    off = _as_offset(index_offset)
+    if num_vals_limit is None:
+        num_vals_limit = (1 << 64) - 1
+    if validate:
+        _validate_bounds(kind, rows_y, rows_x, index[:num_rows], off, row_size, num_vals_limit)
+    fn = {"add_from": native.lib().gp_scatter_add_rows,
+          "assign_to": native.lib().gp_gather_rows,
+          "assign_from": native.lib().gp_scatter_rows}[kind]
+    check(fn(rows_y.data_ptr(), rows_x.data_ptr(), index.data_ptr(), num_rows, off,
+             row_size, num_vals_limit, _stream_ptr(stream)), f"gp row op {kind}")
+
+
+def _validate_bounds(kind, y, x, index, off, row_size, limit) -> None:
+    """Host-side check that every access the kernel will make is in bounds.
+
+    Mirrors the reference guard: rows whose guarded element index is past
+    ``num_vals_limit`` are skipped element-wise, so only guarded-in elements
+    are checked.  One device reduction + one sync.
+    """
+    if index.numel() == 0:
+        return
+    if int(index.min()) < 0:
+        raise ValueError("negative row id in DoubleIndex")
+    r0 = index[:, 0] + off.id0
+    r1 = index[:, 1] + off.id1
+    if kind == "assign_to":      # from = id1 (x), to = id0 (y), guard on y
+        x_rows, y_rows, guarded = r1, r0, r0
+    else:                        # from = id0 (x), to = id1 (y), guard on x
+        x_rows, y_rows, guarded = r0, r1, r0
+    if limit < (1 << 62):
+        active = guarded * row_size < limit   # row touches >= 1 element
+        if not bool(active.any()):
+            return
+        x_rows, y_rows = x_rows[active], y_rows[active]
+    x_max, y_max = int(x_rows.max()), int(y_rows.max())
+    x_need, y_need = (x_max + 1) * row_size, (y_max + 1) * row_size
+    # The guarded side is touched only below the limit.
+    if kind == "assign_to":
+        y_need = min(y_need, limit)
+    else:
+        x_need = min(x_need, limit)
+    if x_need > x.numel():
+        raise ValueError(f"source row {x_max} out of range for rows_x")
+    if y_need > y.numel():
+        raise ValueError(f"destination row {y_max} out of range for rows_y")
+
+
+def add_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, index_offset=None,
+                                   row_size=ROW_DATA_SIZE, num_vals_limit=None,
+                                   stream=None, validate=True) -> None:
+    """``y[(id1+off1)*W + v] += x[(id0+off0)*W + v]`` where ``(id0+off0)*W+v < limit``.
+
+    The client delta accumulate (reference row-op-util.cu:109-142).  Destination
+    rows must be distinct within one call (as for the reference kernel).
+    """
+    _row_op("add_from", rows_y, rows_x, index, num_rows, index_offset, row_size,
+            num_vals_limit, stream, validate)
+
+
+def assign_rows_to_double_index_gpu(rows_y, rows_x, index, num_rows=None, index_offset=None,
+                                    row_size=ROW_DATA_SIZE, num_vals_limit=None,
+                                    stream=None, validate=True) -> None:
+    """``y[(id0+off0)*W + v] = x[(id1+off1)*W + v]`` where ``(id0+off0)*W+v < limit``."""
+    _row_op("assign_to", rows_y, rows_x, index, num_rows, index_offset, row_size,
+            num_vals_limit, stream, validate)
+
+
+def assign_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, index_offset=None,
+                                      row_size=ROW_DATA_SIZE, num_vals_limit=None,
+                                      stream=None, validate=True) -> None:
+    """``y[(id1+off1)*W + v] = x[(id0+off0)*W + v]`` where ``(id0+off0)*W+v < limit``."""
+    _row_op("assign_from", rows_y, rows_x, index, num_rows, index_offset, row_size,
+            num_vals_limit, stream, validate)
+
+
+def bucket_sum_apply(master: torch.Tensor, buckets: Sequence[torch.Tensor],
+                     num_vals: int | None = None, stream=None) -> None:
+    """``master += b[0]; master += b[1]; ...`` in one pass, bit-identical to the
+    sequential form (tablet-server.cpp:119-134 once per client, in order)."""
+    _dev_f32(master, "master")
+    n = master.numel() if num_vals is None else int(num_vals)
+    if n > master.numel():
+        raise ValueError("num_vals exceeds master size")
+    ptrs = (ctypes.c_void_p * max(1, len(buckets)))()
+    for k, b in enumerate(buckets):
+        _dev_f32(b, f"buckets[{k}]")
+        if b.numel() < n:
+            raise ValueError(f"buckets[{k}] smaller than num_vals")
+        if b.device != master.device:
+            raise ValueError("bucket on a different device than master")
+        ptrs[k] = b.data_ptr()
+    check(native.lib().gp_bucket_sum_apply(master.data_ptr(), ptrs, len(buckets), n,
+                                           _stream_ptr(stream)), "gp_bucket_sum_apply")
+
+
+def apply_updates(master: torch.Tensor, updates: Sequence[torch.Tensor], stream=None) -> None:
+    """The server's N-way sum: the reference's per-message ``apply_updates`` for
+    each update in arrival order, as one device pass."""
+    bucket_sum_apply(master, updates, stream=stream)
+
+
+def gpu_add(n: int, a: torch.Tensor, b: torch.Tensor, y: torch.Tensor, stream=None) -> None:
+    """``y[i] = a[i] + b[i]`` for i < n (cpu_add / vsAdd on the device)."""
+    for t, nm in ((a, "a"), (b, "b"), (y, "y")):
+        _dev_f32(t, nm)
+        if t.numel() < n:
+            raise ValueError(f"{nm} smaller than n")
+    check(native.lib().gp_add(int(n), a.data_ptr(), b.data_ptr(), y.data_ptr(),
+                              _stream_ptr(stream)), "gp_add")
+
+
+def add_row_batch_gpu(rows_y: torch.Tensor, rows_x: torch.Tensor, batch_size: int,
+                      row_size: int = ROW_DATA_SIZE, stream=None) -> None:
+    """``y += x`` over ``batch_size`` rows (reference row-op-util.hpp:72-79)."""
+    gpu_add(batch_size * row_size, rows_y, rows_x, rows_y, stream)
+
+
+def zerofy_data_gpu(t: torch.Tensor, stream=None) -> None:
+    _dev_f32(t, "t")
+    check(native.lib().gp_zero(t.data_ptr(), t.numel(), _stream_ptr(stream)), "gp_zero")

@@ -1,0 +1,159 @@
+/*
+ * gp_reduce.h — C-ABI of the MI355X (gfx950) gradient-update reduction path.
+ *
+ * This is the thin boundary between host code (the C++ libgeeps in
+ * geeps_amd/csrc/geeps, the Python test/bench harness through ctypes) and the
+ * hand-written HIP kernels in geeps_amd/csrc/gp_reduce.hip.  Plain pointers and
+ * sizes only; no HIP, torch or C++ types cross it.
+ *
+ * Every entry point replaces one reference function (GeePS, cuihenggang/geeps);
+ * the reference file:line is cited next to it.  Argument meaning follows the
+ * reference exactly (same index semantics, same `num_vals_limit` guard, same
+ * summation order).  Differences that are deliberate:
+ *   - sizes are 64-bit throughout (the reference's `int n` / `int i` grid-stride
+ *     loops overflow past 2^31 elements: src/common/gpu-util/mkl_alternate.hpp:62,
+ *     src/common/gpu-util/device_alternate.hpp:31-54);
+ *   - calls are asynchronous on the given stream (the reference synchronises
+ *     after every launch: src/common/row-op-util.cu:141); the caller syncs;
+ *   - errors are returned as a status code (0 = GP_OK) with a thread-local
+ *     message from gp_last_error(), instead of a glog FATAL abort
+ *     (src/common/gpu-util/device_alternate.hpp:16-28).  The C++ layer above
+ *     turns a non-zero status into an abort with that message.
+ *
+ * All functions are re-entrant and keep no global state besides the
+ * thread-local error string.
+ */
+#ifndef GP_REDUCE_H_
+#define GP_REDUCE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes. */
+#define GP_OK 0
+#define GP_ERR_INVALID 1   /* bad argument (null pointer, zero row size ...) */
+#define GP_ERR_HIP 2       /* a HIP runtime call failed */
+#define GP_ERR_UNSUPPORTED 3
+
+/* Library ABI version; bumped on any signature change. */
+#define GP_ABI_VERSION 1
+
+/* {id0, id1} pair, 16 bytes, identical layout to the reference's
+ * `struct DoubleIndex { size_t id0; size_t id1; }`
+ * (src/common/row-op-util.hpp:40-44).  id0 = row position in the app's op
+ * buffer, id1 = row in the process/param cache
+ * (src/client/clientlib-viter.cpp:841). */
+typedef struct gp_double_index {
+  uint64_t id0;
+  uint64_t id1;
+} gp_double_index;
+
+/* An opaque hipStream_t.  NULL = the device's null stream. */
+typedef void *gp_stream;
+/* An opaque hipEvent_t. */
+typedef void *gp_event;
+
+int gp_abi_version(void);
+const char *gp_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Row operations (client side).  Element (row r, value v) lives at
+ * base[r * row_size + v].  `row_size` is a runtime argument (the public API
+ * fixes it at 128 floats, ROW_DATA_SIZE in geeps-user-defined-types.hpp:54).
+ * ------------------------------------------------------------------------- */
+
+/* Row-indexed scatter-add (the client delta accumulate):
+ *   for r in [0, num_rows), v in [0, row_size):
+ *     from = index[r].id0 + offset.id0;  to = index[r].id1 + offset.id1;
+ *     if (from*row_size + v < num_vals_limit)
+ *       y[to*row_size + v] += x[from*row_size + v];
+ * Replaces add_rows_from_double_index_gpu (src/common/row-op-util.hpp:151-155,
+ * src/common/row-op-util.cu:109-142); CPU twin add_rows_from_double_index_cpu
+ * (src/common/row-op-util.hpp:121-139).
+ * Precondition (as for the reference kernel, whose threads race on a repeated
+ * destination): destination rows index[r].id1 are distinct within one call.
+ * `index` is a DEVICE pointer.  num_rows == 0 is a no-op. */
+int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
+                        size_t num_rows, gp_double_index offset,
+                        size_t row_size, size_t num_vals_limit, gp_stream s);
+
+/* Row-indexed gather (the Read path, refresh leg):
+ *     from = index[r].id1 + offset.id1;  to = index[r].id0 + offset.id0;
+ *     if (to*row_size + v < num_vals_limit)
+ *       y[to*row_size + v] = x[from*row_size + v];
+ * Replaces assign_rows_to_double_index_gpu (src/common/row-op-util.hpp:141-145,
+ * src/common/row-op-util.cu:39-72); CPU twin :81-99. */
+int gp_gather_rows(float *y, const float *x, const gp_double_index *index,
+                   size_t num_rows, gp_double_index offset, size_t row_size,
+                   size_t num_vals_limit, gp_stream s);
+
+/* Row-indexed scatter-assign:
+ *     from = index[r].id0 + offset.id0;  to = index[r].id1 + offset.id1;
+ *     if (from*row_size + v < num_vals_limit)
+ *       y[to*row_size + v] = x[from*row_size + v];
+ * Replaces assign_rows_from_double_index_gpu (src/common/row-op-util.hpp:146-150,
+ * src/common/row-op-util.cu:74-107; no callers in the reference). */
+int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
+                    size_t num_rows, gp_double_index offset, size_t row_size,
+                    size_t num_vals_limit, gp_stream s);
+
+/* ---------------------------------------------------------------------------
+ * Dense reductions (server side).
+ * ------------------------------------------------------------------------- */
+
+/* N-way bucket sum applied to the master shard, in bucket order:
+ *     for i in [0, num_vals):
+ *       master[i] = (((master[i] + b[0][i]) + b[1][i]) + ...) + b[N-1][i]
+ * which is bit-identical to the reference server applying N client messages
+ * in arrival order 0..N-1, each one `cpu_add(n, master, update, master)`
+ * (TabletStorage::apply_updates, src/server/tablet-server.cpp:119-134 ->
+ * cpu_add<float>, src/common/gpu-util/math_functions.cpp:132-136 -> vsAdd,
+ * src/common/gpu-util/mkl_alternate.hpp:59-74).
+ * `buckets` is a HOST array of `num_buckets` DEVICE pointers.
+ * num_buckets == 0 or num_vals == 0 is a no-op.  One launch reads every
+ * byte once: (N + 1) * num_vals * 4 B read, num_vals * 4 B written. */
+int gp_bucket_sum_apply(float *master, const float *const *buckets,
+                        int num_buckets, size_t num_vals, gp_stream s);
+
+/* y[i] = a[i] + b[i] — device form of cpu_add / vsAdd
+ * (src/common/gpu-util/math_functions.hpp:60-61, mkl_alternate.hpp:59-74).
+ * Also covers add_row_batch_gpu's `y += x` (cublasSaxpy with alpha 1,
+ * src/common/row-op-util.hpp:72-79) as gp_add(n, y, x, y). In-place allowed. */
+int gp_add(size_t n, const float *a, const float *b, float *y, gp_stream s);
+
+/* Zero `num_vals` floats — DataStorage::zerofy_data_gpu
+ * (src/common/common-util.hpp:445-456). */
+int gp_zero(float *y, size_t num_vals, gp_stream s);
+
+/* ---------------------------------------------------------------------------
+ * Runtime helpers, so host C++ never names a HIP type.
+ * ------------------------------------------------------------------------- */
+int gp_device_count(int *count);
+int gp_set_device(int device);
+int gp_get_device(int *device);
+int gp_malloc_device(void **ptr, size_t bytes);
+int gp_free_device(void *ptr);
+int gp_malloc_host(void **ptr, size_t bytes); /* pinned (mallocHost) */
+int gp_free_host(void *ptr);
+/* Direction inferred from the pointers (cudaMemcpyDefault in the reference). */
+int gp_memcpy_async(void *dst, const void *src, size_t bytes, gp_stream s);
+int gp_memset_async(void *dst, int value, size_t bytes, gp_stream s);
+int gp_stream_create(gp_stream *s);      /* non-blocking stream */
+int gp_stream_destroy(gp_stream s);
+int gp_stream_synchronize(gp_stream s);
+int gp_device_synchronize(void);
+int gp_event_create(gp_event *e);
+int gp_event_destroy(gp_event e);
+int gp_event_record(gp_event e, gp_stream s);
+int gp_event_synchronize(gp_event e);
+int gp_event_elapsed_ms(float *ms, gp_event start, gp_event stop);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* GP_REDUCE_H_ */

@@ -1,0 +1,39 @@
+"""Worker bodies for the multi-process (gloo, CPU) tests of geeps_amd.shard.
+
+The exchange / partition / refresh logic runs exactly as on the GPU; only the
+apply step is swapped for the CPU oracle (the HIP kernel needs a device), which
+is test infrastructure standing in for the kernel under test elsewhere.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def oracle_apply(master: torch.Tensor, buckets) -> None:
+    from oracle import oracle
+    m = master.numpy()
+    oracle.apply_updates(m, [b.contiguous().numpy() for b in buckets])
+
+
+def full_delta(c: int, num_rows: int, W: int) -> torch.Tensor:
+    from oracle import oracle
+    return torch.from_numpy(oracle.synthetic_delta(c, num_rows * W))
+
+
+def run_shard(rank, world, port, num_rows, W, num_clients, exchange, steps, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geeps_amd.shard import ShardedReducer
+        red = ShardedReducer(num_rows, W, num_clients, device="cpu", exchange=exchange,
+                             apply_fn=oracle_apply)
+        for step in range(steps):
+            deltas = [full_delta(c + 100 * step, num_rows, W) for c in red.hosted]
+            table = red.step(deltas)
+        np.save(os.path.join(out_dir, f"table_{rank}.npy"), table.numpy()[:num_rows * W])
+        np.save(os.path.join(out_dir, f"hosted_{rank}.npy"), np.array(red.hosted))
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,73 @@
+"""The C-ABI library loads and exports every symbol include/gp_reduce.h declares
+(no compute calls: runs without a GPU)."""
+import ctypes
+import os
+import subprocess
+
+from conftest import REPO
+
+from geeps_amd import native
+
+
+def test_header_declares_expected_entry_points():
+    syms = native.declared_symbols()
+    for s in ("gp_scatter_add_rows", "gp_gather_rows", "gp_scatter_rows",
+              "gp_bucket_sum_apply", "gp_add", "gp_zero", "gp_last_error"):
+        assert s in syms
+    # every declared symbol has a ctypes signature and vice versa
+    assert set(syms) == set(native._SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(native.LIB_PATH), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], check=True,
+                         capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [s for s in native.declared_symbols() if s not in exported]
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_abi():
+    L = native.lib()
+    assert L.gp_abi_version() == 1
+    assert isinstance(L.gp_last_error(), bytes)
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", native.LIB_PATH],
+                         capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in out
+    blob = open(native.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_invalid_arguments_rejected_without_device():
+    # argument validation happens before any HIP call
+    L = native.lib()
+    rc = L.gp_bucket_sum_apply(None, None, 2, 16, None)
+    assert rc == 1 and b"null" in L.gp_last_error()
+    rc = L.gp_scatter_add_rows(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), 4,
+                               native.DoubleIndex(0, 0), 0, 100, None)
+    assert rc == 1 and b"row_size" in L.gp_last_error()
+    # zero-size calls are no-ops that never touch the device
+    assert L.gp_bucket_sum_apply(None, None, 0, 16, None) == 0
+    assert L.gp_scatter_add_rows(None, None, None, 0, native.DoubleIndex(0, 0), 128, 0, None) == 0
+
+
+def test_product_does_not_import_oracle():
+    """No product source imports, links or calls the CPU oracle."""
+    import re
+    pat = re.compile(r"^\s*(from\s+oracle|import\s+oracle)|liboracle|oracle_\w+\s*\(|oracle\.\w+\(",
+                     re.M)
+    for root, _, files in os.walk(os.path.join(REPO, "geeps_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hpp", ".hip", ".h")) or f == "Makefile":
+                text = open(os.path.join(root, f)).read()
+                assert not pat.search(text), os.path.join(root, f)
+    for lib in ("libgp_reduce.so", "libgeeps.so"):
+        p = os.path.join(REPO, "geeps_amd", "lib", lib)
+        if os.path.exists(p):
+            out = subprocess.run(["nm", "-D", p], capture_output=True, text=True).stdout
+            assert "oracle_" not in out
+            deps = subprocess.run(["readelf", "-d", p], capture_output=True, text=True).stdout
+            assert "liboracle" not in deps

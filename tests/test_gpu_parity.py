@@ -1,0 +1,254 @@
+"""HIP path vs the CPU oracle, through the C-ABI (GPU box only).
+
+Bar: bit-exact.  Every kernel here is integer indexing plus fp32 adds in the
+reference's order, so results must match the oracle bit for bit (compared as
+uint32 views, so -0.0 / NaN payloads count too).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _ops():
+    from geeps_amd import rowops
+    return {"add_from": (rowops.add_rows_from_double_index_gpu, oracle.add_rows_from_double_index),
+            "assign_to": (rowops.assign_rows_to_double_index_gpu, oracle.assign_rows_to_double_index),
+            "assign_from": (rowops.assign_rows_from_double_index_gpu,
+                            oracle.assign_rows_from_double_index)}
+
+
+# ---- golden fixtures -------------------------------------------------------------
+
+def test_golden_rowops(dev, golden_rowops, manifest):
+    ops = _ops()
+    for name, spec in manifest["rowops"].items():
+        x, y, idx = (golden_rowops[f"{name}.{k}"] for k in ("x", "y", "index"))
+        ty = T(y, dev)
+        ops[spec["kind"]][0](ty, T(x, dev), T(idx, dev), idx.shape[0], tuple(spec["offset"]),
+                             spec["row_size"], spec["num_vals_limit"])
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(golden_rowops[f"{name}.expect"])), name
+
+
+def test_golden_bucket(dev, golden_bucket):
+    from geeps_amd import rowops
+    d = golden_bucket["deltas"]
+    for N in (1, 2, 8):
+        m = torch.zeros(d.shape[1], dtype=torch.float32, device=dev)
+        rowops.apply_updates(m, [T(d[c], dev) for c in range(N)])
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(m.cpu().numpy()), bits(golden_bucket[f"master_zero_N{N}"])), N
+    m = T(golden_bucket["master_seeded_init"], dev)
+    rowops.apply_updates(m, [T(d[c], dev) for c in range(8)])
+    assert np.array_equal(bits(m.cpu().numpy()), bits(golden_bucket["master_seeded_N8"]))
+    m = torch.zeros(d.shape[1], dtype=torch.float32, device=dev)
+    rowops.apply_updates(m, [T(d[c], dev) for c in reversed(range(8))])
+    assert np.array_equal(bits(m.cpu().numpy()), bits(golden_bucket["master_zero_N8_reversed"]))
+
+
+# ---- randomized sweeps vs the oracle ---------------------------------------------
+
+@pytest.mark.parametrize("kind", ["add_from", "assign_to", "assign_from"])
+@pytest.mark.parametrize("W", [1, 2, 3, 4, 5, 8, 12, 16, 60, 64, 100, 128, 256, 1000, 1024, 4096])
+def test_rowop_sweep(dev, kind, W):
+    rng = np.random.default_rng(W * 7 + len(kind))
+    n_cache = max(8, 300000 // (W * 4)) + 5
+    n_op = max(1, (n_cache * 2) // 3)
+    idx = np.stack([rng.permutation(n_op), rng.choice(n_cache, n_op, replace=False)], 1)
+    idx = idx.astype(np.int64)
+    if kind == "assign_to":
+        x = rng.standard_normal(n_cache * W).astype(np.float32)
+        y = rng.standard_normal(n_op * W).astype(np.float32)
+    else:
+        x = rng.standard_normal(n_op * W).astype(np.float32)
+        y = rng.standard_normal(n_cache * W).astype(np.float32)
+    for limit in (None, int(n_op * W * 0.6) + 1):
+        gpu_fn, ora_fn = _ops()[kind]
+        e = y.copy()
+        ora_fn(e, x, idx, (0, 0), W, limit)
+        ty = T(y, dev)
+        gpu_fn(ty, T(x, dev), T(idx, dev), n_op, (0, 0), W, limit)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), (kind, W, limit)
+
+
+@pytest.mark.parametrize("kind", ["add_from", "assign_to", "assign_from"])
+def test_rowop_offsets_and_unaligned_base(dev, kind):
+    """Non-zero offsets, and base pointers 4 B off 16-B alignment (scalar path)."""
+    rng = np.random.default_rng(3)
+    W, n_cache, n_op, off = 128, 500, 200, (13, 29)
+    idx = np.stack([np.arange(n_op), rng.choice(n_cache - off[1], n_op, replace=False)], 1)
+    idx = idx.astype(np.int64)
+    xs = (n_cache if kind == "assign_to" else n_op + off[0]) * W
+    ys = (n_op + off[0] if kind == "assign_to" else n_cache) * W
+    x = rng.standard_normal(xs + 1).astype(np.float32)
+    y = rng.standard_normal(ys + 1).astype(np.float32)
+    gpu_fn, ora_fn = _ops()[kind]
+    for shift in (0, 1):
+        e = y[shift:shift + ys].copy()
+        ora_fn(e, x[shift:shift + xs].copy(), idx, off, W)
+        ty_full = T(y, dev)
+        tx_full = T(x, dev)
+        ty = ty_full[shift:shift + ys]
+        gpu_fn(ty, tx_full[shift:shift + xs], T(idx, dev), n_op, off, W)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), shift
+        # nothing outside the view was touched
+        assert np.array_equal(bits(ty_full.cpu().numpy()[:shift]), bits(y[:shift]))
+
+
+@pytest.mark.parametrize("N", list(range(1, 21)))
+def test_bucket_sum_n_way(dev, N):
+    """1..20 buckets (more than 8 = chained launches, order preserved)."""
+    from geeps_amd import rowops
+    n = 12345 + N  # ragged: not a multiple of 4
+    ups = [oracle.synthetic_delta(c, n) for c in range(N)]
+    m0 = np.random.default_rng(N).standard_normal(n).astype(np.float32)
+    e = m0.copy()
+    oracle.apply_updates(e, ups)
+    m = T(m0, dev)
+    rowops.bucket_sum_apply(m, [T(u, dev) for u in ups])
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(m.cpu().numpy()), bits(e))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 255, 256, 257, 1023, 1024 * 256 + 3])
+def test_bucket_sum_sizes_and_alignment(dev, n):
+    from geeps_amd import rowops
+    ups = [oracle.synthetic_delta(c, n + 1) for c in range(3)]
+    for shift in (0, 1):
+        e = np.zeros(n, np.float32)
+        oracle.apply_updates(e, [u[shift:shift + n].copy() for u in ups])
+        backing = torch.zeros(n + 1, dtype=torch.float32, device=dev)
+        m = backing[shift:shift + n]
+        tb = [T(u, dev)[shift:shift + n] for u in ups]
+        rowops.bucket_sum_apply(m, tb)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(m.cpu().numpy()), bits(e)), (n, shift)
+        if shift:
+            assert backing[0].item() == 0.0
+
+
+def test_gpu_add_and_zero(dev):
+    from geeps_amd import rowops
+    n = 100_001
+    a, b = oracle.synthetic_delta(1, n), oracle.synthetic_delta(2, n)
+    y = torch.empty(n, dtype=torch.float32, device=dev)
+    rowops.gpu_add(n, T(a, dev), T(b, dev), y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(y.cpu().numpy()), bits(oracle.vs_add(a, b)))
+    ty = T(a, dev)
+    rowops.add_row_batch_gpu(ty, T(b, dev), n // 128, 128)
+    e = a.copy()
+    e[:(n // 128) * 128] = oracle.vs_add(a[:(n // 128) * 128], b[:(n // 128) * 128])
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e))
+    rowops.zerofy_data_gpu(ty)
+    assert int(torch.count_nonzero(ty)) == 0
+
+
+def test_empty_calls_are_noops(dev):
+    from geeps_amd import rowops
+    y = torch.ones(256, dtype=torch.float32, device=dev)
+    idx = torch.zeros((0, 2), dtype=torch.int64, device=dev)
+    rowops.add_rows_from_double_index_gpu(y, y, idx, 0)
+    rowops.bucket_sum_apply(y, [])
+    torch.cuda.synchronize()
+    assert torch.all(y == 1)
+
+
+def test_out_of_range_index_rejected_before_launch(dev):
+    from geeps_amd import rowops
+    y = torch.zeros(4 * 128, dtype=torch.float32, device=dev)
+    x = torch.zeros(4 * 128, dtype=torch.float32, device=dev)
+    idx = torch.tensor([[0, 4]], dtype=torch.int64, device=dev)
+    with pytest.raises(ValueError):
+        rowops.add_rows_from_double_index_gpu(y, x, idx, 1)
+    with pytest.raises(ValueError):
+        rowops.assign_rows_to_double_index_gpu(y, x, idx, 1)
+
+
+def test_side_stream(dev):
+    from geeps_amd import rowops
+    n = 1 << 20
+    ups = [oracle.synthetic_delta(c, n) for c in range(4)]
+    e = np.zeros(n, np.float32)
+    oracle.apply_updates(e, ups)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        m = torch.zeros(n, dtype=torch.float32, device=dev)
+        tb = [T(u, dev) for u in ups]
+        rowops.bucket_sum_apply(m, tb)   # launched on s (current stream)
+    s.synchronize()
+    assert np.array_equal(bits(m.cpu().numpy()), bits(e))
+
+
+# ---- full BASELINE sizes: sampled-row exactness ---------------------------------
+
+def _sample_rows(rng, R, k=2048):
+    # always include the first and last rows (grid-stride head and tail)
+    return np.unique(np.concatenate([[0, R - 1], rng.choice(R, size=k, replace=False)]))
+
+
+@pytest.mark.slow
+def test_full_size_8way_bucket_sum(dev):
+    """1M rows x 1024 fp32, 8 clients (36 GiB resident).  Per-element arithmetic is
+    independent across elements, so the oracle on sampled rows is an exact check."""
+    from geeps_amd import rowops
+    R, W, N = 1 << 20, 1024, 8
+    n = R * W
+    g = torch.Generator(device=dev)
+    buckets = []
+    for c in range(N):
+        g.manual_seed(1000 + c)
+        buckets.append(torch.rand(n, generator=g, device=dev) - 0.5)
+    g.manual_seed(77)
+    master = torch.rand(n, generator=g, device=dev) - 0.5
+    rows = _sample_rows(np.random.default_rng(0), R)
+    ridx = torch.from_numpy(rows).to(dev)
+    m0 = master.view(R, W)[ridx].cpu().numpy().ravel()
+    bs = [b.view(R, W)[ridx].cpu().numpy().ravel() for b in buckets]
+    rowops.bucket_sum_apply(master, buckets)
+    torch.cuda.synchronize()
+    oracle.apply_updates(m0, bs)
+    got = master.view(R, W)[ridx].cpu().numpy().ravel()
+    assert np.array_equal(bits(got), bits(m0))
+
+
+@pytest.mark.slow
+def test_full_size_scatter_add_permuted(dev):
+    """8M RowData rows (the 1M x 1024 table through the 128-float API), random
+    permutation DoubleIndex; sampled rows exact vs oracle, and x added then
+    subtracted restores y bit-exactly on integer-valued data."""
+    from geeps_amd import rowops
+    R, W = 1 << 23, 128
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    perm = torch.randperm(R, generator=g, device=dev)
+    idx = torch.stack([torch.arange(R, device=dev), perm], 1).contiguous()
+    x = torch.randint(-64, 64, (R * W,), generator=g, device=dev).float()
+    y = torch.randint(-64, 64, (R * W,), generator=g, device=dev).float()
+    y0 = y.clone()
+    rows = _sample_rows(np.random.default_rng(1), R)
+    rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), W, R * W, validate=False)
+    torch.cuda.synchronize()
+    # oracle on the sampled op rows: y[perm[r]] = y0[perm[r]] + x[r]
+    pr = perm.cpu().numpy()[rows]
+    ridx, pidx = torch.from_numpy(rows).to(dev), torch.from_numpy(pr).to(dev)
+    got = y.view(R, W)[pidx].cpu().numpy()
+    e = y0.view(R, W)[pidx].cpu().numpy() + x.view(R, W)[ridx].cpu().numpy()
+    assert np.array_equal(bits(got), bits(e.astype(np.float32)))
+    rowops.add_rows_from_double_index_gpu(y, -x, idx, R, (0, 0), W, R * W, validate=False)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
