@@ -1,0 +1,807 @@
+// ClientLib — see client.hpp.  Reference: src/client/clientlib*.cpp.
+#include "client.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <set>
+#include <sstream>
+#include <unordered_set>
+
+#include "check.hpp"
+#include "net.hpp"
+
+namespace geeps {
+
+ClientLib *client_lib = nullptr;
+
+namespace {
+
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+constexpr size_t kRowBytes = sizeof(RowData);
+constexpr double kConnectTimeoutS = 300.0;
+constexpr int kWaitWarnMs = 12000;  // the reference's 12 s timed_wait warnings
+
+struct PinnedPool {
+  std::vector<std::shared_ptr<PinnedArray<float>>> bufs;
+  std::shared_ptr<PinnedArray<float>> get(size_t floats) {
+    for (auto &b : bufs)
+      if (b.use_count() == 1 && b->size() >= floats) return b;
+    bufs.push_back(std::make_shared<PinnedArray<float>>(std::max<size_t>(floats, 1)));
+    return bufs.back();
+  }
+};
+
+}  // namespace
+
+std::string ClientStats::to_json() const {
+  std::ostringstream o;
+  o << "{\"nr_read\": " << nr_read << ", \"nr_update\": " << nr_update
+    << ", \"nr_clock\": " << nr_clock << ", \"nr_push\": " << nr_push
+    << ", \"nr_refresh\": " << nr_refresh << ", \"rows_updated\": " << rows_updated
+    << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
+    << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
+    << ", \"update_time\": " << update_time << ", \"push_time\": " << push_time
+    << ", \"refresh_time\": " << refresh_time << "}";
+  return o.str();
+}
+
+void ChannelSink::read_row_batch_reply(uint32_t client_id, const RowBatchReply &r) {
+  lib_->remote_reply(channel_, client_id, r);
+}
+
+void ChannelSink::shutdown_ack(uint32_t client_id) { lib_->remote_shutdown_ack(channel_, client_id); }
+
+// ---------------------------------------------------------------------------
+// construction: servers, streams, sockets (clientlib.cpp:53-158)
+// ---------------------------------------------------------------------------
+ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
+    : process_id_(process_id),
+      config_(config),
+      num_processes_((uint32_t)std::max<size_t>(1, config.host_list.size())),
+      num_channels_(std::max(1u, config.num_comm_channels)) {
+  GP_CHECK_MSG(process_id_ < num_processes_,
+               "process_id " << process_id_ << " >= host_list.size() " << num_processes_);
+  GP_CHECK(config_.num_tables > 0);
+  GP_CHECK_MSG(config_.port_list.empty() || config_.port_list.size() >= num_processes_,
+               "port_list must have one port per host");
+  GP_CALL(gp_get_device(&device_));
+  channels_.resize(num_channels_);
+  for (uint32_t c = 0; c < num_channels_; ++c) {
+    auto ch = std::make_unique<Channel>();
+    ch->id = c;
+    ch->tables.resize(config_.num_tables);
+    ch->stream = std::make_unique<Stream>();
+    ch->recv_stream = std::make_unique<Stream>();
+    ch->send_stream = std::make_unique<Stream>();
+    ch->reply_stream = std::make_unique<Stream>();
+    ch->sink = std::make_unique<ChannelSink>(this, c);
+    ch->server = std::make_unique<TabletServer>(process_id_, c, num_processes_,
+                                                config_.num_tables, ch->sink.get());
+    ch->server_fd.assign(num_processes_, -1);
+    ch->client_fd.assign(num_processes_, -1);
+    channels_[c] = std::move(ch);
+  }
+  start_network();
+}
+
+ClientLib::~ClientLib() { shutdown(); }
+
+uint16_t ClientLib::port_of(uint32_t process, uint32_t channel) const {
+  // The reference binds tcp_base_port + channel on every host and ignores
+  // port_list (clientlib.cpp:57-60, 111-112; server-entry.cpp:56-57); honouring
+  // port_list lets several processes share one host (BASELINE config 1).
+  const uint32_t base = config_.port_list.empty() ? config_.tcp_base_port : config_.port_list[process];
+  return (uint16_t)(base + channel);
+}
+
+void ClientLib::start_network() {
+  if (num_processes_ == 1) return;
+  // 1. listen: this process's tablet server of every channel
+  for (auto &chp : channels_) {
+    std::string err;
+    chp->listen_fd = listen_tcp(port_of(process_id_, chp->id), &err);
+    GP_CHECK_MSG(chp->listen_fd >= 0, err);
+  }
+  accept_thread_ = std::thread([this] {
+    GP_CALL(gp_set_device(device_));
+    for (auto &chp : channels_) server_accept_loop(*chp, (int)num_processes_ - 1);
+  });
+  // 2. connect: this process's client to every remote server
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    for (uint32_t s = 0; s < num_processes_; ++s) {
+      if (s == process_id_) continue;
+      std::string err;
+      const int fd = connect_tcp(config_.host_list[s], port_of(s, ch.id), kConnectTimeoutS, &err);
+      GP_CHECK_MSG(fd >= 0, err);
+      const uint32_t hello[2] = {kHelloCmd, process_id_};
+      GP_CHECK(send_frame(fd, {Part{hello, sizeof hello}}));
+      ch.server_fd[s] = fd;
+      ch.client_readers.emplace_back([this, &ch, s, fd] { client_reader(ch, s, fd); });
+    }
+  }
+  accept_thread_.join();
+}
+
+void ClientLib::server_accept_loop(Channel &ch, int expected) {
+  for (int i = 0; i < expected; ++i) {
+    const int fd = accept_tcp(ch.listen_fd);
+    GP_CHECK_MSG(fd >= 0, "accept failed on channel " << ch.id);
+    std::vector<RecvPart> parts;
+    std::vector<std::vector<char>> scratch;
+    GP_CHECK(recv_frame(fd, parts, scratch, nullptr, nullptr));
+    GP_CHECK(parts.size() == 1 && parts[0].size == 8);
+    uint32_t hello[2];
+    std::memcpy(hello, parts[0].data, 8);
+    GP_CHECK_EQ(hello[0], kHelloCmd);
+    GP_CHECK_LT(hello[1], num_processes_);
+    GP_CHECK_MSG(ch.client_fd[hello[1]] < 0, "duplicate client " << hello[1]);
+    ch.client_fd[hello[1]] = fd;
+    const uint32_t cid = hello[1];
+    ch.server_readers.emplace_back([this, &ch, cid, fd] { server_reader(ch, cid, fd); });
+  }
+}
+
+// Server side of a client connection: CLOCK_WITH_UPDATES_BATCH / CLOCK frames
+// (ClientServerDecode::decode_msg, server-encoder-decoder.cpp:153-183).
+void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
+  GP_CALL(gp_set_device(device_));
+  PinnedPool pool;
+  struct Ctx {
+    PinnedPool *pool;
+    std::shared_ptr<PinnedArray<float>> rows;
+  } ctx{&pool, nullptr};
+  auto alloc = [](void *c, size_t i, size_t size) -> void * {
+    auto *x = static_cast<Ctx *>(c);
+    if (i != 2) return nullptr;
+    x->rows = x->pool->get((size + 3) / 4);
+    return x->rows->data();
+  };
+  std::vector<RecvPart> parts;
+  std::vector<std::vector<char>> scratch;
+  for (;;) {
+    ctx.rows.reset();
+    if (!recv_frame(fd, parts, scratch, alloc, &ctx)) break;
+    GP_CHECK(!parts.empty() && parts[0].size >= 1);
+    const command_t cmd = *static_cast<const command_t *>(parts[0].data);
+    if (cmd == CLOCK_WITH_UPDATES_BATCH) {
+      GP_CHECK(parts.size() == 3 && parts[0].size == sizeof(cs_clock_with_updates_batch_msg_t));
+      cs_clock_with_updates_batch_msg_t h;
+      std::memcpy(&h, parts[0].data, sizeof h);
+      GP_CHECK_EQ(h.client_id, client_id);
+      const size_t n = parts[1].size / sizeof(RowKey);
+      GP_CHECK_EQ(parts[2].size, n * kRowBytes);
+      UpdateBatch b;
+      b.client_id = h.client_id;
+      b.clock = h.clock;
+      b.table_id = h.table_id;
+      b.keys.resize(n);
+      if (n) std::memcpy(b.keys.data(), parts[1].data, parts[1].size);
+      b.host_rows = ctx.rows;
+      ch.server->post_updates(std::move(b));
+    } else if (cmd == CLOCK) {
+      GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(cs_clock_msg_t));
+      cs_clock_msg_t h;
+      std::memcpy(&h, parts[0].data, sizeof h);
+      ch.server->post_clock(h.client_id, h.clock, h.table_id);
+    } else if (cmd == SHUTDOWN) {
+      // The client sends nothing after this (shutdown handshake).
+      ch.server->post_shutdown(client_id);
+      break;
+    } else {
+      GP_CHECK_MSG(false, "server received unknown command " << (int)cmd);
+    }
+  }
+}
+
+// Client side of a server connection: READ_ROW_BATCH replies
+// (ServerClientDecode::read_row_batch, client/encoder-decoder.cpp:228-251).
+void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
+  GP_CALL(gp_set_device(device_));
+  PinnedArray<float> buf;
+  auto alloc = [](void *c, size_t i, size_t size) -> void * {
+    auto *b = static_cast<PinnedArray<float> *>(c);
+    if (i != 2) return nullptr;
+    if (b->size() * 4 < size) b->resize((size + 3) / 4);
+    return b->data();
+  };
+  std::vector<RecvPart> parts;
+  std::vector<std::vector<char>> scratch;
+  for (;;) {
+    if (!recv_frame(fd, parts, scratch, alloc, &buf)) break;
+    GP_CHECK(!parts.empty() && parts[0].size >= 1);
+    const command_t cmd = *static_cast<const command_t *>(parts[0].data);
+    if (cmd == SHUTDOWN) break;  // the server will send nothing more
+    GP_CHECK(parts.size() == 3 && parts[0].size == sizeof(sc_read_row_batch_msg_t));
+    sc_read_row_batch_msg_t h;
+    std::memcpy(&h, parts[0].data, sizeof h);
+    GP_CHECK_EQ(h.cmd, (command_t)READ_ROW_BATCH);
+    GP_CHECK_EQ(h.server_id, server_id);
+    const size_t n = parts[1].size / sizeof(RowKey);
+    GP_CHECK_EQ(parts[2].size, n * kRowBytes);
+    recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
+                   static_cast<const float *>(parts[2].data), n, false);
+  }
+}
+
+void ClientLib::remote_shutdown_ack(uint32_t channel, uint32_t client_id) {
+  if (client_id == process_id_) return;
+  Channel &ch = *channels_[channel];
+  cs_clock_msg_t h{};
+  h.cmd = SHUTDOWN;
+  h.client_id = process_id_;
+  GP_CHECK_MSG(send_frame(ch.client_fd[client_id], {Part{&h, sizeof h}}),
+               "shutdown ack to client " << client_id << " failed");
+}
+
+// The tablet server's reply to one client (read_row_batch_reply,
+// server-encoder-decoder.cpp:228-250): in-process -> device copy, remote ->
+// D2H into pinned memory and one frame on the client's socket.
+void ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r) {
+  if (client_id == process_id_) {
+    recv_row_batch(channel, r.server_id, r.table_id, r.data_age, r.self_clock, r.device_rows,
+                   r.num_rows, true);
+    return;
+  }
+  Channel &ch = *channels_[channel];
+  const int fd = ch.client_fd[client_id];
+  GP_CHECK_MSG(fd >= 0, "no connection to client " << client_id);
+  const size_t floats = r.num_rows * ROW_DATA_SIZE;
+  if (ch.reply_buf.size() < floats) ch.reply_buf.resize(floats);
+  if (floats) {
+    GP_CALL(gp_memcpy_async(ch.reply_buf.data(), r.device_rows, floats * 4, ch.reply_stream->get()));
+    ch.reply_stream->sync();
+  }
+  sc_read_row_batch_msg_t h{};
+  h.cmd = READ_ROW_BATCH;
+  h.server_id = r.server_id;
+  h.data_age = r.data_age;
+  h.self_clock = r.self_clock;
+  h.table_id = r.table_id;
+  GP_CHECK_MSG(send_frame(fd, {Part{&h, sizeof h}, Part{r.keys, r.num_rows * sizeof(RowKey)},
+                               Part{ch.reply_buf.data(), floats * 4}}),
+               "send to client " << client_id << " failed");
+}
+
+// ---------------------------------------------------------------------------
+// virtual iteration (clientlib-viter.cpp)
+// ---------------------------------------------------------------------------
+int ClientLib::virtual_op(OpInfo &&op) {
+  GP_CHECK_MSG(!finished_vi_, "virtual op after FinishVirtualIteration");
+  opseq_.push_back(std::move(op));
+  return (int)opseq_.size() - 1;
+}
+
+uint32_t ClientLib::channel_of(uint32_t table_id, row_idx_t row) const {
+  return (uint32_t)(row / rows_per_channel_[table_id]);  // clientlib.cpp:216-219
+}
+
+void ClientLib::finish_virtual_iteration() {
+  GP_CHECK(!finished_vi_);
+  finished_vi_ = true;
+  const uint32_t T = config_.num_tables;
+
+  // Post-steps inherit their pre-step's table and locality (vi_thread_finalize).
+  for (auto &op : opseq_) {
+    if (op.type == OpInfo::WRITE || op.type == OpInfo::POST_READ) {
+      GP_CHECK(op.prestep_handle >= 0 && (size_t)op.prestep_handle < opseq_.size());
+      const OpInfo &pre = opseq_[op.prestep_handle];
+      GP_CHECK(pre.type == (op.type == OpInfo::WRITE ? OpInfo::PRE_WRITE : OpInfo::READ));
+      op.local = pre.local;
+      op.table_id = pre.table_id;
+    } else if ((op.type == OpInfo::READ || op.type == OpInfo::PRE_WRITE) && !op.local) {
+      GP_CHECK_MSG(op.table < T, "table " << op.table << " >= num_tables " << T);
+      op.table_id = (uint32_t)op.table;
+    }
+  }
+  for (auto &op : opseq_)
+    if ((op.type == OpInfo::WRITE || op.type == OpInfo::POST_READ) && !op.local)
+      op.table_id = opseq_[op.prestep_handle].table_id;
+
+  // Last write of each table, among the ops up to the last CLOCK.
+  std::vector<bool> seen(T, false);
+  bool clock_seen = false;
+  for (size_t i = opseq_.size(); i-- > 0;) {
+    OpInfo &op = opseq_[i];
+    if (op.type == OpInfo::CLOCK) clock_seen = true;
+    if (!clock_seen) continue;
+    if (!op.local && op.type == OpInfo::WRITE && !seen[op.table_id]) {
+      seen[op.table_id] = true;
+      op.table_last_write = true;
+    }
+  }
+  for (uint32_t t = 0; t < T; ++t) GP_CHECK_MSG(seen[t], "No one writes table " << t);
+
+  // Param cache rows in first-access order per table (vi_decide_param_cache).
+  std::vector<std::vector<row_idx_t>> keys(T);
+  std::vector<std::unordered_set<row_idx_t>> known(T);
+  for (auto &op : opseq_) {
+    if (op.local || (op.type != OpInfo::READ && op.type != OpInfo::PRE_WRITE) || op.rows.empty())
+      continue;
+    auto &kn = known[op.table_id];
+    const bool fresh = !kn.count(op.rows[0]);
+    for (row_idx_t r : op.rows) {
+      if (fresh) {
+        GP_CHECK_MSG(!kn.count(r), "row " << r << " of a new key batch already cached");
+        kn.insert(r);
+        keys[op.table_id].push_back(r);
+      } else {
+        GP_CHECK_MSG(kn.count(r), "row " << r << " mixes new and cached keys in one op");
+      }
+    }
+  }
+  rows_per_channel_.assign(T, 1);
+  for (uint32_t t = 0; t < T; ++t)
+    rows_per_channel_[t] = std::max<size_t>(1, (keys[t].size() + num_channels_ - 1) / num_channels_);
+
+  // Oplog entries per cache row: 1, or slack + 1 with read-my-writes
+  // (vi_decide_param_cache, clientlib-viter.cpp:507-517); used for planning only,
+  // the pool grows on demand.
+  iter_t max_slack = 0;
+  for (auto &op : opseq_)
+    if (!op.local && op.type == OpInfo::READ) max_slack = std::max(max_slack, op.slack);
+  const size_t entries = config_.read_my_writes ? (size_t)max_slack + 1 : 1;
+
+  size_t planned = 0;
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    for (uint32_t t = 0; t < T; ++t) {
+      ParamCache &pc = ch.tables[t];
+      for (row_idx_t r : keys[t]) {
+        if (channel_of(t, r) != ch.id) continue;
+        pc.index[r] = pc.num_rows++;
+        pc.row_keys.emplace_back(t, r);
+      }
+      pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
+      if (pc.num_rows) GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.stream->get()));
+      planned += pc.num_rows * kRowBytes * (1 + entries);
+      pc.server_row_start.resize(num_processes_);
+      pc.server_num_rows.resize(num_processes_);
+      const size_t div = pc.num_rows / num_processes_, res = pc.num_rows % num_processes_;
+      for (size_t i = 0; i < num_processes_; ++i) {
+        pc.server_row_start[i] = div * i + std::min(i, res);
+        pc.server_num_rows[i] = div + (i < res ? 1 : 0);
+      }
+      pc.per_server_data_age.assign(num_processes_, INITIAL_DATA_AGE);
+      pc.server_clock.assign(num_processes_, INITIAL_DATA_AGE);
+    }
+    ch.stream->sync();
+  }
+  for (auto &chp : channels_)
+    for (uint32_t t = 0; t < T; ++t)
+      GP_CHECK_MSG(chp->tables[t].num_rows <= rows_per_channel_[t] || num_channels_ == 1,
+                   "channel " << chp->id << " of table " << t << " holds rows past its range");
+
+  // Op buffers, DoubleIndex, local storage.
+  for (auto &op : opseq_) {
+    if (op.type != OpInfo::READ && op.type != OpInfo::PRE_WRITE) continue;
+    if (op.local) {
+      auto &slot = local_storage_[op.rows];
+      if (!slot) {
+        slot = std::make_unique<DeviceArray<float>>(std::max<size_t>(1, op.rows.size()) * ROW_DATA_SIZE);
+        GP_CALL(gp_zero(slot->data(), slot->size(), nullptr));
+        planned += slot->bytes();
+      }
+      op.local_ptr = slot->data();
+      continue;
+    }
+    op.buffer.resize(std::max<size_t>(1, op.rows.size()) * ROW_DATA_SIZE);
+    GP_CALL(gp_zero(op.buffer.data(), op.buffer.size(), nullptr));
+    planned += op.buffer.bytes();
+    create_double_index(op);
+  }
+  GP_CALL(gp_device_synchronize());
+  if (planned > config_.gpu_memory_capacity) {
+    std::ostringstream o;
+    o << "planned HBM use " << planned << " B exceeds gpu_memory_capacity "
+      << config_.gpu_memory_capacity << " B";
+    GP_CHECK_MSG(config_.mm_warning_level < 2, o.str());
+    std::cerr << "libgeeps WARNING: " << o.str() << " (all data kept in HBM)\n";
+  }
+}
+
+// One DoubleIndex per op, grouped by channel, each channel's id1 set a
+// contiguous, duplicate-free cache range (vi_create_double_index,
+// clientlib-viter.cpp:817-883; the scatter-add kernel relies on distinct id1).
+void ClientLib::create_double_index(OpInfo &op) {
+  std::vector<std::vector<gp_double_index>> per(num_channels_);
+  for (size_t j = 0; j < op.rows.size(); ++j) {
+    const uint32_t c = channel_of(op.table_id, op.rows[j]);
+    GP_CHECK_LT(c, num_channels_);
+    ParamCache &pc = channels_[c]->tables[op.table_id];
+    auto it = pc.index.find(op.rows[j]);
+    GP_CHECK_MSG(it != pc.index.end(), "row " << op.rows[j] << " not in the param cache");
+    per[c].push_back(gp_double_index{j, it->second});
+  }
+  std::vector<gp_double_index> flat;
+  flat.reserve(op.rows.size());
+  op.ch_start.assign(num_channels_, 0);
+  op.ch_size.assign(num_channels_, 0);
+  for (uint32_t c = 0; c < num_channels_; ++c) {
+    op.ch_start[c] = flat.size();
+    op.ch_size[c] = per[c].size();
+    if (!per[c].empty()) {
+      uint64_t lo = per[c][0].id1, hi = lo;
+      std::unordered_set<uint64_t> ids;
+      for (auto &d : per[c]) {
+        lo = std::min<uint64_t>(lo, d.id1);
+        hi = std::max<uint64_t>(hi, d.id1);
+        ids.insert(d.id1);
+      }
+      GP_CHECK_MSG(ids.size() == per[c].size(), "duplicate rows in one op");
+      GP_CHECK_EQ(hi - lo + 1, (uint64_t)per[c].size());
+    }
+    flat.insert(flat.end(), per[c].begin(), per[c].end());
+  }
+  op.index.resize(std::max<size_t>(1, flat.size()));
+  if (!flat.empty())
+    GP_CALL(gp_memcpy_async(op.index.data(), flat.data(), flat.size() * sizeof(gp_double_index),
+                            nullptr));
+  GP_CALL(gp_device_synchronize());
+}
+
+void ClientLib::start_iterations() {
+  GP_CHECK_MSG(finished_vi_, "StartIterations before FinishVirtualIteration");
+  started_ = true;
+  last_handle_ = -1;
+}
+
+void ClientLib::check_handle(int handle) {
+  GP_CHECK(handle >= 0 && (size_t)handle < opseq_.size());
+  if (started_) {
+    GP_CHECK_MSG(handle == last_handle_ + 1,
+                 "handle mismatch: " << handle << " after " << last_handle_);
+    last_handle_ = handle;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Read / PostRead (clientlib.cpp:349-473; clientlib-data.cpp:191-278)
+// ---------------------------------------------------------------------------
+bool ClientLib::read_batch(RowData **buffer, int handle) {
+  check_handle(handle);
+  OpInfo &op = opseq_[handle];
+  GP_CHECK(op.type == OpInfo::READ);
+  GP_CHECK_MSG(!op.in_use, "Read of handle " << handle << " before its PostRead");
+  if (op.local) {
+    *buffer = reinterpret_cast<RowData *>(op.local_ptr);
+    op.in_use = true;
+    return true;
+  }
+  const double t0 = now_s();
+  const iter_t need = iteration_ - op.slack - 1;
+  double waited = 0;
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    ParamCache &pc = ch.tables[op.table_id];
+    std::unique_lock<std::mutex> lk(ch.mu);
+    const double w0 = now_s();
+    while (pc.data_age < need) {
+      if (!ch.cv.wait_for(lk, std::chrono::milliseconds(kWaitWarnMs),
+                          [&] { return pc.data_age >= need; }) &&
+          ch.id == 0) {
+        std::cerr << "machine " << process_id_ << " wait time out! Need: " << need
+                  << " Data age: " << pc.data_age << std::endl;
+      }
+    }
+    waited += now_s() - w0;
+    if (op.ch_size[ch.id])
+      GP_CALL(gp_gather_rows(reinterpret_cast<float *>(op.buffer.data()), pc.data.data(),
+                             op.index.data() + op.ch_start[ch.id], op.ch_size[ch.id],
+                             gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit,
+                             ch.stream->get()));
+    ch.stream->sync();
+  }
+  *buffer = reinterpret_cast<RowData *>(op.buffer.data());
+  op.in_use = true;
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nr_read++;
+  stats_.rows_read += op.rows.size();
+  stats_.read_wait_time += waited;
+  stats_.read_time += now_s() - t0;
+  return true;
+}
+
+void ClientLib::postread_batch(int handle) {
+  check_handle(handle);
+  OpInfo &op = opseq_[handle];
+  GP_CHECK(op.type == OpInfo::POST_READ);
+  OpInfo &pre = opseq_[op.prestep_handle];
+  GP_CHECK(pre.type == OpInfo::READ);
+  // GPU-resident local data is used in place, so `keep` needs no copy back
+  // (the reference copies back only for CPU-placed local data).
+  pre.in_use = false;
+}
+
+// ---------------------------------------------------------------------------
+// PreUpdate / Update (clientlib.cpp:475-614; clientlib-data.cpp:304-396)
+// ---------------------------------------------------------------------------
+void ClientLib::preupdate_batch(RowOpVal **buffer, int handle) {
+  check_handle(handle);
+  OpInfo &op = opseq_[handle];
+  GP_CHECK(op.type == OpInfo::PRE_WRITE);
+  GP_CHECK(!op.local);
+  GP_CHECK_MSG(!op.in_use, "PreUpdate of handle " << handle << " before its Update");
+  op.in_use = true;
+  *buffer = reinterpret_cast<RowOpVal *>(op.buffer.data());
+}
+
+std::shared_ptr<DeviceArray<float>> ClientLib::get_oplog(ParamCache &pc, iter_t clock,
+                                                         gp_stream s) {
+  auto it = pc.oplog.find(clock);
+  if (it != pc.oplog.end()) return it->second;
+  // create_oplog_entry + zerofy_data_gpu (clientlib.cpp:265-280,
+  // clientlib-data.cpp:356-371).  A pooled buffer is reused once nothing (the
+  // in-process server's pending bucket included) references it.
+  std::shared_ptr<DeviceArray<float>> buf;
+  for (auto &b : pc.oplog_pool)
+    if (b.use_count() == 1) {
+      buf = b;
+      break;
+    }
+  if (!buf) {
+    pc.oplog_pool.push_back(std::make_shared<DeviceArray<float>>(pc.num_rows * ROW_DATA_SIZE));
+    buf = pc.oplog_pool.back();
+  }
+  GP_CALL(gp_zero(buf->data(), pc.num_rows * ROW_DATA_SIZE, s));
+  pc.oplog[clock] = buf;
+  return buf;
+}
+
+void ClientLib::update_batch(int handle) {
+  check_handle(handle);
+  OpInfo &op = opseq_[handle];
+  GP_CHECK(op.type == OpInfo::WRITE);
+  OpInfo &pre = opseq_[op.prestep_handle];
+  GP_CHECK(pre.type == OpInfo::PRE_WRITE && !pre.local);
+  GP_CHECK_MSG(pre.in_use, "Update of handle " << handle << " without PreUpdate");
+  const double t0 = now_s();
+  const iter_t clock = iteration_;
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    const size_t n = pre.ch_size[ch.id];
+    std::lock_guard<std::mutex> lk(ch.mu);
+    ParamCache &pc = ch.tables[pre.table_id];
+    if (pc.num_rows == 0) continue;
+    auto oplog = get_oplog(pc, clock, ch.stream->get());
+    if (n) {
+      const gp_double_index *idx = pre.index.data() + pre.ch_start[ch.id];
+      GP_CALL(gp_scatter_add_rows(oplog->data(), pre.buffer.data(), idx, n, gp_double_index{0, 0},
+                                  ROW_DATA_SIZE, pre.num_vals_limit, ch.stream->get()));
+      if (config_.read_my_writes)
+        GP_CALL(gp_scatter_add_rows(pc.data.data(), pre.buffer.data(), idx, n,
+                                    gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
+                                    ch.stream->get()));
+    }
+    ch.stream->sync();
+  }
+  pre.in_use = false;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.nr_update++;
+    stats_.rows_updated += pre.rows.size();
+    stats_.update_time += now_s() - t0;
+  }
+  // After StartIterations the table is clocked at its last write
+  // (reclaim_worker_update, clientlib-bg-access.cpp:534-538).
+  if (started_ && op.table_last_write) clock_table(clock + 1, op.table_id);
+}
+
+// ---------------------------------------------------------------------------
+// Clock (clientlib.cpp:282-314, 617-625) and the push (clientlib-data.cpp:436-522)
+// ---------------------------------------------------------------------------
+void ClientLib::iterate() {
+  iteration_++;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.nr_clock++;
+  }
+  if (started_) {
+    last_handle_ = -1;
+  } else {
+    clock_all(iteration_);
+  }
+}
+
+void ClientLib::clock_all(iter_t clock) {
+  for (uint32_t t = 0; t < config_.num_tables; ++t) clock_table(clock, t);
+}
+
+void ClientLib::clock_table(iter_t clock, uint32_t table_id) {
+  fast_clock_ = clock;
+  const iter_t signalled = clock - 1;  // "clock c" means clock c-1 is finished
+  for (auto &chp : channels_) push_updates(*chp, signalled, table_id);
+}
+
+void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
+  const double t0 = now_s();
+  std::shared_ptr<DeviceArray<float>> oplog;
+  std::vector<size_t> starts, counts;
+  std::vector<RowKey> keys;
+  {
+    std::lock_guard<std::mutex> lk(ch.mu);
+    ParamCache &pc = ch.tables[table_id];
+    auto it = pc.oplog.find(clock);
+    if (it != pc.oplog.end()) oplog = it->second;
+    if (oplog && !config_.read_my_writes) pc.oplog.erase(it);  // reclaim_oplog
+    starts = pc.server_row_start;
+    counts = pc.server_num_rows;
+    keys = pc.row_keys;
+  }
+  size_t remote_bytes = 0;
+  for (uint32_t s = 0; s < num_processes_; ++s) {
+    if (!oplog) {
+      // clock_broadcast: a CLOCK with no updates (encoder-decoder.cpp:85-100).
+      if (s == process_id_) {
+        ch.server->post_clock(process_id_, clock, table_id);
+      } else {
+        cs_clock_msg_t h{};
+        h.cmd = CLOCK;
+        h.client_id = process_id_;
+        h.clock = clock;
+        h.table_id = table_id;
+        GP_CHECK(send_frame(ch.server_fd[s], {Part{&h, sizeof h}}));
+      }
+      continue;
+    }
+    const size_t a = starts[s], n = counts[s];
+    if (s == process_id_) {
+      UpdateBatch b;
+      b.client_id = process_id_;
+      b.clock = clock;
+      b.table_id = table_id;
+      b.keys.assign(keys.begin() + a, keys.begin() + a + n);
+      b.device_rows = oplog->data() + a * ROW_DATA_SIZE;
+      b.keepalive = oplog;  // zero-copy: the server reads the oplog slice in place
+      ch.server->post_updates(std::move(b));
+    } else {
+      const size_t floats = n * ROW_DATA_SIZE;
+      if (ch.send_buf.size() < floats) ch.send_buf.resize(floats);
+      if (floats) {
+        GP_CALL(gp_memcpy_async(ch.send_buf.data(), oplog->data() + a * ROW_DATA_SIZE, floats * 4,
+                                ch.send_stream->get()));
+        ch.send_stream->sync();
+      }
+      cs_clock_with_updates_batch_msg_t h{};
+      h.cmd = CLOCK_WITH_UPDATES_BATCH;
+      h.client_id = process_id_;
+      h.clock = clock;
+      h.table_id = table_id;
+      GP_CHECK(send_frame(ch.server_fd[s], {Part{&h, sizeof h},
+                                            Part{keys.data() + a, n * sizeof(RowKey)},
+                                            Part{ch.send_buf.data(), floats * 4}}));
+      remote_bytes += floats * 4;
+    }
+  }
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nr_push++;
+  stats_.bytes_pushed_remote += remote_bytes;
+  stats_.push_time += now_s() - t0;
+}
+
+void ClientLib::reclaim_oplogs(ParamCache &pc, iter_t upto) {
+  for (auto it = pc.oplog.begin(); it != pc.oplog.end() && it->first <= upto;)
+    it = pc.oplog.erase(it);
+}
+
+// recv_row_batch + recv_row_batch_gpu + server_clock_cbk
+// (clientlib-data.cpp:51-151, clientlib-cbk.cpp:81-104).
+void ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id,
+                               iter_t data_age, iter_t self_clock, const float *rows,
+                               size_t num_rows, bool device) {
+  const double t0 = now_s();
+  Channel &ch = *channels_[channel];
+  {
+    std::lock_guard<std::mutex> lk(ch.mu);
+    GP_CHECK_LT(table_id, ch.tables.size());
+    ParamCache &pc = ch.tables[table_id];
+    GP_CHECK_LT(server_id, num_processes_);
+    // An empty reply means the server has seen no updates for the table yet:
+    // the shard is all zeros, as the freshly zeroed cache already is.
+    GP_CHECK_MSG(num_rows == pc.server_num_rows[server_id] || num_rows == 0,
+                 "refresh of " << num_rows << " rows, expected " << pc.server_num_rows[server_id]);
+    iter_t &age = pc.per_server_data_age[server_id];
+    GP_CHECK_MSG(data_age > age, "old or duplicate data received: " << data_age << " vs " << age);
+    GP_CHECK_LE(data_age, self_clock);
+    age = data_age;
+    // server_clock_cbk: oplogs the servers have all applied can go.
+    GP_CHECK_LE(pc.server_clock[server_id], data_age);
+    pc.server_clock[server_id] = data_age;
+    const iter_t min_clock = *std::min_element(pc.server_clock.begin(), pc.server_clock.end());
+    if (min_clock > pc.server_clock_min) {
+      reclaim_oplogs(pc, min_clock);
+      pc.server_clock_min = min_clock;
+    }
+    if (num_rows) {
+      float *dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
+      const size_t floats = num_rows * ROW_DATA_SIZE;
+      GP_CALL(gp_memcpy_async(dst, rows, floats * 4, ch.recv_stream->get()));
+      if (config_.read_my_writes) {
+        // Re-apply this client's own not-yet-reflected updates
+        // (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
+        for (iter_t c = self_clock + 1, fc = fast_clock_.load(); c <= fc; ++c) {
+          auto it = pc.oplog.find(c);
+          if (it == pc.oplog.end()) continue;
+          const float *op = it->second->data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
+          GP_CALL(gp_add(floats, dst, op, dst, ch.recv_stream->get()));
+        }
+      }
+      ch.recv_stream->sync();
+    }
+    pc.data_age = *std::min_element(pc.per_server_data_age.begin(), pc.per_server_data_age.end());
+  }
+  ch.cv.notify_all();
+  (void)device;
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nr_refresh++;
+  stats_.refresh_time += now_s() - t0;
+}
+
+// ---------------------------------------------------------------------------
+// stats / shutdown (clientlib.cpp:185-263)
+// ---------------------------------------------------------------------------
+std::string ClientLib::json_stats() {
+  std::ostringstream o;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    o << "{\"process_id\": " << process_id_ << ", \"client\": " << stats_.to_json()
+      << ", \"servers\": [";
+  }
+  for (size_t c = 0; c < channels_.size(); ++c)
+    o << (c ? ", " : "") << channels_[c]->server->stats_json();
+  o << "]}";
+  const std::string json = o.str();
+  if (!config_.output_dir.empty()) {
+    std::ofstream f(config_.output_dir + "/json_stats." + std::to_string(process_id_),
+                    std::ofstream::out | std::ofstream::app);
+    f << json << std::endl;
+  }
+  return json;
+}
+
+// Shutdown handshake: every client tells every server it is done; a server
+// acknowledges all clients once all have; each process then tears down.  A peer
+// therefore never sees a connection close while it still expects a message.
+void ClientLib::shutdown() {
+  if (stopping_.exchange(true)) return;
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    for (uint32_t s = 0; s < num_processes_; ++s) {
+      if (s == process_id_) {
+        ch.server->post_shutdown(process_id_);
+      } else {
+        cs_clock_msg_t h{};
+        h.cmd = SHUTDOWN;
+        h.client_id = process_id_;
+        GP_CHECK(send_frame(ch.server_fd[s], {Part{&h, sizeof h}}));
+      }
+    }
+  }
+  for (auto &chp : channels_) chp->server->wait_shutdown();
+  for (auto &chp : channels_) {
+    for (auto &t : chp->client_readers)
+      if (t.joinable()) t.join();
+    for (auto &t : chp->server_readers)
+      if (t.joinable()) t.join();
+    chp->server->stop();
+    for (int fd : chp->server_fd) close_fd(fd);
+    for (int fd : chp->client_fd) close_fd(fd);
+    close_fd(chp->listen_fd);
+  }
+  GP_CALL(gp_device_synchronize());
+}
+
+void ClientLib::quiesce() {
+  if (stopping_.load()) return;
+  for (auto &chp : channels_) chp->server->drain();
+  gp_device_synchronize();
+}
+
+}  // namespace geeps

@@ -1,0 +1,193 @@
+#ifndef GEEPS_AMD_CLIENT_HPP_
+#define GEEPS_AMD_CLIENT_HPP_
+
+// Client library behind the GeePs facade (include/geeps.hpp).
+//
+// Mirrors the reference ClientLib (src/client/clientlib.hpp:419-602) on the
+// points the reduction path depends on:
+//   * virtual iteration: the op sequence, the param cache built in first-access
+//     order, rows split over channels (row / rows_per_channel,
+//     src/client/clientlib.cpp:216-224) and over servers by contiguous cache
+//     range (src/client/clientlib-viter.cpp:674-682), one DoubleIndex per
+//     READ / PRE_WRITE op grouped by channel (clientlib-viter.cpp:817-883);
+//   * Update(): the row-indexed scatter-add of the app's device buffer into the
+//     clock's oplog (update_batch_gpu, src/client/clientlib-data.cpp:346-396)
+//     — gp_scatter_add_rows;
+//   * clock push: each server gets its contiguous slice of the oplog
+//     (push_updates_param_cache, clientlib-data.cpp:436-522) — a zero-copy
+//     device slice for the in-process server, D2H + socket for remote ones;
+//   * refresh: the server's shard lands in the param cache
+//     (recv_row_batch_gpu, clientlib-data.cpp:110-151) and Read() gathers the
+//     op's rows (assign_rows_to_double_index) — gp_gather_rows.
+//
+// Everything lives in HBM (288 GB per MI355X): param cache, oplogs, op buffers
+// and local storage; there is no CPU param-cache tier.  API calls run on the
+// calling thread; device work is ordered on per-channel HIP streams and synced
+// before a call returns data to the app.
+
+#include <atomic>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "device.hpp"
+#include "geeps.hpp"
+#include "server.hpp"
+#include "wire.hpp"
+
+namespace geeps {
+
+struct OpInfo {
+  enum Type { READ, POST_READ, PRE_WRITE, WRITE, CLOCK };
+  Type type = CLOCK;
+  table_id_t table = 0;
+  std::vector<row_idx_t> rows;
+  iter_t slack = 0;
+  size_t num_vals_limit = 0;
+  bool local = false;
+  bool fetch = false;
+  bool keep = false;
+  int prestep_handle = -1;
+
+  // Decided by FinishVirtualIteration.
+  uint32_t table_id = 0;
+  bool table_last_write = false;
+  DeviceArray<gp_double_index> index;  // channel-major
+  std::vector<size_t> ch_start, ch_size;
+  DeviceArray<float> buffer;           // READ / PRE_WRITE op buffer
+  float *local_ptr = nullptr;          // local READ: GPU-resident storage
+  bool in_use = false;
+};
+
+struct ParamCache {
+  std::unordered_map<row_idx_t, size_t> index;  // row id -> cache row
+  std::vector<RowKey> row_keys;
+  size_t num_rows = 0;
+  DeviceArray<float> data;                       // num_rows x 128, HBM
+  std::vector<size_t> server_row_start, server_num_rows;
+  std::map<iter_t, std::shared_ptr<DeviceArray<float>>> oplog;
+  std::vector<std::shared_ptr<DeviceArray<float>>> oplog_pool;
+  std::vector<iter_t> per_server_data_age;
+  iter_t data_age = INITIAL_DATA_AGE;
+  std::vector<iter_t> server_clock;
+  iter_t server_clock_min = INITIAL_DATA_AGE;
+};
+
+struct ClientStats {
+  uint64_t nr_read = 0, nr_update = 0, nr_clock = 0, nr_push = 0, nr_refresh = 0;
+  uint64_t rows_updated = 0, rows_read = 0, bytes_pushed_remote = 0;
+  double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
+  std::string to_json() const;
+};
+
+class ClientLib;
+
+// Per-channel endpoint the tablet server replies through.
+class ChannelSink : public ClientSink {
+ public:
+  ChannelSink(ClientLib *lib, uint32_t channel) : lib_(lib), channel_(channel) {}
+  void read_row_batch_reply(uint32_t client_id, const RowBatchReply &reply) override;
+  void shutdown_ack(uint32_t client_id) override;
+
+ private:
+  ClientLib *lib_;
+  uint32_t channel_;
+};
+
+struct Channel {
+  uint32_t id = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<ParamCache> tables;
+  std::unique_ptr<Stream> stream, recv_stream, send_stream, reply_stream;
+  std::unique_ptr<ChannelSink> sink;
+  std::unique_ptr<TabletServer> server;
+  // client side: one socket per remote server (-1 = in-process server)
+  std::vector<int> server_fd;
+  std::vector<std::thread> client_readers;
+  PinnedArray<float> send_buf;
+  // server side: one socket per remote client
+  int listen_fd = -1;
+  std::vector<int> client_fd;
+  std::vector<std::thread> server_readers;
+  PinnedArray<float> reply_buf;
+};
+
+class ClientLib {
+ public:
+  ClientLib(uint32_t process_id, const GeePsConfig &config);
+  ~ClientLib();
+
+  // virtual iteration (clientlib-viter.cpp:69-118)
+  int virtual_op(OpInfo &&op);
+  void finish_virtual_iteration();
+  void start_iterations();
+
+  // real accesses (clientlib.cpp:349-625)
+  bool read_batch(RowData **buffer, int handle);
+  void postread_batch(int handle);
+  void preupdate_batch(RowOpVal **buffer, int handle);
+  void update_batch(int handle);
+  void iterate();
+
+  std::string json_stats();
+  void shutdown();
+
+  // server -> client refresh (recv_row_batch, clientlib-data.cpp:51-108)
+  void recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id, iter_t data_age,
+                      iter_t self_clock, const float *rows, size_t num_rows, bool device);
+  void remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r);
+  void remote_shutdown_ack(uint32_t channel, uint32_t client_id);
+  // Let in-flight device work finish (process exit without Shutdown()).
+  void quiesce();
+
+ private:
+  void check_handle(int handle);
+  uint32_t channel_of(uint32_t table_id, row_idx_t row) const;
+  void create_double_index(OpInfo &op);
+  void clock_all(iter_t clock);
+  void clock_table(iter_t clock, uint32_t table_id);
+  void push_updates(Channel &ch, iter_t clock, uint32_t table_id);
+  std::shared_ptr<DeviceArray<float>> get_oplog(ParamCache &pc, iter_t clock, gp_stream s);
+  void reclaim_oplogs(ParamCache &pc, iter_t upto);
+  void start_network();
+  void server_accept_loop(Channel &ch, int expected);
+  void server_reader(Channel &ch, uint32_t client_id, int fd);
+  void client_reader(Channel &ch, uint32_t server_id, int fd);
+  uint16_t port_of(uint32_t process, uint32_t channel) const;
+
+  const uint32_t process_id_;
+  const GeePsConfig config_;
+  const uint32_t num_processes_;
+  const uint32_t num_channels_;
+  int device_ = 0;
+
+  std::vector<OpInfo> opseq_;
+  std::map<std::vector<row_idx_t>, std::unique_ptr<DeviceArray<float>>> local_storage_;
+  std::vector<size_t> rows_per_channel_;
+  std::vector<std::unique_ptr<Channel>> channels_;
+
+  iter_t iteration_ = 0;
+  std::atomic<iter_t> fast_clock_{0};
+  int last_handle_ = -1;
+  bool finished_vi_ = false;
+  bool started_ = false;
+  std::atomic<bool> stopping_{false};
+  std::thread accept_thread_;
+
+  std::mutex stats_mu_;
+  ClientStats stats_;
+};
+
+// The process-wide instance (the reference's `client_lib` singleton,
+// src/client/clientlib.hpp:419-602).
+extern ClientLib *client_lib;
+
+}  // namespace geeps
+
+#endif  // GEEPS_AMD_CLIENT_HPP_

@@ -1,0 +1,124 @@
+#ifndef GEEPS_AMD_DEVICE_HPP_
+#define GEEPS_AMD_DEVICE_HPP_
+
+// RAII owners for device memory, pinned host memory, streams and events, all
+// through the C-ABI (include/gp_reduce.h) so that no HIP type appears in the
+// host library.
+
+#include <cstddef>
+#include <utility>
+
+#include "check.hpp"
+#include "gp_reduce.h"
+
+namespace geeps {
+
+class Stream {
+ public:
+  Stream() { GP_CALL(gp_stream_create(&s_)); }
+  ~Stream() {
+    if (s_) gp_stream_destroy(s_);
+  }
+  Stream(const Stream &) = delete;
+  Stream &operator=(const Stream &) = delete;
+  gp_stream get() const { return s_; }
+  void sync() const { GP_CALL(gp_stream_synchronize(s_)); }
+
+ private:
+  gp_stream s_ = nullptr;
+};
+
+class Event {
+ public:
+  Event() { GP_CALL(gp_event_create(&e_)); }
+  ~Event() {
+    if (e_) gp_event_destroy(e_);
+  }
+  Event(const Event &) = delete;
+  Event &operator=(const Event &) = delete;
+  void record(const Stream &s) { GP_CALL(gp_event_record(e_, s.get())); }
+  void sync() { GP_CALL(gp_event_synchronize(e_)); }
+  gp_event get() const { return e_; }
+
+ private:
+  gp_event e_ = nullptr;
+};
+
+// A device (HBM) array of T.
+template <typename T>
+class DeviceArray {
+ public:
+  DeviceArray() = default;
+  explicit DeviceArray(size_t n) { resize(n); }
+  ~DeviceArray() { release(); }
+  DeviceArray(const DeviceArray &) = delete;
+  DeviceArray &operator=(const DeviceArray &) = delete;
+  DeviceArray(DeviceArray &&o) noexcept { swap(o); }
+  DeviceArray &operator=(DeviceArray &&o) noexcept {
+    if (this != &o) {
+      release();
+      swap(o);
+    }
+    return *this;
+  }
+  void resize(size_t n) {
+    release();
+    if (n) {
+      void *p = nullptr;
+      GP_CALL(gp_malloc_device(&p, n * sizeof(T)));
+      p_ = static_cast<T *>(p);
+    }
+    n_ = n;
+  }
+  void release() {
+    if (p_) GP_CALL(gp_free_device(p_));
+    p_ = nullptr;
+    n_ = 0;
+  }
+  void swap(DeviceArray &o) noexcept {
+    std::swap(p_, o.p_);
+    std::swap(n_, o.n_);
+  }
+  T *data() const { return p_; }
+  size_t size() const { return n_; }
+  size_t bytes() const { return n_ * sizeof(T); }
+
+ private:
+  T *p_ = nullptr;
+  size_t n_ = 0;
+};
+
+// Page-locked host memory (the reference's mallocHost, common-util.hpp).
+template <typename T>
+class PinnedArray {
+ public:
+  PinnedArray() = default;
+  explicit PinnedArray(size_t n) { resize(n); }
+  ~PinnedArray() { release(); }
+  PinnedArray(const PinnedArray &) = delete;
+  PinnedArray &operator=(const PinnedArray &) = delete;
+  void resize(size_t n) {
+    release();
+    if (n) {
+      void *p = nullptr;
+      GP_CALL(gp_malloc_host(&p, n * sizeof(T)));
+      p_ = static_cast<T *>(p);
+    }
+    n_ = n;
+  }
+  void release() {
+    if (p_) GP_CALL(gp_free_host(p_));
+    p_ = nullptr;
+    n_ = 0;
+  }
+  T *data() const { return p_; }
+  size_t size() const { return n_; }
+
+ private:
+  T *p_ = nullptr;
+  size_t n_ = 0;
+};
+
+}  // namespace geeps
+
+#endif  // GEEPS_AMD_DEVICE_HPP_

@@ -1,0 +1,259 @@
+// Tablet server — see server.hpp.  Reference: src/server/tablet-server.cpp.
+#include "server.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <future>
+#include <sstream>
+
+#include "check.hpp"
+
+namespace geeps {
+
+namespace {
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+std::string ServerStats::to_json() const {
+  std::ostringstream o;
+  o << "{\"nr_update\": " << nr_update << ", \"nr_local_update\": " << nr_local_update
+    << ", \"nr_clock\": " << nr_clock << ", \"nr_refresh\": " << nr_refresh
+    << ", \"nr_apply_launches\": " << nr_apply_launches
+    << ", \"nr_buckets_applied\": " << nr_buckets_applied
+    << ", \"apply_time\": " << apply_time << ", \"stage_time\": " << stage_time
+    << ", \"refresh_time\": " << refresh_time << "}";
+  return o.str();
+}
+
+TabletServer::TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num_clients,
+                           uint32_t num_tables, ClientSink *sink)
+    : server_id_(server_id), channel_id_(channel_id), num_clients_(num_clients), sink_(sink) {
+  GP_CHECK(sink_);
+  GP_CHECK(num_clients_ > 0);
+  tables_.resize(num_tables);
+  for (auto &t : tables_) t.vec_clock.assign(num_clients_, INITIAL_DATA_AGE);
+  thread_ = std::thread([this] { run(); });
+}
+
+TabletServer::~TabletServer() { stop(); }
+
+void TabletServer::post_updates(UpdateBatch &&batch) {
+  Msg m{Msg::kUpdates, std::move(batch)};
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    queue_.push_back(std::move(m));
+  }
+  cv_.notify_one();
+}
+
+void TabletServer::post_clock(uint32_t client_id, iter_t clock, uint32_t table_id) {
+  Msg m{Msg::kClock, UpdateBatch{}};
+  m.client_id = client_id;
+  m.clock = clock;
+  m.table_id = table_id;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    queue_.push_back(std::move(m));
+  }
+  cv_.notify_one();
+}
+
+void TabletServer::post_shutdown(uint32_t client_id) {
+  Msg m{Msg::kShutdown, UpdateBatch{}};
+  m.client_id = client_id;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    queue_.push_back(std::move(m));
+  }
+  cv_.notify_one();
+}
+
+void TabletServer::wait_shutdown() {
+  std::unique_lock<std::mutex> lk(mu_);
+  shutdown_cv_.wait(lk, [this] { return shutdown_done_; });
+}
+
+void TabletServer::drain() {
+  if (!thread_.joinable()) return;
+  std::promise<void> p;
+  auto f = p.get_future();
+  Msg m{Msg::kDrain, UpdateBatch{}};
+  m.done = [&p] { p.set_value(); };
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    queue_.push_back(std::move(m));
+  }
+  cv_.notify_one();
+  f.wait();
+}
+
+std::string TabletServer::stats_json() {
+  if (!thread_.joinable()) return stats_.to_json();
+  std::promise<std::string> p;
+  auto f = p.get_future();
+  Msg m{Msg::kDrain, UpdateBatch{}};
+  m.done = [this, &p] { p.set_value(stats_.to_json()); };
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    queue_.push_back(std::move(m));
+  }
+  cv_.notify_one();
+  return f.get();
+}
+
+void TabletServer::stop() {
+  if (!thread_.joinable()) return;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    queue_.push_back(Msg{Msg::kStop, UpdateBatch{}});
+  }
+  cv_.notify_one();
+  thread_.join();
+}
+
+void TabletServer::run() {
+  for (;;) {
+    Msg m{Msg::kStop, UpdateBatch{}};
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this] { return !queue_.empty(); });
+      m = std::move(queue_.front());
+      queue_.pop_front();
+    }
+    switch (m.kind) {
+      case Msg::kUpdates: {
+        // CLOCK_WITH_UPDATES_BATCH: update_row_batch() then clock()
+        // (server-encoder-decoder.cpp:104-110).
+        const uint32_t c = m.batch.client_id, tb = m.batch.table_id;
+        const iter_t ck = m.batch.clock;
+        update_row_batch(m.batch);
+        clock(c, ck, tb);
+        break;
+      }
+      case Msg::kClock:
+        clock(m.client_id, m.clock, m.table_id);
+        break;
+      case Msg::kShutdown:
+        // Per-connection order guarantees the client's updates and clocks
+        // were all processed before its SHUTDOWN.
+        if (++shutdown_count_ == num_clients_) {
+          for (auto &t : tables_) apply_pending(t);
+          for (uint32_t c = 0; c < num_clients_; ++c) sink_->shutdown_ack(c);
+          std::lock_guard<std::mutex> lk(mu_);
+          shutdown_done_ = true;
+          shutdown_cv_.notify_all();
+        }
+        break;
+      case Msg::kDrain:
+        if (m.done) m.done();
+        break;
+      case Msg::kStop:
+        return;
+    }
+  }
+}
+
+std::shared_ptr<DeviceArray<float>> TabletServer::stage_buffer(DataTable &t) {
+  for (auto &b : t.stage_pool)
+    if (b.use_count() == 1) return b;  // not referenced by a pending bucket
+  t.stage_pool.push_back(std::make_shared<DeviceArray<float>>(t.row_count * ROW_DATA_SIZE));
+  return t.stage_pool.back();
+}
+
+// TabletStorage::update_row_batch (src/server/tablet-server.cpp:81-117).
+void TabletServer::update_row_batch(UpdateBatch &b) {
+  const size_t batch_size = b.keys.size();
+  stats_.nr_update += batch_size;
+  if (b.client_id == server_id_) stats_.nr_local_update += batch_size;
+  GP_CHECK_LT(b.table_id, tables_.size());
+  DataTable &t = tables_[b.table_id];
+  GP_CHECK_LT(b.client_id, t.vec_clock.size());
+  const iter_t cur = t.vec_clock[b.client_id];
+  GP_CHECK_MSG(cur == INITIAL_DATA_AGE || b.clock == cur + 1,
+               "CS clocks out of sync, client = " << b.client_id << " clock = " << b.clock
+                                                  << " cur_clock = " << cur);
+  if (batch_size == 0) return;
+  if (t.row_count == 0) {
+    // The first message defines the shard: zeroed master, keys copied
+    // (tablet-server.cpp:108-114).  Later messages are summed positionally.
+    t.row_count = batch_size;
+    t.master.resize(batch_size * ROW_DATA_SIZE);
+    GP_CALL(gp_zero(t.master.data(), t.master.size(), stream_.get()));
+    t.row_keys = b.keys;
+  }
+  GP_CHECK_EQ(t.row_count, batch_size);
+
+  Pending p;
+  if (b.device_rows) {
+    p.rows = b.device_rows;
+    p.keepalive = std::move(b.keepalive);
+  } else {
+    GP_CHECK(b.host_rows && b.host_rows->size() >= batch_size * ROW_DATA_SIZE);
+    const double t0 = now_s();
+    auto stage = stage_buffer(t);
+    GP_CALL(gp_memcpy_async(stage->data(), b.host_rows->data(),
+                            batch_size * ROW_DATA_SIZE * sizeof(float), stream_.get()));
+    stream_.sync();  // host buffer is released when `b` dies
+    stats_.stage_time += now_s() - t0;
+    p.rows = stage->data();
+    p.keepalive = stage;
+  }
+  t.pending.push_back(std::move(p));
+  if (t.pending.size() >= kMaxPendingBuckets) apply_pending(t);
+}
+
+// All queued buckets in arrival order, one launch: master = ((m + b0) + b1) ...
+void TabletServer::apply_pending(DataTable &t) {
+  if (t.pending.empty()) return;
+  const double t0 = now_s();
+  std::vector<const float *> ptrs;
+  ptrs.reserve(t.pending.size());
+  for (auto &p : t.pending) ptrs.push_back(p.rows);
+  GP_CALL(gp_bucket_sum_apply(t.master.data(), ptrs.data(), (int)ptrs.size(),
+                              t.row_count * ROW_DATA_SIZE, stream_.get()));
+  stream_.sync();
+  stats_.nr_apply_launches++;
+  stats_.nr_buckets_applied += ptrs.size();
+  t.pending.clear();  // releases oplog slices / staging buffers
+  stats_.apply_time += now_s() - t0;
+}
+
+// TabletStorage::clock (src/server/tablet-server.cpp:169-212).
+void TabletServer::clock(uint32_t client_id, iter_t clock, uint32_t table_id) {
+  stats_.nr_clock++;
+  GP_CHECK_LT(table_id, tables_.size());
+  DataTable &t = tables_[table_id];
+  GP_CHECK_LT(client_id, t.vec_clock.size());
+  if (t.vec_clock[client_id] != INITIAL_DATA_AGE) GP_CHECK_EQ(clock, t.vec_clock[client_id] + 1);
+  t.vec_clock[client_id] = clock;
+  const iter_t new_global = *std::min_element(t.vec_clock.begin(), t.vec_clock.end());
+  if (new_global != t.global_clock) {
+    if (t.global_clock != INITIAL_DATA_AGE) GP_CHECK_EQ(new_global, t.global_clock + 1);
+    t.global_clock = new_global;
+    send_refresh(table_id);
+  }
+}
+
+// process_multiclient_pending_reads (tablet-server.cpp:136-163): the whole
+// shard to every client, starting client rotated by the clock.
+void TabletServer::send_refresh(uint32_t table_id) {
+  DataTable &t = tables_[table_id];
+  apply_pending(t);
+  const double t0 = now_s();
+  const iter_t n = (iter_t)num_clients_;
+  const uint32_t start = (uint32_t)(((t.global_clock % n) + n) % n);
+  for (uint32_t i = 0; i < num_clients_; ++i) {
+    const uint32_t c = (start + i) % num_clients_;
+    RowBatchReply r{server_id_, t.global_clock, t.vec_clock[c], table_id,
+                    t.row_keys.data(), t.master.data(), t.row_count};
+    sink_->read_row_batch_reply(c, r);
+  }
+  stats_.nr_refresh++;
+  stats_.refresh_time += now_s() - t0;
+}
+
+}  // namespace geeps

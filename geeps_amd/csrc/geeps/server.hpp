@@ -1,0 +1,161 @@
+#ifndef GEEPS_AMD_SERVER_HPP_
+#define GEEPS_AMD_SERVER_HPP_
+
+// Tablet server: the server half of the gradient-update reduction path.
+//
+// One TabletServer runs per (process, communication channel), as the
+// reference's ServerThreadEntry does (src/server/server-entry.cpp:51-88).  It
+// owns, per table, the master copy of this server's row shard in HBM and the
+// vector clock of its clients, and serves two messages:
+//
+//   CLOCK_WITH_UPDATES_BATCH  -> update_row_batch() then clock()
+//                                (ClientServerDecode::clock_with_updates_batch,
+//                                 src/server/server-encoder-decoder.cpp:86-113)
+//   CLOCK                     -> clock()
+//
+// The reference adds every arriving update into the CPU master immediately
+// (TabletStorage::apply_updates -> cpu_add, src/server/tablet-server.cpp:119-134).
+// Here arriving update batches queue as device buckets in arrival order and
+// are summed into the master by ONE gp_bucket_sum_apply launch right before the
+// master is observed (the refresh sent when the global clock advances), or
+// when the queue reaches kMaxPendingBuckets.  The per-element order of fp32
+// adds is the arrival order in both cases, so the master is bit-identical to
+// the reference's; the device reads each bucket once and the master once per
+// refresh instead of once per client.
+
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "device.hpp"
+#include "wire.hpp"
+
+namespace geeps {
+
+// Rows of one client's clock update for one server: n keys and n RowOpVal.
+// Exactly one of `device_rows` (in-process client: a zero-copy slice of its
+// oplog, kept alive by `keepalive` until applied) or `host_rows` (received
+// from a socket into pinned memory) is set.
+struct UpdateBatch {
+  uint32_t client_id = 0;
+  iter_t clock = 0;
+  uint32_t table_id = 0;
+  std::vector<RowKey> keys;
+  const float *device_rows = nullptr;
+  std::shared_ptr<void> keepalive;
+  std::shared_ptr<PinnedArray<float>> host_rows;
+};
+
+// The refreshed shard, as the server hands it to a client sink.  `device_rows`
+// stays valid only for the duration of the sink call.
+struct RowBatchReply {
+  uint32_t server_id;
+  iter_t data_age;
+  iter_t self_clock;
+  uint32_t table_id;
+  const RowKey *keys;
+  const float *device_rows;
+  size_t num_rows;
+};
+
+// Where the server sends refreshed shards (ServerClientEncode::read_row_batch_reply,
+// src/server/server-encoder-decoder.cpp:228-250).
+class ClientSink {
+ public:
+  virtual ~ClientSink() = default;
+  virtual void read_row_batch_reply(uint32_t client_id, const RowBatchReply &reply) = 0;
+  // Every client has said SHUTDOWN: nothing more will be sent to `client_id`.
+  virtual void shutdown_ack(uint32_t client_id) = 0;
+};
+
+struct ServerStats {
+  uint64_t nr_update = 0;        // rows received (tablet-server.hpp stats)
+  uint64_t nr_local_update = 0;
+  uint64_t nr_clock = 0;
+  uint64_t nr_refresh = 0;
+  uint64_t nr_apply_launches = 0;
+  uint64_t nr_buckets_applied = 0;
+  double apply_time = 0;         // s, including the launch sync
+  double stage_time = 0;         // s, H2D of socket-delivered buckets
+  double refresh_time = 0;       // s, sending refreshed shards
+  std::string to_json() const;
+};
+
+class TabletServer {
+ public:
+  static constexpr size_t kMaxPendingBuckets = 8;
+
+  TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num_clients,
+               uint32_t num_tables, ClientSink *sink);
+  ~TabletServer();
+  TabletServer(const TabletServer &) = delete;
+  TabletServer &operator=(const TabletServer &) = delete;
+
+  // Thread-safe; processed in posting order by the server thread.
+  void post_updates(UpdateBatch &&batch);
+  void post_clock(uint32_t client_id, iter_t clock, uint32_t table_id);
+  // Client `client_id` will send nothing more.  Once every client has said so,
+  // each is acknowledged through ClientSink::shutdown_ack.
+  void post_shutdown(uint32_t client_id);
+  // Blocks until every client has sent SHUTDOWN and all were acknowledged.
+  void wait_shutdown();
+  // Blocks until every message posted before it has been processed.
+  void drain();
+  void stop();
+  std::string stats_json();
+
+  uint32_t server_id() const { return server_id_; }
+
+ private:
+  struct Pending {
+    const float *rows;
+    std::shared_ptr<void> keepalive;
+  };
+  struct DataTable {
+    std::vector<iter_t> vec_clock;
+    iter_t global_clock = INITIAL_DATA_AGE;
+    size_t row_count = 0;
+    std::vector<RowKey> row_keys;
+    DeviceArray<float> master;
+    std::vector<Pending> pending;
+    std::vector<std::shared_ptr<DeviceArray<float>>> stage_pool;
+  };
+  struct Msg {
+    enum Kind { kUpdates, kClock, kShutdown, kDrain, kStop } kind;
+    UpdateBatch batch;
+    uint32_t client_id = 0;
+    iter_t clock = 0;
+    uint32_t table_id = 0;
+    std::function<void()> done;
+  };
+
+  void run();
+  void update_row_batch(UpdateBatch &batch);
+  void clock(uint32_t client_id, iter_t clock, uint32_t table_id);
+  void apply_pending(DataTable &t);
+  void send_refresh(uint32_t table_id);
+  std::shared_ptr<DeviceArray<float>> stage_buffer(DataTable &t);
+
+  const uint32_t server_id_, channel_id_, num_clients_;
+  ClientSink *sink_;
+  std::vector<DataTable> tables_;
+  Stream stream_;
+  ServerStats stats_;
+
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Msg> queue_;
+  uint32_t shutdown_count_ = 0;  // server thread only
+  bool shutdown_done_ = false;    // guarded by mu_
+  std::condition_variable shutdown_cv_;
+  std::thread thread_;
+};
+
+}  // namespace geeps
+
+#endif  // GEEPS_AMD_SERVER_HPP_

@@ -156,10 +156,15 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
   size_t done = 0;
   if (vec && n >= 4) {
-    constexpr int U = NB <= 2 ? 4 : (NB <= 5 ? 2 : 1);
+    // 4 block-strides per thread at 2 blocks per CU: (NB + 1) * 4 dwordx4 loads
+    // in flight per lane.  Measured on MI355X at 8 x 4 GiB buckets: +2-3 % over
+    // 1 stride at 8 blocks/CU (profiles/r01/bucket_tune_sweep*.txt).
+    constexpr int U = 4;
+    constexpr int kPerCU = NB <= 2 ? 4 : 2;
     const size_t n4 = n / 4;
     const size_t tiles = (n4 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    const size_t grid = tiles < grid_cap() ? tiles : grid_cap();
+    const size_t cap = (size_t)num_cus() * kPerCU;
+    const size_t grid = tiles < cap ? tiles : cap;
     hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U>), dim3((unsigned)grid),
                        dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out),
                        reinterpret_cast<const f4 *>(in), b, n4);

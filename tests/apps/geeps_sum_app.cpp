@@ -1,0 +1,148 @@
+// geeps_sum_app — drives libgeeps through the unchanged public API
+// (include/geeps.hpp) the way a data-parallel app does, and checks every Read.
+//
+//   geeps_sum_app <process_id> <num_processes> <base_port> <rows> <clocks>
+//                 <slack> <channels> <read_my_writes> [float]
+//
+// Each process declares one table of `rows` RowData rows: Read(all rows,
+// slack), PreUpdate(all rows), PostRead, Update, Clock.  Process p's delta at
+// clock c for element e is a small integer (exact in fp32, so the check is
+// independent of the order in which the server received the processes'
+// updates).  With `float` and one process the deltas are random floats and the
+// expected value is the sequential fp32 sum (bit-exact).
+//
+// BSP (slack 0): the Read at iteration i must equal exactly the sum of every
+// process's deltas for clocks 0 .. i-1 (clock 0 is the setup clock before
+// StartIterations).  SSP: it must lie between the sums through clock
+// i-slack-1 and through clock i+slack (deltas are positive).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "geeps.hpp"
+
+static float delta(int p, int c, size_t e, bool fl) {
+  if (fl) {
+    uint32_t x = (uint32_t)(e * 2654435761u) ^ (uint32_t)(c * 40503u + p * 977u + 12345u);
+    x ^= x >> 13;
+    x *= 0x5bd1e995u;
+    x ^= x >> 15;
+    return (float)(x & 0xffffff) / 16777216.0f - 0.5f;
+  }
+  return (float)(1 + ((p * 7 + c * 3 + e) % 5));  // 1..5
+}
+
+#define HCK(x)                                                     \
+  do {                                                             \
+    hipError_t e_ = (x);                                           \
+    if (e_ != hipSuccess) {                                        \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); \
+      std::exit(3);                                                \
+    }                                                              \
+  } while (0)
+
+int main(int argc, char **argv) {
+  if (argc < 9) {
+    std::fprintf(stderr, "usage: %s pid nproc base_port rows clocks slack channels rmw [float]\n",
+                 argv[0]);
+    return 2;
+  }
+  const int pid = std::atoi(argv[1]), P = std::atoi(argv[2]), base = std::atoi(argv[3]);
+  const size_t rows = std::strtoull(argv[4], 0, 10);
+  const int clocks = std::atoi(argv[5]), slack = std::atoi(argv[6]);
+  const int channels = std::atoi(argv[7]), rmw = std::atoi(argv[8]);
+  const bool fl = argc > 9 && std::string(argv[9]) == "float";
+  if (fl && P != 1) {
+    std::fprintf(stderr, "float mode needs one process (order-independent check otherwise)\n");
+    return 2;
+  }
+  const size_t n = rows * ROW_DATA_SIZE;
+
+  GeePsConfig cfg;
+  for (int i = 0; i < P; ++i) {
+    cfg.host_list.push_back("127.0.0.1");
+    cfg.port_list.push_back(base + 16 * i);
+  }
+  cfg.num_comm_channels = channels;
+  cfg.read_my_writes = rmw;
+  cfg.gpu_memory_capacity = (size_t)1 << 34;
+  GeePs *ps = new GeePs(pid, cfg);
+
+  std::vector<size_t> ids(rows);
+  for (size_t r = 0; r < rows; ++r) ids[r] = r;
+  const int h_read = ps->VirtualRead(0, ids, slack);
+  const int h_pre = ps->VirtualPreUpdate(0, ids);
+  const int h_post = ps->VirtualPostRead(h_read);
+  const int h_upd = ps->VirtualUpdate(h_pre);
+  ps->VirtualClock();
+  ps->FinishVirtualIteration();
+
+  std::vector<float> host(n), got(n);
+  // PreUpdate -> fill on the device -> [PostRead] -> Update, in declared order.
+  auto push = [&](int c, bool post_read) {
+    RowOpVal *buf = nullptr;
+    ps->PreUpdate(h_pre, &buf);
+    for (size_t e = 0; e < n; ++e) host[e] = delta(pid, c, e, fl);
+    HCK(hipMemcpy(buf, host.data(), n * 4, hipMemcpyHostToDevice));
+    if (post_read) ps->PostRead(h_post);
+    ps->Update(h_upd);
+  };
+  // Expected sums through clock k, over all processes, in the order the
+  // single-process server applies them (k = -1: zeros).
+  std::vector<std::vector<float>> through(clocks + 2, std::vector<float>(n, 0.0f));
+  for (int k = 0; k <= clocks; ++k) {
+    through[k + 1] = through[k];
+    for (int p = 0; p < P; ++p)
+      for (size_t e = 0; e < n; ++e) through[k + 1][e] += delta(p, k, e, fl);
+  }
+  auto sum_through = [&](int k) -> const std::vector<float> & {
+    if (k < -1) k = -1;
+    if (k > clocks) k = clocks;
+    return through[k + 1];
+  };
+
+  // Setup clock (clock 0) before StartIterations, as apps/helloworld does.
+  push(0, false);
+  ps->Clock();
+  ps->StartIterations();
+
+  int bad = 0;
+  for (int it = 1; it <= clocks; ++it) {
+    RowData *rbuf = nullptr;
+    ps->Read(h_read, &rbuf);
+    HCK(hipMemcpy(got.data(), rbuf, n * 4, hipMemcpyDeviceToHost));
+    if (slack == 0 && !rmw) {
+      const auto &e = sum_through(it - 1);
+      for (size_t i = 0; i < n && bad < 5; ++i) {
+        if (std::memcmp(&got[i], &e[i], 4) != 0) {
+          std::fprintf(stderr, "p%d it%d elem %zu: got %.9g expected %.9g\n", pid, it, i, got[i], e[i]);
+          ++bad;
+        }
+      }
+    } else if (!fl) {
+      const auto &lo = sum_through(it - slack - 1);
+      const auto &hi = sum_through(it + slack + (rmw ? 1 : 0));
+      for (size_t i = 0; i < n && bad < 5; ++i) {
+        if (!(got[i] >= lo[i] && got[i] <= hi[i])) {
+          std::fprintf(stderr, "p%d it%d elem %zu: got %g outside [%g, %g]\n", pid, it, i, got[i],
+                       lo[i], hi[i]);
+          ++bad;
+        }
+      }
+    }
+    push(it, true);
+    ps->Clock();
+  }
+  std::string stats = ps->GetStats();
+  std::printf("%s p%d rows=%zu clocks=%d slack=%d channels=%d rmw=%d %s\n", bad ? "MISMATCH" : "OK",
+              pid, rows, clocks, slack, channels, rmw, fl ? "float" : "int");
+  std::printf("stats %s\n", stats.c_str());
+  std::fflush(stdout);
+  ps->Shutdown();
+  return bad ? 1 : 0;
+}

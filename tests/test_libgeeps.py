@@ -1,0 +1,128 @@
+"""The drop-in libgeeps behind the unchanged include/geeps.hpp.
+
+CPU: the library exports the reference's GeePs symbol set, and an app compiled
+against the public header links with -lgeeps alone.
+GPU: the reference's own apps/helloworld (compiled unchanged by build()) runs to
+its expected output, and tests/apps/geeps_sum_app checks every Read against
+exact sums across 1-3 processes over loopback TCP (BASELINE config 1: "2 local
+PS processes over loopback"), BSP and SSP, 1-2 channels, read-my-writes.
+"""
+import os
+import socket
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+LIB = os.path.join(REPO, "geeps_amd", "lib", "libgeeps.so")
+SUM_APP = os.path.join(REPO, "build", "tests", "geeps_sum_app")
+HELLO = os.path.join(REPO, "build", "ref_apps", "helloworld")
+
+# Every member of class GeePs in the reference header (include/geeps.hpp:73-98).
+GEEPS_SYMBOLS = [
+    "GeePs::GeePs(unsigned int, GeePsConfig const&)",
+    "GeePs::Shutdown()",
+    "GeePs::GetStats[abi:cxx11]()",
+    "GeePs::StartIterations()",
+    "GeePs::VirtualRead(unsigned long, std::vector<unsigned long, std::allocator<unsigned long> > const&, int)",
+    "GeePs::VirtualPostRead(int)",
+    "GeePs::VirtualPreUpdate(unsigned long, std::vector<unsigned long, std::allocator<unsigned long> > const&)",
+    "GeePs::VirtualUpdate(int)",
+    "GeePs::VirtualLocalAccess(std::vector<unsigned long, std::allocator<unsigned long> > const&, bool)",
+    "GeePs::VirtualPostLocalAccess(int, bool)",
+    "GeePs::VirtualClock()",
+    "GeePs::FinishVirtualIteration()",
+    "GeePs::Read(int, ArrayData**)",
+    "GeePs::PostRead(int)",
+    "GeePs::PreUpdate(int, ArrayData**)",
+    "GeePs::Update(int)",
+    "GeePs::LocalAccess(int, ArrayData**)",
+    "GeePs::PostLocalAccess(int)",
+    "GeePs::Clock()",
+]
+
+
+def test_libgeeps_exports_reference_symbol_set():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-DC", "--defined-only", LIB], check=True, capture_output=True,
+                         text=True).stdout
+    missing = [s for s in GEEPS_SYMBOLS if s not in out]
+    assert not missing, missing
+
+
+def test_app_links_with_public_header_only(tmp_path):
+    src = tmp_path / "app.cpp"
+    src.write_text('#include "geeps.hpp"\nint main() { GeePsConfig c; (void)c;\n'
+                   '  if (0) { GeePs g(0, c); int h = g.VirtualClock(); (void)h; g.Clock(); }\n'
+                   '  return 0; }\n')
+    subprocess.run(["g++", "-O2", str(src), "-I", os.path.join(REPO, "include"),
+                    "-L", os.path.dirname(LIB), "-lgeeps", "-o", str(tmp_path / "app")], check=True)
+
+
+def _ports(n_proc, channels):
+    """A base port with n_proc * 16 free ports above it (port_list[p] = base + 16 p)."""
+    for _ in range(50):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            base = s.getsockname()[1]
+        if base + 16 * n_proc + channels < 65000:
+            return base
+    raise RuntimeError("no port range")
+
+
+def _run_app(P, rows, clocks, slack, channels, rmw, mode="int", timeout=240):
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    base = _ports(P, channels)
+    procs = [subprocess.Popen([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
+                               str(channels), str(rmw), mode],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for p in range(P)]
+    outs = []
+    try:
+        for pr in procs:
+            o, e = pr.communicate(timeout=timeout)
+            outs.append((pr.returncode, o, e))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    for p, (rc, o, e) in enumerate(outs):
+        assert rc == 0 and o.startswith("OK"), f"process {p} rc={rc}\n{o}\n{e[-3000:]}"
+    return outs
+
+
+@pytest.mark.gpu
+def test_reference_helloworld_runs_unchanged(dev):
+    if not os.path.exists(HELLO):
+        pytest.skip("helloworld not built (needs /root/reference at build time)")
+    r = subprocess.run([HELLO], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert 'Finished "training", hello world!' in r.stdout
+
+
+@pytest.mark.gpu
+def test_single_process_float_bit_exact(dev):
+    _run_app(1, rows=512, clocks=6, slack=0, channels=1, rmw=0, mode="float")
+
+
+@pytest.mark.gpu
+def test_single_process_two_channels(dev):
+    _run_app(1, rows=1000, clocks=5, slack=0, channels=2, rmw=0)
+
+
+@pytest.mark.gpu
+def test_two_processes_loopback_bsp(dev):
+    # BASELINE config 1: 2 local PS processes over loopback, 1K x 64 fp32 = 512 RowData rows
+    _run_app(2, rows=512, clocks=10, slack=0, channels=1, rmw=0)
+
+
+@pytest.mark.gpu
+def test_three_processes_two_channels_ssp(dev):
+    _run_app(3, rows=777, clocks=8, slack=1, channels=2, rmw=0)
+
+
+@pytest.mark.gpu
+def test_two_processes_read_my_writes(dev):
+    _run_app(2, rows=300, clocks=6, slack=1, channels=1, rmw=1)
