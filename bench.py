@@ -62,6 +62,7 @@ def parse():
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=1 << 17)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-rowops", action="store_true")
     return p.parse_args()
 
 
@@ -170,6 +171,44 @@ def host_inclusive(rows, W, clients, dev, steps=3):
             "note": "pinned H2D of all client buckets + one N-way sum + D2H of the shard"}
 
 
+def rowops_leg(rows, W, dev, reps=5):
+    """The client half of the path at the same table size: the 1M x 1024 table
+    through the 128-float API is 8M RowData rows; one Update of all of them is a
+    row-indexed scatter-add into the oplog over a random-permutation DoubleIndex
+    (reference add_rows_from_double_index_gpu, row-op-util.cu:109-142), and one
+    Read is the gather back (assign_rows_to_double_index_gpu, :39-72).
+    Algorithmic bytes per launch: scatter-add 3*n*512 + 16*n, gather 2*n*512 + 16*n."""
+    from geeps_amd import rowops
+    R = rows * W // 128
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    perm = torch.randperm(R, generator=g, device=dev)
+    idx = torch.stack([torch.arange(R, device=dev), perm], 1).contiguous()
+    x = torch.rand(R * 128, generator=g, device=dev)
+    y = torch.zeros(R * 128, device=dev)
+    stream = torch.cuda.current_stream()
+    out = {}
+    for name, fn, nbytes in (
+            ("scatter_add", rowops.add_rows_from_double_index_gpu, 3 * R * 512 + 16 * R),
+            ("gather", rowops.assign_rows_to_double_index_gpu, 2 * R * 512 + 16 * R)):
+        fn(y, x, idx, R, (0, 0), 128, R * 128, validate=False)  # warm-up
+        ms = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn(y, x, idx, R, (0, 0), 128, R * 128, validate=False)
+            b.record(stream)
+            b.synchronize()
+            ms.append(a.elapsed_time(b))
+        avg = sum(ms) / len(ms)
+        gbps = nbytes / (avg / 1e3) / 1e9
+        out[name] = {"rows": R, "row_size": 128, "index": "random permutation",
+                     "avg_kernel_ms": round(avg, 4), "GBps": round(gbps, 1),
+                     "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_launch": nbytes,
+                     "traffic": load_traffic(f"rowops_{name}_r{R}_w128")}
+    return out
+
+
 def cpu_baseline(rows, W, clients, seconds):
     """The oracle's restatement of the reference server arithmetic, timed on the
     host (bounded sample).  1 thread = the reference's one server thread per
@@ -261,10 +300,15 @@ def main():
 
     host_inc = None
     cpu = None
+    rowops_res = None
     if rank == 0 and world == 1:
         del deltas
         red = None
         torch.cuda.empty_cache()
+        if not args.no_rowops:
+            log("[rank 0] client row-op leg")
+            rowops_res = rowops_leg(R, W, dev)
+            torch.cuda.empty_cache()
         if not args.no_host_inclusive:
             log("[rank 0] host-inclusive leg")
             host_inc = host_inclusive(R // 8, W, C, dev)
@@ -307,6 +351,8 @@ def main():
             line["exchange_inclusive"] = result_exchange
         if host_inc:
             line["host_inclusive"] = host_inc
+        if rowops_res:
+            line["client_rowops"] = rowops_res
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -220,6 +220,63 @@ __global__ __launch_bounds__(kB) void bsum_pol(f4 *__restrict__ out, const f4 *_
   }
 }
 
+
+// Diagnostic: same loads and adds, but the store goes to a 64 KiB L2-resident
+// window (wrong results) — separates the HBM write cost from everything else.
+template <int U>
+__global__ __launch_bounds__(kB) void bsum_fakestore(f4 *__restrict__ out, const f4 *__restrict__ in,
+                                                     Ptrs b, size_t n4) {
+  constexpr int NB = 8;
+  const size_t tile = (size_t)kB * U;
+  const size_t stride = (size_t)gridDim.x * tile;
+  size_t base = (size_t)blockIdx.x * tile + threadIdx.x;
+  for (; base + (U - 1) * kB < n4; base += stride) {
+    f4 acc[U];
+    f4 v[NB][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = in[base + u * kB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[k][u] = __builtin_nontemporal_load(b.p[k] + base + u * kB);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc[u] += v[k][u];
+      out[(base + u * kB) & 4095] = acc[u];
+    }
+  }
+}
+
+// R contiguous regions swept concurrently: block b works in region b % R.
+template <int U, int R>
+__global__ __launch_bounds__(kB) void bsum_regions(f4 *__restrict__ out, const f4 *__restrict__ in,
+                                                   Ptrs b, size_t n4) {
+  constexpr int NB = 8;
+  const size_t per = (n4 + R - 1) / R;
+  const unsigned reg = blockIdx.x % R, gb = gridDim.x / R, lb = blockIdx.x / R;
+  const size_t lo = reg * per, hi = (lo + per < n4) ? lo + per : n4;
+  const size_t tile = (size_t)kB * U;
+  const size_t stride = (size_t)gb * tile;
+  size_t base = lo + (size_t)lb * tile + threadIdx.x;
+  for (; base + (U - 1) * kB < hi; base += stride) {
+    f4 acc[U];
+    f4 v[NB][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = in[base + u * kB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[k][u] = __builtin_nontemporal_load(b.p[k] + base + u * kB);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc[u] += v[k][u];
+      out[base + u * kB] = acc[u];
+    }
+  }
+}
+
 __global__ void copy_k(f4 *__restrict__ out, const f4 *__restrict__ in, size_t n4) {
   const size_t stride = (size_t)gridDim.x * kB;
   for (size_t i = (size_t)blockIdx.x * kB + threadIdx.x; i < n4; i += stride) out[i] = in[i];
@@ -275,21 +332,21 @@ int main(int argc, char **argv) {
   };
 #define ADD(NAME, BYTES, ...) vs.push_back(V{NAME, BYTES, [&]() { __VA_ARGS__; }, {}})
   f4 *s4 = reinterpret_cast<f4 *>(scratch);
-  ADD("U1 ntB pc8 (prod)", sum_bytes, (bsum<8, 1, true, false, false><<<grid(8, 1), kB>>>(m4, m4, P, n4)));
-  ADD("U4 ntB pc2", sum_bytes, (bsum<8, 4, true, false, false><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
-  ADD("U4 ntB ntS pc2", sum_bytes, (bsum<8, 4, true, false, true><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
-  ADD("U2 ntB pc2", sum_bytes, (bsum<8, 2, true, false, false><<<grid(2, 2), kB>>>(m4, m4, P, n4)));
-  ADD("U4 ntB pc1", sum_bytes, (bsum<8, 4, true, false, false><<<grid(1, 4), kB>>>(m4, m4, P, n4)));
-  ADD("U2 ntB pc1", sum_bytes, (bsum<8, 2, true, false, false><<<grid(1, 2), kB>>>(m4, m4, P, n4)));
-  ADD("U1 oop pc8", sum_bytes, (bsum<8, 1, true, false, false><<<grid(8, 1), kB>>>(s4, m4, P, n4)));
-  ADD("U4 oop pc2", sum_bytes, (bsum<8, 4, true, false, false><<<grid(2, 4), kB>>>(s4, m4, P, n4)));
+  ADD("U4 pc2 (prod)", sum_bytes, (bsum<8, 4, true, false, false><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
+  ADD("U1 pc8 (r01 prod)", sum_bytes, (bsum<8, 1, true, false, false><<<grid(8, 1), kB>>>(m4, m4, P, n4)));
+  ADD("U2 pc1", sum_bytes, (bsum<8, 2, true, false, false><<<grid(1, 2), kB>>>(m4, m4, P, n4)));
+  ADD("U2 pc2", sum_bytes, (bsum<8, 2, true, false, false><<<grid(2, 2), kB>>>(m4, m4, P, n4)));
+  ADD("U3 pc2", sum_bytes, (bsum<8, 3, true, false, false><<<grid(2, 3), kB>>>(m4, m4, P, n4)));
+  ADD("U4 pc3", sum_bytes, (bsum<8, 4, true, false, false><<<grid(3, 4), kB>>>(m4, m4, P, n4)));
+  ADD("U4 fakestore pc2", 9.0 * n * 4, (bsum_fakestore<4><<<grid(2, 4), kB>>>(s4, m4, P, n4)));
+  ADD("U1 fakestore pc8", 9.0 * n * 4, (bsum_fakestore<1><<<grid(8, 1), kB>>>(s4, m4, P, n4)));
+  ADD("U4 reg2 pc2", sum_bytes, (bsum_regions<4, 2><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
+  ADD("U4 reg4 pc2", sum_bytes, (bsum_regions<4, 4><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
+  ADD("U4 reg8 pc2", sum_bytes, (bsum_regions<4, 8><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
+  ADD("U1 reg8 pc8", sum_bytes, (bsum_regions<1, 8><<<grid(8, 1), kB>>>(m4, m4, P, n4)));
   ADD("U4 st sc1 pc2", sum_bytes, (bsum_pol<4, 1><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
-  ADD("U4 st sc0sc1 pc2", sum_bytes, (bsum_pol<4, 2><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
-  ADD("U4 st ntsc1 pc2", sum_bytes, (bsum_pol<4, 3><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
-  ADD("U4 st all pc2", sum_bytes, (bsum_pol<4, 4><<<grid(2, 4), kB>>>(m4, m4, P, n4)));
-  ADD("U1 st sc1 pc8", sum_bytes, (bsum_pol<1, 1><<<grid(8, 1), kB>>>(m4, m4, P, n4)));
-  ADD("U1 st ntsc1 pc8", sum_bytes, (bsum_pol<1, 3><<<grid(8, 1), kB>>>(m4, m4, P, n4)));
   ADD("read9 only pc8", 9.0 * n * 4, (read_only<8><<<grid(8, 1), kB>>>(m4, m4, P, n4, 0)));
+  ADD("write1 only pc8", 1.0 * n * 4, (write_only<<<grid(8, 1), kB>>>(s4, n4)));
 
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
