@@ -48,7 +48,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -63,24 +63,33 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=1 << 17)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-rowops", action="store_true")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def init_dist(n_gpus):
+def init_dist(n_gpus, backend="nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "gloo":  # CPU rehearsal of the multi-rank flow (tests only)
+        if world > 1:
+            dist.init_process_group("gloo")
+        return (dist.get_rank() if world > 1 else 0), world, torch.device("cpu")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return (dist.get_rank() if world > 1 else 0), world, torch.device("cuda", local)
 
 
-def barrier(world):
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def barrier(world, dev):
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
 
 
 def max_over_ranks(x: float, world: int, dev) -> float:
@@ -105,32 +114,40 @@ def make_deltas(hosted, n, dev):
 def timed_apply(red, steps, warmup, world, dev):
     """Device-resident reduction: K launches, HIP events around each one on the
     launch stream, wall clock bracketed by barrier + synchronize."""
-    stream = torch.cuda.current_stream()
     for _ in range(warmup):
         red.apply()
+    if dev.type != "cuda":  # CPU rehearsal: wall clock only
+        barrier(world, dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            red.apply()
+        barrier(world, dev)
+        wall = time.perf_counter() - t0
+        return wall, [wall * 1e3 / steps] * steps
+    stream = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
-    barrier(world)
+    barrier(world, dev)
     t0 = time.perf_counter()
     for a, b in evs:
         a.record(stream)
         red.apply()
         b.record(stream)
     torch.cuda.synchronize()
-    barrier(world)
+    barrier(world, dev)
     wall = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     return wall, kernel_ms
 
 
-def timed_exchange(red, deltas, steps, warmup, world):
+def timed_exchange(red, deltas, steps, warmup, world, dev):
     for _ in range(warmup):
         red.step(deltas)
-    barrier(world)
+    barrier(world, dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         red.step(deltas)
-    barrier(world)
+    barrier(world, dev)
     return time.perf_counter() - t0
 
 
@@ -261,21 +278,24 @@ def load_traffic(workload_key):
         return None
 
 
-def main():
-    args = parse()
-    rank, world, dev = init_dist(args.gpus)
+def main(argv=None, backend="nccl", apply_fn=None):
+    """`backend="gloo"` + `apply_fn` exist only for tests/test_bench_dist.py, which
+    rehearses this multi-rank flow on CPU ranks; the benchmark itself always
+    runs nccl (RCCL) ranks on GPUs with the HIP kernel."""
+    args = parse(argv)
+    rank, world, dev = init_dist(args.gpus, backend)
     import geeps_amd
     from geeps_amd.shard import ShardedReducer
     geeps_amd.lib()  # the HIP library must be there; no fallback
 
     R, W, C = args.rows, args.width, args.clients
-    red = ShardedReducer(R, W, C, dev, exchange=args.exchange)
+    red = ShardedReducer(R, W, C, dev, exchange=args.exchange, apply_fn=apply_fn)
     L = red.layout
     log(f"[rank {rank}] shard rows [{L.row_start}, {L.row_start + L.local_rows}) "
         f"hosting clients {red.hosted}")
     deltas = make_deltas(red.hosted, R * W, dev)
     red.push(deltas)  # buckets resident on their shard
-    torch.cuda.synchronize()
+    _sync(dev)
 
     wall, kernel_ms = timed_apply(red, args.steps, args.warmup, world, dev)
     wall = max_over_ranks(wall, world, dev)
@@ -292,7 +312,7 @@ def main():
     workload_key = f"r{R}_w{W}_c{C}_g{world}"
     result_exchange = None
     if world > 1 and args.exchange_steps > 0:
-        ex = timed_exchange(red, deltas, args.exchange_steps, 1, world)
+        ex = timed_exchange(red, deltas, args.exchange_steps, 1, world, dev)
         ex = max_over_ranks(ex, world, dev) / args.exchange_steps
         result_exchange = {"ms_per_step": ex * 1e3, "value": delta_bytes / ex / 1e9,
                            "unit": "GB/s", "exchange": args.exchange,
@@ -301,7 +321,7 @@ def main():
     host_inc = None
     cpu = None
     rowops_res = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and dev.type == "cuda":
         del deltas
         red = None
         torch.cuda.empty_cache()
@@ -356,6 +376,7 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return line if rank == 0 else None
 
 
 if __name__ == "__main__":

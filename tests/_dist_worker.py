@@ -37,3 +37,15 @@ def run_shard(rank, world, port, num_rows, W, num_clients, exchange, steps, out_
         np.save(os.path.join(out_dir, f"hosted_{rank}.npy"), np.array(red.hosted))
     finally:
         dist.destroy_process_group()
+
+
+def run_bench(rank, world, port, argv, out_dir):
+    """bench.py's multi-rank flow on gloo CPU ranks (oracle as the apply step)."""
+    import json
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world)})
+    import bench
+    line = bench.main(argv, backend="gloo", apply_fn=oracle_apply)
+    if rank == 0:
+        with open(os.path.join(out_dir, "bench.json"), "w") as f:
+            json.dump(line, f)
