@@ -2,7 +2,11 @@
 // (include/geeps.hpp) the way a data-parallel app does, and checks every Read.
 //
 //   geeps_sum_app <process_id> <num_processes> <base_port> <rows> <clocks>
-//                 <slack> <channels> <read_my_writes> [float]
+//                 <slack> <channels> <read_my_writes> [int|float] [layers]
+//
+// `layers` (comma-separated row counts, summing to `rows`) switches to a
+// Caffe-like op sequence: a Read per parameter blob in forward order, then per
+// blob in reverse order PreUpdate / PostRead / Update, then Clock.
 //
 // Each process declares one table of `rows` RowData rows: Read(all rows,
 // slack), PreUpdate(all rows), PostRead, Update, Clock.  Process p's delta at
@@ -57,6 +61,19 @@ int main(int argc, char **argv) {
   const int clocks = std::atoi(argv[5]), slack = std::atoi(argv[6]);
   const int channels = std::atoi(argv[7]), rmw = std::atoi(argv[8]);
   const bool fl = argc > 9 && std::string(argv[9]) == "float";
+  std::vector<size_t> layer_rows;
+  if (argc > 10) {
+    std::string spec = argv[10];
+    size_t pos = 0;
+    while (pos < spec.size()) {
+      const size_t c = spec.find(',', pos);
+      layer_rows.push_back(std::strtoull(spec.substr(pos, c - pos).c_str(), 0, 10));
+      if (c == std::string::npos) break;
+      pos = c + 1;
+    }
+  } else {
+    layer_rows.push_back(std::strtoull(argv[4], 0, 10));
+  }
   if (fl && P != 1) {
     std::fprintf(stderr, "float mode needs one process (order-independent check otherwise)\n");
     return 2;
@@ -73,24 +90,42 @@ int main(int argc, char **argv) {
   cfg.gpu_memory_capacity = (size_t)1 << 34;
   GeePs *ps = new GeePs(pid, cfg);
 
-  std::vector<size_t> ids(rows);
-  for (size_t r = 0; r < rows; ++r) ids[r] = r;
-  const int h_read = ps->VirtualRead(0, ids, slack);
-  const int h_pre = ps->VirtualPreUpdate(0, ids);
-  const int h_post = ps->VirtualPostRead(h_read);
-  const int h_upd = ps->VirtualUpdate(h_pre);
+  size_t total = 0;
+  for (size_t r : layer_rows) total += r;
+  if (total != rows) {
+    std::fprintf(stderr, "layer rows sum to %zu, not %zu\n", total, rows);
+    return 2;
+  }
+  const size_t L = layer_rows.size();
+  std::vector<size_t> first(L);
+  std::vector<int> h_read(L), h_pre(L), h_post(L), h_upd(L);
+  for (size_t l = 0, r0 = 0; l < L; r0 += layer_rows[l], ++l) first[l] = r0;
+  auto ids_of = [&](size_t l) {
+    std::vector<size_t> ids(layer_rows[l]);
+    for (size_t r = 0; r < layer_rows[l]; ++r) ids[r] = first[l] + r;
+    return ids;
+  };
+  for (size_t l = 0; l < L; ++l) h_read[l] = ps->VirtualRead(0, ids_of(l), slack);
+  for (size_t l = L; l-- > 0;) {
+    h_pre[l] = ps->VirtualPreUpdate(0, ids_of(l));
+    h_post[l] = ps->VirtualPostRead(h_read[l]);
+    h_upd[l] = ps->VirtualUpdate(h_pre[l]);
+  }
   ps->VirtualClock();
   ps->FinishVirtualIteration();
 
   std::vector<float> host(n), got(n);
   // PreUpdate -> fill on the device -> [PostRead] -> Update, in declared order.
   auto push = [&](int c, bool post_read) {
-    RowOpVal *buf = nullptr;
-    ps->PreUpdate(h_pre, &buf);
-    for (size_t e = 0; e < n; ++e) host[e] = delta(pid, c, e, fl);
-    HCK(hipMemcpy(buf, host.data(), n * 4, hipMemcpyHostToDevice));
-    if (post_read) ps->PostRead(h_post);
-    ps->Update(h_upd);
+    for (size_t l = L; l-- > 0;) {
+      RowOpVal *buf = nullptr;
+      ps->PreUpdate(h_pre[l], &buf);
+      const size_t e0 = first[l] * ROW_DATA_SIZE, ne = layer_rows[l] * ROW_DATA_SIZE;
+      for (size_t e = 0; e < ne; ++e) host[e0 + e] = delta(pid, c, e0 + e, fl);
+      HCK(hipMemcpy(buf, host.data() + e0, ne * 4, hipMemcpyHostToDevice));
+      if (post_read) ps->PostRead(h_post[l]);
+      ps->Update(h_upd[l]);
+    }
   };
   // Expected sums through clock k, over all processes, in the order the
   // single-process server applies them (k = -1: zeros).
@@ -113,9 +148,12 @@ int main(int argc, char **argv) {
 
   int bad = 0;
   for (int it = 1; it <= clocks; ++it) {
-    RowData *rbuf = nullptr;
-    ps->Read(h_read, &rbuf);
-    HCK(hipMemcpy(got.data(), rbuf, n * 4, hipMemcpyDeviceToHost));
+    for (size_t l = 0; l < L; ++l) {
+      RowData *rbuf = nullptr;
+      ps->Read(h_read[l], &rbuf);
+      const size_t e0 = first[l] * ROW_DATA_SIZE, ne = layer_rows[l] * ROW_DATA_SIZE;
+      HCK(hipMemcpy(got.data() + e0, rbuf, ne * 4, hipMemcpyDeviceToHost));
+    }
     if (slack == 0 && !rmw) {
       const auto &e = sum_through(it - 1);
       for (size_t i = 0; i < n && bad < 5; ++i) {
@@ -139,8 +177,9 @@ int main(int argc, char **argv) {
     ps->Clock();
   }
   std::string stats = ps->GetStats();
-  std::printf("%s p%d rows=%zu clocks=%d slack=%d channels=%d rmw=%d %s\n", bad ? "MISMATCH" : "OK",
-              pid, rows, clocks, slack, channels, rmw, fl ? "float" : "int");
+  std::printf("%s p%d rows=%zu layers=%zu clocks=%d slack=%d channels=%d rmw=%d %s\n",
+              bad ? "MISMATCH" : "OK", pid, rows, L, clocks, slack, channels, rmw,
+              fl ? "float" : "int");
   std::printf("stats %s\n", stats.c_str());
   std::fflush(stdout);
   ps->Shutdown();

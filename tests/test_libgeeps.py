@@ -126,3 +126,77 @@ def test_three_processes_two_channels_ssp(dev):
 @pytest.mark.gpu
 def test_two_processes_read_my_writes(dev):
     _run_app(2, rows=300, clocks=6, slack=1, channels=1, rmw=1)
+
+
+# ---- BASELINE configs 4 and 5: layered param tables (Caffe is absent) ---------
+
+def _rows(count):
+    return (count + 127) // 128  # each blob padded to whole 128-float rows
+
+
+# bvlc_alexnet parameter blobs (weights, bias) with Caffe's grouped conv2/4/5:
+# 60,965,224 parameters in total.
+ALEXNET_BLOBS = [96 * 3 * 11 * 11, 96, 256 * 48 * 5 * 5, 256, 384 * 256 * 3 * 3, 384,
+                 384 * 192 * 3 * 3, 384, 256 * 192 * 3 * 3, 256, 4096 * 9216, 4096,
+                 4096 * 4096, 4096, 1000 * 4096, 1000]
+
+
+def inception_cifar_blobs():
+    """SYNTHESIZED Inception-style CIFAR-10 net (the GeePS Caffe submodule with
+    examples/cifar10/2parts is absent): conv 3->64, then 6 inception modules
+    (1x1 / 3x3-reduce+3x3 / 5x5-reduce+5x5 / pool-proj branches), then a 10-way fc."""
+    blobs, cin = [64 * 3 * 3 * 3, 64], 64
+    for b1, r3, b3, r5, b5, pp in [(32, 48, 64, 8, 16, 16), (64, 64, 96, 16, 48, 32),
+                                   (96, 48, 104, 8, 24, 32), (80, 56, 112, 12, 32, 32),
+                                   (64, 64, 128, 12, 32, 32), (112, 72, 144, 16, 32, 32)]:
+        for w in (b1 * cin, r3 * cin, b3 * r3 * 9, r5 * cin, b5 * r5 * 25, pp * cin):
+            blobs.append(w)
+        blobs += [b1, r3, b3, r5, b5, pp]
+        cin = b1 + b3 + b5 + pp
+    blobs += [10 * cin, 10]
+    return blobs
+
+
+def _layer_spec(blobs):
+    rows = [_rows(c) for c in blobs]
+    return sum(rows), ",".join(str(r) for r in rows)
+
+
+def test_alexnet_table_size():
+    assert sum(ALEXNET_BLOBS) == 60_965_224
+    rows, _ = _layer_spec(ALEXNET_BLOBS)
+    assert 476_000 < rows < 477_000
+
+
+@pytest.mark.gpu
+def test_config4_inception_cifar_two_workers(dev):
+    rows, spec = _layer_spec(inception_cifar_blobs())
+    _run_app_layers(2, rows, spec, clocks=5, slack=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_config5_alexnet_8_workers_8_shards_staleness_1(dev):
+    rows, spec = _layer_spec(ALEXNET_BLOBS)
+    _run_app_layers(8, rows, spec, clocks=4, slack=1, timeout=900)
+
+
+def _run_app_layers(P, rows, spec, clocks, slack, timeout=600):
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    base = _ports(P, 1)
+    procs = [subprocess.Popen([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
+                               "1", "0", "int", spec],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for p in range(P)]
+    outs = []
+    try:
+        for pr in procs:
+            o, e = pr.communicate(timeout=timeout)
+            outs.append((pr.returncode, o, e))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    for p, (rc, o, e) in enumerate(outs):
+        assert rc == 0 and o.startswith("OK"), f"process {p} rc={rc}\n{o}\n{e[-3000:]}"
