@@ -310,13 +310,23 @@ def main(argv=None, backend="nccl", apply_fn=None):
     achieved_min = max_over_ranks(-achieved, world, dev) * -1  # slowest rank
 
     workload_key = f"r{R}_w{W}_c{C}_g{world}"
-    result_exchange = None
+    result_exchange = []
     if world > 1 and args.exchange_steps > 0:
-        ex = timed_exchange(red, deltas, args.exchange_steps, 1, world, dev)
-        ex = max_over_ranks(ex, world, dev) / args.exchange_steps
-        result_exchange = {"ms_per_step": ex * 1e3, "value": delta_bytes / ex / 1e9,
-                           "unit": "GB/s", "exchange": args.exchange,
-                           "note": "RCCL exchange of the buckets + N-way sum + all-gather refresh"}
+        # Both exchanges: "a2a" (RCCL all-to-all, bit-exact client order) and
+        # "rs" (RCCL reduce-scatter, ring-order sum), each + N-way sum + all-gather.
+        for kind in (args.exchange, "rs" if args.exchange == "a2a" else "a2a"):
+            r = red if kind == args.exchange else ShardedReducer(R, W, C, dev, exchange=kind,
+                                                                 apply_fn=apply_fn)
+            ex = timed_exchange(r, deltas, args.exchange_steps, 1, world, dev)
+            ex = max_over_ranks(ex, world, dev) / args.exchange_steps
+            result_exchange.append({"ms_per_step": round(ex * 1e3, 3),
+                                    "value": round(delta_bytes / ex / 1e9, 2), "unit": "GB/s",
+                                    "exchange": kind,
+                                    "note": "RCCL bucket exchange + N-way sum + all-gather refresh"})
+            if r is not red:
+                del r
+                if dev.type == "cuda":
+                    torch.cuda.empty_cache()
 
     host_inc = None
     cpu = None
@@ -368,7 +378,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
             "cpu_baseline": cpu,
         }
         if result_exchange:
-            line["exchange_inclusive"] = result_exchange
+            line["exchange_inclusive"] = result_exchange[0]
+            line["exchange_inclusive_alt"] = result_exchange[1]
         if host_inc:
             line["host_inclusive"] = host_inc
         if rowops_res:

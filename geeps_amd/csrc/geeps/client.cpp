@@ -182,8 +182,11 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       b.client_id = h.client_id;
       b.clock = h.clock;
       b.table_id = h.table_id;
-      b.keys.resize(n);
-      if (n) std::memcpy(b.keys.data(), parts[1].data, parts[1].size);
+      auto keys = std::make_shared<std::vector<RowKey>>(n);
+      if (n) std::memcpy(keys->data(), parts[1].data, parts[1].size);
+      b.keys = keys->data();
+      b.num_rows = n;
+      b.keys_owner = keys;
       b.host_rows = ctx.rows;
       ch.server->post_updates(std::move(b));
     } else if (cmd == CLOCK) {
@@ -357,7 +360,7 @@ void ClientLib::finish_virtual_iteration() {
       for (row_idx_t r : keys[t]) {
         if (channel_of(t, r) != ch.id) continue;
         pc.index[r] = pc.num_rows++;
-        pc.row_keys.emplace_back(t, r);
+        pc.row_keys->emplace_back(t, r);
       }
       pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
       if (pc.num_rows) GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.stream->get()));
@@ -398,12 +401,54 @@ void ClientLib::finish_virtual_iteration() {
     create_double_index(op);
   }
   GP_CALL(gp_device_synchronize());
+  decide_fused_init();
   if (planned > config_.gpu_memory_capacity) {
     std::ostringstream o;
     o << "planned HBM use " << planned << " B exceeds gpu_memory_capacity "
       << config_.gpu_memory_capacity << " B";
     GP_CHECK_MSG(config_.mm_warning_level < 2, o.str());
     std::cerr << "libgeeps WARNING: " << o.str() << " (all data kept in HBM)\n";
+  }
+}
+
+// Per (channel, table): do the update ops of one clock (the WRITEs before the
+// first CLOCK op) write every oplog row exactly once, unguarded?  Then, after
+// StartIterations (when the op order is enforced), each op may write its rows as
+// 0.0f + x instead of zerofying the whole oplog and adding: bit-identical, one
+// pass fewer over the oplog (see gp_scatter_init_rows).
+void ClientLib::decide_fused_init() {
+  clock_handle_ = -1;
+  for (size_t i = 0; i < opseq_.size(); ++i)
+    if (opseq_[i].type == OpInfo::CLOCK) {
+      clock_handle_ = (int)i;
+      break;
+    }
+  const size_t end = clock_handle_ < 0 ? opseq_.size() : (size_t)clock_handle_;
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    ch.init_ok.assign(config_.num_tables, false);
+    if (clock_handle_ < 0) continue;
+    for (uint32_t t = 0; t < config_.num_tables; ++t) {
+      const ParamCache &pc = ch.tables[t];
+      std::vector<uint8_t> seen(pc.num_rows, 0);
+      size_t covered = 0;
+      bool ok = pc.num_rows > 0;
+      for (size_t i = 0; i < end && ok; ++i) {
+        const OpInfo &w = opseq_[i];
+        if (w.type != OpInfo::WRITE || w.local || w.table_id != t) continue;
+        const OpInfo &pre = opseq_[w.prestep_handle];
+        if (pre.num_vals_limit < pre.rows.size() * ROW_DATA_SIZE) ok = false;
+        // the op's id1 set in this channel is the contiguous range checked in
+        // create_double_index; recover it from the row ids
+        for (row_idx_t r : pre.rows) {
+          if (channel_of(t, r) != ch.id) continue;
+          const size_t id1 = pc.index.at(r);
+          if (seen[id1]++) ok = false;
+          ++covered;
+        }
+      }
+      ch.init_ok[t] = ok && covered == pc.num_rows;
+    }
   }
 }
 
@@ -534,7 +579,7 @@ void ClientLib::preupdate_batch(RowOpVal **buffer, int handle) {
 }
 
 std::shared_ptr<DeviceArray<float>> ClientLib::get_oplog(ParamCache &pc, iter_t clock,
-                                                         gp_stream s) {
+                                                         gp_stream s, bool zero) {
   auto it = pc.oplog.find(clock);
   if (it != pc.oplog.end()) return it->second;
   // create_oplog_entry + zerofy_data_gpu (clientlib.cpp:265-280,
@@ -550,7 +595,7 @@ std::shared_ptr<DeviceArray<float>> ClientLib::get_oplog(ParamCache &pc, iter_t 
     pc.oplog_pool.push_back(std::make_shared<DeviceArray<float>>(pc.num_rows * ROW_DATA_SIZE));
     buf = pc.oplog_pool.back();
   }
-  GP_CALL(gp_zero(buf->data(), pc.num_rows * ROW_DATA_SIZE, s));
+  if (zero) GP_CALL(gp_zero(buf->data(), pc.num_rows * ROW_DATA_SIZE, s));
   pc.oplog[clock] = buf;
   return buf;
 }
@@ -570,11 +615,18 @@ void ClientLib::update_batch(int handle) {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[pre.table_id];
     if (pc.num_rows == 0) continue;
-    auto oplog = get_oplog(pc, clock, ch.stream->get());
+    const bool fused = started_ && ch.init_ok[pre.table_id];
+    auto oplog = get_oplog(pc, clock, ch.stream->get(), /*zero=*/!fused);
     if (n) {
       const gp_double_index *idx = pre.index.data() + pre.ch_start[ch.id];
-      GP_CALL(gp_scatter_add_rows(oplog->data(), pre.buffer.data(), idx, n, gp_double_index{0, 0},
-                                  ROW_DATA_SIZE, pre.num_vals_limit, ch.stream->get()));
+      if (fused)
+        GP_CALL(gp_scatter_init_rows(oplog->data(), pre.buffer.data(), idx, n,
+                                     gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
+                                     ch.stream->get()));
+      else
+        GP_CALL(gp_scatter_add_rows(oplog->data(), pre.buffer.data(), idx, n,
+                                    gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
+                                    ch.stream->get()));
       if (config_.read_my_writes)
         GP_CALL(gp_scatter_add_rows(pc.data.data(), pre.buffer.data(), idx, n,
                                     gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
@@ -604,6 +656,12 @@ void ClientLib::iterate() {
     stats_.nr_clock++;
   }
   if (started_) {
+    // Every declared op of the iteration must have run (the reference's
+    // background workers replay the whole sequence; a skipped op would stall
+    // them), which is also what makes the fused oplog init safe.
+    GP_CHECK_MSG(clock_handle_ < 0 || last_handle_ == clock_handle_ - 1,
+                 "Clock() after handle " << last_handle_ << " but the iteration declares ops up to "
+                                         << clock_handle_ - 1);
     last_handle_ = -1;
   } else {
     clock_all(iteration_);
@@ -624,7 +682,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
   const double t0 = now_s();
   std::shared_ptr<DeviceArray<float>> oplog;
   std::vector<size_t> starts, counts;
-  std::vector<RowKey> keys;
+  std::shared_ptr<const std::vector<RowKey>> keys;  // immutable after FinishVirtualIteration
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[table_id];
@@ -657,7 +715,9 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       b.client_id = process_id_;
       b.clock = clock;
       b.table_id = table_id;
-      b.keys.assign(keys.begin() + a, keys.begin() + a + n);
+      b.keys = keys->data() + a;
+      b.num_rows = n;
+      b.keys_owner = keys;
       b.device_rows = oplog->data() + a * ROW_DATA_SIZE;
       b.keepalive = oplog;  // zero-copy: the server reads the oplog slice in place
       ch.server->post_updates(std::move(b));
@@ -675,7 +735,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       h.clock = clock;
       h.table_id = table_id;
       GP_CHECK(send_frame(ch.server_fd[s], {Part{&h, sizeof h},
-                                            Part{keys.data() + a, n * sizeof(RowKey)},
+                                            Part{keys->data() + a, n * sizeof(RowKey)},
                                             Part{ch.send_buf.data(), floats * 4}}));
       remote_bytes += floats * 4;
     }

@@ -66,7 +66,7 @@ struct OpInfo {
 
 struct ParamCache {
   std::unordered_map<row_idx_t, size_t> index;  // row id -> cache row
-  std::vector<RowKey> row_keys;
+  std::shared_ptr<std::vector<RowKey>> row_keys = std::make_shared<std::vector<RowKey>>();
   size_t num_rows = 0;
   DeviceArray<float> data;                       // num_rows x 128, HBM
   std::vector<size_t> server_row_start, server_num_rows;
@@ -104,6 +104,9 @@ struct Channel {
   std::mutex mu;
   std::condition_variable cv;
   std::vector<ParamCache> tables;
+  // Per table: the clock's update ops write every oplog row of this channel
+  // exactly once, so the first touch may be gp_scatter_init_rows (fused zero).
+  std::vector<bool> init_ok;
   std::unique_ptr<Stream> stream, recv_stream, send_stream, reply_stream;
   std::unique_ptr<ChannelSink> sink;
   std::unique_ptr<TabletServer> server;
@@ -153,7 +156,9 @@ class ClientLib {
   void clock_all(iter_t clock);
   void clock_table(iter_t clock, uint32_t table_id);
   void push_updates(Channel &ch, iter_t clock, uint32_t table_id);
-  std::shared_ptr<DeviceArray<float>> get_oplog(ParamCache &pc, iter_t clock, gp_stream s);
+  std::shared_ptr<DeviceArray<float>> get_oplog(ParamCache &pc, iter_t clock, gp_stream s,
+                                                bool zero);
+  void decide_fused_init();
   void reclaim_oplogs(ParamCache &pc, iter_t upto);
   void start_network();
   void server_accept_loop(Channel &ch, int expected);
@@ -175,6 +180,7 @@ class ClientLib {
   iter_t iteration_ = 0;
   std::atomic<iter_t> fast_clock_{0};
   int last_handle_ = -1;
+  int clock_handle_ = -1;  // index of the first CLOCK op
   bool finished_vi_ = false;
   bool started_ = false;
   std::atomic<bool> stopping_{false};

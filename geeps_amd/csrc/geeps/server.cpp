@@ -166,7 +166,7 @@ std::shared_ptr<DeviceArray<float>> TabletServer::stage_buffer(DataTable &t) {
 
 // TabletStorage::update_row_batch (src/server/tablet-server.cpp:81-117).
 void TabletServer::update_row_batch(UpdateBatch &b) {
-  const size_t batch_size = b.keys.size();
+  const size_t batch_size = b.num_rows;
   stats_.nr_update += batch_size;
   if (b.client_id == server_id_) stats_.nr_local_update += batch_size;
   GP_CHECK_LT(b.table_id, tables_.size());
@@ -183,7 +183,7 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
     t.row_count = batch_size;
     t.master.resize(batch_size * ROW_DATA_SIZE);
     GP_CALL(gp_zero(t.master.data(), t.master.size(), stream_.get()));
-    t.row_keys = b.keys;
+    t.row_keys.assign(b.keys, b.keys + batch_size);
   }
   GP_CHECK_EQ(t.row_count, batch_size);
 

@@ -45,7 +45,11 @@ struct UpdateBatch {
   uint32_t client_id = 0;
   iter_t clock = 0;
   uint32_t table_id = 0;
-  std::vector<RowKey> keys;
+  // n keys at `keys`, kept alive by `keys_owner` (the client's immutable
+  // param-cache key list, or the received frame's copy): never copied per push.
+  const RowKey *keys = nullptr;
+  size_t num_rows = 0;
+  std::shared_ptr<const void> keys_owner;
   const float *device_rows = nullptr;
   std::shared_ptr<void> keepalive;
   std::shared_ptr<PinnedArray<float>> host_rows;

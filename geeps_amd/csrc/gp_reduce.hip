@@ -208,6 +208,7 @@ enum RowOp : int {
   kAddFrom = 0,     // y[id1] += x[id0], guard on the x index
   kAssignTo = 1,    // y[id0]  = x[id1], guard on the y index
   kAssignFrom = 2,  // y[id1]  = x[id0], guard on the x index
+  kInitFrom = 3,    // y[id1]  = 0.0f + x[id0] (0.0f where the x index is guarded out)
 };
 
 template <int OP>
@@ -274,6 +275,8 @@ __global__ __launch_bounds__(kBlock) void row_op_kernel(
           if (live[k]) {
             if (OP == kAddFrom)
               yv[to[k] * vw + j] = ys[k] + xs[k];
+            else if (OP == kInitFrom)
+              yv[to[k] * vw + j] = T(0.0f) + xs[k];  // == zerofy then +=, -0 -> +0 included
             else
               yv[to[k] * vw + j] = xs[k];
           }
@@ -291,8 +294,12 @@ __global__ __launch_bounds__(kBlock) void row_op_kernel(
             const float xv1 = x[from[k] * row_size + e];
             if (OP == kAddFrom)
               y[to[k] * row_size + e] += xv1;
+            else if (OP == kInitFrom)
+              y[to[k] * row_size + e] = 0.0f + xv1;
             else
               y[to[k] * row_size + e] = xv1;
+          } else if (OP == kInitFrom) {
+            y[to[k] * row_size + e] = 0.0f;  // the zerofied value the add never touched
           }
         }
       }
@@ -383,6 +390,13 @@ int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
                     size_t num_vals_limit, gp_stream s) {
   return launch_row_op<kAssignFrom>(y, x, index, num_rows, offset, row_size,
                                     num_vals_limit, (hipStream_t)s);
+}
+
+int gp_scatter_init_rows(float *y, const float *x, const gp_double_index *index,
+                         size_t num_rows, gp_double_index offset, size_t row_size,
+                         size_t num_vals_limit, gp_stream s) {
+  return launch_row_op<kInitFrom>(y, x, index, num_rows, offset, row_size,
+                                  num_vals_limit, (hipStream_t)s);
 }
 
 int gp_bucket_sum_apply(float *master, const float *const *buckets,

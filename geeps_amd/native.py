@@ -39,6 +39,7 @@ _SIGNATURES = {
     "gp_scatter_add_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
+    "gp_scatter_init_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_bucket_sum_apply": (_i, [_vp, _c.POINTER(_vp), _i, _sz, _vp]),
     "gp_add": (_i, [_sz, _vp, _vp, _vp, _vp]),
     "gp_zero": (_i, [_vp, _sz, _vp]),

@@ -83,6 +83,7 @@ def _row_op(kind: str, rows_y, rows_x, index, num_rows, index_offset, row_size,
     if validate:
         _validate_bounds(kind, rows_y, rows_x, index[:num_rows], off, row_size, num_vals_limit)
     fn = {"add_from": native.lib().gp_scatter_add_rows,
+          "init_from": native.lib().gp_scatter_init_rows,
           "assign_to": native.lib().gp_gather_rows,
           "assign_from": native.lib().gp_scatter_rows}[kind]
     check(fn(rows_y.data_ptr(), rows_x.data_ptr(), index.data_ptr(), num_rows, off,
@@ -133,6 +134,15 @@ def add_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, index_o
     rows must be distinct within one call (as for the reference kernel).
     """
     _row_op("add_from", rows_y, rows_x, index, num_rows, index_offset, row_size,
+            num_vals_limit, stream, validate)
+
+
+def init_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, index_offset=None,
+                                    row_size=ROW_DATA_SIZE, num_vals_limit=None,
+                                    stream=None, validate=True) -> None:
+    """Fused ``zerofy_data_gpu`` + ``add_rows_from_double_index_gpu`` for the
+    listed destination rows: ``y[id1] = 0.0f + x[id0]`` (0.0f where guarded out)."""
+    _row_op("init_from", rows_y, rows_x, index, num_rows, index_offset, row_size,
             num_vals_limit, stream, validate)
 
 

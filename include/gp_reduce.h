@@ -81,6 +81,20 @@ int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
                         size_t num_rows, gp_double_index offset,
                         size_t row_size, size_t num_vals_limit, gp_stream s);
 
+/* Fused zerofy + scatter-add for a destination the call's rows cover:
+ *     y[to*row_size + v] = 0.0f + x[from*row_size + v]   (from*row_size+v < limit)
+ *     y[to*row_size + v] = 0.0f                          (otherwise)
+ * for every listed row — bit-identical, per listed destination row, to
+ * DataStorage::zerofy_data_gpu (common-util.hpp:445-456) followed by
+ * gp_scatter_add_rows (0.0f + x maps -0.0 to +0.0 exactly as the add does).
+ * Destinations NOT listed are left untouched (not zeroed): the caller uses it
+ * only when the clock's update ops cover every oplog row exactly once
+ * (client.cpp, FinishVirtualIteration).  Same index semantics and precondition
+ * as gp_scatter_add_rows. */
+int gp_scatter_init_rows(float *y, const float *x, const gp_double_index *index,
+                         size_t num_rows, gp_double_index offset,
+                         size_t row_size, size_t num_vals_limit, gp_stream s);
+
 /* Row-indexed gather (the Read path, refresh leg):
  *     from = index[r].id1 + offset.id1;  to = index[r].id0 + offset.id0;
  *     if (to*row_size + v < num_vals_limit)

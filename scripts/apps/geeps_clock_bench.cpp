@@ -1,0 +1,89 @@
+// geeps_clock_bench — end-to-end clock rate of libgeeps through the public API.
+//
+//   geeps_clock_bench <process_id> <num_processes> <base_port> <rows> <clocks> <warmup>
+//
+// One table of `rows` RowData rows; per clock the app does what apps/helloworld
+// does, at scale: Read(all rows) -> PreUpdate(all rows) -> PostRead -> Update
+// -> Clock, with the update buffer filled on the device.  A clock therefore runs
+// the whole reduction path: oplog zero + row-indexed scatter-add (Update), the
+// push of each server's slice (zero-copy in process, D2H + TCP otherwise), the
+// server's bucket sum into its master shard, the refresh of every client's
+// param cache, and the gather into the Read buffer.  Prints one JSON line.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "geeps.hpp"
+
+#define HCK(x)                                                     \
+  do {                                                             \
+    hipError_t e_ = (x);                                           \
+    if (e_ != hipSuccess) {                                        \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); \
+      std::exit(3);                                                \
+    }                                                              \
+  } while (0)
+
+int main(int argc, char **argv) {
+  if (argc < 7) {
+    std::fprintf(stderr, "usage: %s pid nproc base_port rows clocks warmup\n", argv[0]);
+    return 2;
+  }
+  const int pid = std::atoi(argv[1]), P = std::atoi(argv[2]), base = std::atoi(argv[3]);
+  const size_t rows = std::strtoull(argv[4], 0, 10);
+  const int clocks = std::atoi(argv[5]), warmup = std::atoi(argv[6]);
+  GeePsConfig cfg;
+  for (int i = 0; i < P; ++i) {
+    cfg.host_list.push_back("127.0.0.1");
+    cfg.port_list.push_back(base + 16 * i);
+  }
+  GeePs *ps = new GeePs(pid, cfg);
+  std::vector<size_t> ids(rows);
+  for (size_t r = 0; r < rows; ++r) ids[r] = r;
+  const int hr = ps->VirtualRead(0, ids, 0);
+  const int hp = ps->VirtualPreUpdate(0, ids);
+  const int hpr = ps->VirtualPostRead(hr);
+  const int hu = ps->VirtualUpdate(hp);
+  ps->VirtualClock();
+  ps->FinishVirtualIteration();
+
+  RowOpVal *ub = nullptr;
+  ps->PreUpdate(hp, &ub);
+  HCK(hipMemset(ub, 0, rows * sizeof(RowOpVal)));
+  ps->Update(hu);
+  ps->Clock();
+  ps->StartIterations();
+
+  using clk = std::chrono::steady_clock;
+  clk::time_point t0;
+  for (int c = 0; c < warmup + clocks; ++c) {
+    if (c == warmup) t0 = clk::now();
+    RowData *rb = nullptr;
+    ps->Read(hr, &rb);
+    ps->PreUpdate(hp, &ub);
+    // the app's "gradient": 0.5 everywhere, written on the device
+    HCK(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(ub), 0x3f000000, rows * ROW_DATA_SIZE));
+    HCK(hipDeviceSynchronize());
+    ps->PostRead(hpr);
+    ps->Update(hu);
+    ps->Clock();
+  }
+  // the last Read waits for the last clock's refresh: include it
+  RowData *rb = nullptr;
+  ps->Read(hr, &rb);
+  const double s = std::chrono::duration<double>(clk::now() - t0).count();
+  float probe = 0;
+  HCK(hipMemcpy(&probe, rb, 4, hipMemcpyDeviceToHost));
+  const double per = s / clocks;
+  const double table_bytes = (double)rows * sizeof(RowData);
+  std::printf("{\"process\": %d, \"processes\": %d, \"rows\": %zu, \"table_bytes\": %.0f, "
+              "\"clocks\": %d, \"ms_per_clock\": %.4f, \"delta_GBps\": %.2f, \"probe\": %.1f}\n",
+              pid, P, rows, table_bytes, clocks, per * 1e3, table_bytes / per / 1e9, probe);
+  std::fflush(stdout);
+  std::fprintf(stderr, "stats %s\n", ps->GetStats().c_str());
+  ps->Shutdown();
+  return 0;
+}

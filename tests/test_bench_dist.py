@@ -31,4 +31,6 @@ def test_bench_multirank_flow(tmp_path, world, exchange):
     assert line["value"] > 0 and line["roofline"]["bound"] == "hbm"
     assert line["config"]["shards"] == world and line["config"]["exchange"] == exchange
     assert line["exchange_inclusive"]["value"] > 0
+    assert line["exchange_inclusive"]["exchange"] == exchange
+    assert line["exchange_inclusive_alt"]["exchange"] != exchange
     assert line["cpu_baseline"] is None  # rank-0 CPU baseline runs only at N = 1

@@ -252,3 +252,33 @@ def test_full_size_scatter_add_permuted(dev):
     rowops.add_rows_from_double_index_gpu(y, -x, idx, R, (0, 0), W, R * W, validate=False)
     torch.cuda.synchronize()
     assert torch.equal(y, y0)
+
+
+@pytest.mark.parametrize("W,limit_frac,shift", [(128, None, 0), (64, 0.55, 0), (130, None, 0),
+                                               (128, 0.7, 1), (1024, None, 0)])
+def test_scatter_init_equals_zero_then_add(dev, W, limit_frac, shift):
+    """gp_scatter_init_rows == zerofy + add_rows_from_double_index on every listed
+    destination row (the oracle: zeros, then the reference add), including -0.0
+    deltas (0.0f + -0.0f = +0.0f) and rows past num_vals_limit; rows not listed
+    keep their old contents."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(W + int((limit_frac or 0) * 100))
+    n_cache, n_op = 600, 400
+    dst = rng.choice(n_cache, n_op, replace=False)
+    idx = np.stack([rng.permutation(n_op), dst], 1).astype(np.int64)
+    x = rng.standard_normal(n_op * W + 1).astype(np.float32)
+    x[rng.choice(n_op * W, 500, replace=False)] = np.float32(-0.0)
+    y = rng.standard_normal(n_cache * W + 1).astype(np.float32)
+    limit = None if limit_frac is None else int(n_op * W * limit_frac) + 3
+    xs, ys = x[shift:shift + n_op * W].copy(), y[shift:shift + n_cache * W].copy()
+    e = ys.copy()
+    listed = np.zeros(n_cache, bool)
+    listed[dst] = True
+    e.reshape(n_cache, W)[listed] = 0.0
+    oracle.add_rows_from_double_index(e, xs, idx, (0, 0), W, limit)
+    ty_full, tx_full = T(y, dev), T(x, dev)
+    ty = ty_full[shift:shift + n_cache * W]
+    rowops.init_rows_from_double_index_gpu(ty, tx_full[shift:shift + n_op * W], T(idx, dev),
+                                           n_op, (0, 0), W, limit)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e))
