@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -72,6 +73,17 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
   GP_CHECK_MSG(config_.port_list.empty() || config_.port_list.size() >= num_processes_,
                "port_list must have one port per host");
   GP_CALL(gp_get_device(&device_));
+  // Same-node peers exchange rows device to device through IPC-mapped HBM
+  // (xGMI between GPUs); GEEPS_TRANSPORT=tcp forces the socket data path.
+  const char *transport = std::getenv("GEEPS_TRANSPORT");
+  const bool allow_ipc = !(transport && std::string(transport) == "tcp");
+  auto norm = [](const std::string &h) {
+    return (h == "localhost" || h == "local" || h == "127.0.0.1") ? std::string("127.0.0.1") : h;
+  };
+  same_node_.assign(num_processes_, false);
+  for (uint32_t s = 0; s < num_processes_; ++s)
+    same_node_[s] = allow_ipc && num_processes_ > 1 &&
+                    norm(config_.host_list[s]) == norm(config_.host_list[process_id_]);
   channels_.resize(num_channels_);
   for (uint32_t c = 0; c < num_channels_; ++c) {
     auto ch = std::make_unique<Channel>();
@@ -85,7 +97,11 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->server = std::make_unique<TabletServer>(process_id_, c, num_processes_,
                                                 config_.num_tables, ch->sink.get());
     ch->server_fd.assign(num_processes_, -1);
+    for (uint32_t s = 0; s < num_processes_; ++s)
+      ch->server_send_mu.push_back(std::make_unique<std::mutex>());
     ch->client_fd.assign(num_processes_, -1);
+    ch->ipc_oplogs.resize(num_processes_);
+    ch->inbox_of.assign(num_processes_, std::vector<InboxEntry>(config_.num_tables));
     channels_[c] = std::move(ch);
   }
   start_network();
@@ -172,12 +188,12 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == CLOCK_WITH_UPDATES_BATCH) {
-      GP_CHECK(parts.size() == 3 && parts[0].size == sizeof(cs_clock_with_updates_batch_msg_t));
+      GP_CHECK((parts.size() == 3 || parts.size() == 4) &&
+               parts[0].size == sizeof(cs_clock_with_updates_batch_msg_t));
       cs_clock_with_updates_batch_msg_t h;
       std::memcpy(&h, parts[0].data, sizeof h);
       GP_CHECK_EQ(h.client_id, client_id);
       const size_t n = parts[1].size / sizeof(RowKey);
-      GP_CHECK_EQ(parts[2].size, n * kRowBytes);
       UpdateBatch b;
       b.client_id = h.client_id;
       b.clock = h.clock;
@@ -187,8 +203,52 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       b.keys = keys->data();
       b.num_rows = n;
       b.keys_owner = keys;
-      b.host_rows = ctx.rows;
+      if (parts.size() == 4) {
+        // Same-node client: the rows stay in its oplog, mapped here over IPC.
+        GP_CHECK(parts[2].size == 0 && parts[3].size == sizeof(IpcRowsRef));
+        IpcRowsRef ref;
+        std::memcpy(&ref, parts[3].data, sizeof ref);
+        GP_CHECK_EQ(ref.bytes, n * kRowBytes);
+        auto &mapped = ch.ipc_oplogs[client_id];
+        if (ref.has_handle) {
+          auto old = mapped.find(ref.buffer_id);
+          if (old != mapped.end()) GP_CALL(gp_ipc_close_handle(old->second));
+          void *p = nullptr;
+          GP_CALL(gp_ipc_open_handle(&p, ref.handle));
+          mapped[ref.buffer_id] = p;
+        }
+        auto it = mapped.find(ref.buffer_id);
+        GP_CHECK_MSG(it != mapped.end(), "unmapped oplog buffer " << ref.buffer_id);
+        b.device_rows = reinterpret_cast<const float *>(static_cast<const char *>(it->second) +
+                                                        ref.offset);
+        b.device_remote = true;
+      } else {
+        GP_CHECK_EQ(parts[2].size, n * kRowBytes);
+        b.host_rows = ctx.rows;
+      }
       ch.server->post_updates(std::move(b));
+    } else if (cmd == kCmdIpcInbox) {
+      GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(IpcInboxMsg));
+      IpcInboxMsg m;
+      std::memcpy(&m, parts[0].data, sizeof m);
+      GP_CHECK_EQ(m.client_id, client_id);
+      GP_CHECK(m.table_id < config_.num_tables && m.num_slots == kInboxSlots);
+      InboxEntry e;
+      for (uint32_t k = 0; k < kInboxSlots; ++k) GP_CALL(gp_ipc_open_handle(&e.slot[k], m.handle[k]));
+      e.bytes = m.bytes;
+      e.registered = true;
+      std::lock_guard<std::mutex> lk(ch.ipc_mu);
+      ch.inbox_of[client_id][m.table_id] = e;
+    } else if (cmd == kCmdRefreshAck) {
+      GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(RefreshAckMsg));
+      RefreshAckMsg a;
+      std::memcpy(&a, parts[0].data, sizeof a);
+      GP_CHECK(a.table_id < config_.num_tables && a.slot < kInboxSlots);
+      {
+        std::lock_guard<std::mutex> lk(ch.ipc_mu);
+        ch.inbox_of[client_id][a.table_id].busy[a.slot] = false;
+      }
+      ch.ipc_cv.notify_all();
     } else if (cmd == CLOCK) {
       GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(cs_clock_msg_t));
       cs_clock_msg_t h;
@@ -222,15 +282,106 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == SHUTDOWN) break;  // the server will send nothing more
-    GP_CHECK(parts.size() == 3 && parts[0].size == sizeof(sc_read_row_batch_msg_t));
+    GP_CHECK((parts.size() == 3 || parts.size() == 4) &&
+             parts[0].size == sizeof(sc_read_row_batch_msg_t));
     sc_read_row_batch_msg_t h;
     std::memcpy(&h, parts[0].data, sizeof h);
     GP_CHECK_EQ(h.cmd, (command_t)READ_ROW_BATCH);
     GP_CHECK_EQ(h.server_id, server_id);
+    GP_CHECK_LT(h.table_id, config_.num_tables);
+    if (parts.size() == 4) {
+      // Same-node server wrote the shard into our inbox slot over IPC.
+      GP_CHECK(parts[3].size == sizeof(IpcRefreshSlot));
+      IpcRefreshSlot sl;
+      std::memcpy(&sl, parts[3].data, sizeof sl);
+      GP_CHECK_LT(sl.slot, kInboxSlots);
+      auto &slot = ch.tables[h.table_id].inbox[server_id][sl.slot];
+      GP_CHECK(slot);
+      recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock, slot->data(),
+                     sl.num_rows, true);
+      RefreshAckMsg a{};
+      a.cmd = kCmdRefreshAck;
+      a.client_id = process_id_;
+      a.table_id = h.table_id;
+      a.slot = sl.slot;
+      send_to_server(ch, server_id, {Part{&a, sizeof a}});
+      continue;
+    }
     const size_t n = parts[1].size / sizeof(RowKey);
     GP_CHECK_EQ(parts[2].size, n * kRowBytes);
     recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
                    static_cast<const float *>(parts[2].data), n, false);
+  }
+}
+
+// Refresh to a same-node client: copy the shard device to device into the
+// client's inbox slot (data_age parity), then a 4-part control frame.  A slot is
+// rewritten only after the client ACKed consuming it, so the client's copy into
+// its param cache (under its channel lock) never races this write.
+bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r) {
+  InboxEntry *ib = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(ch.ipc_mu);
+    InboxEntry &e = ch.inbox_of[client_id][r.table_id];
+    if (e.registered) ib = &e;
+  }
+  if (!ib || r.num_rows == 0) return false;
+  const uint32_t slot = (uint32_t)(((r.data_age % 2) + 2) % 2);
+  {
+    std::unique_lock<std::mutex> lk(ch.ipc_mu);
+    while (ib->busy[slot]) {
+      if (!ch.ipc_cv.wait_for(lk, std::chrono::milliseconds(kWaitWarnMs),
+                              [&] { return !ib->busy[slot]; }))
+        std::cerr << "server " << process_id_ << " waiting for client " << client_id
+                  << " to consume refresh slot " << slot << std::endl;
+    }
+    ib->busy[slot] = true;
+  }
+  const size_t bytes = r.num_rows * kRowBytes;
+  GP_CHECK_LE(bytes, ib->bytes);
+  GP_CALL(gp_memcpy_async(ib->slot[slot], r.device_rows, bytes, ch.reply_stream->get()));
+  ch.reply_stream->sync();
+  sc_read_row_batch_msg_t h{};
+  h.cmd = READ_ROW_BATCH;
+  h.server_id = r.server_id;
+  h.data_age = r.data_age;
+  h.self_clock = r.self_clock;
+  h.table_id = r.table_id;
+  IpcRefreshSlot sl{slot, 0, r.num_rows};
+  GP_CHECK_MSG(send_frame(ch.client_fd[client_id], {Part{&h, sizeof h}, Part{nullptr, 0},
+                                                    Part{nullptr, 0}, Part{&sl, sizeof sl}}),
+               "send to client " << client_id << " failed");
+  return true;
+}
+
+void ClientLib::send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts) {
+  std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
+  GP_CHECK_MSG(send_frame(ch.server_fd[s], parts), "send to server " << s << " failed");
+}
+
+// Same-node servers get kInboxSlots device buffers per table to write refreshed
+// shards into (FinishVirtualIteration, once the shard sizes are known).
+void ClientLib::register_inboxes() {
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    for (uint32_t t = 0; t < config_.num_tables; ++t) {
+      ParamCache &pc = ch.tables[t];
+      pc.inbox.resize(num_processes_);
+      for (uint32_t s = 0; s < num_processes_; ++s) {
+        if (!ipc_to(s) || pc.server_num_rows[s] == 0) continue;
+        IpcInboxMsg m{};
+        m.cmd = kCmdIpcInbox;
+        m.client_id = process_id_;
+        m.table_id = t;
+        m.num_slots = kInboxSlots;
+        m.bytes = pc.server_num_rows[s] * kRowBytes;
+        for (uint32_t k = 0; k < kInboxSlots; ++k) {
+          pc.inbox[s][k] = std::make_unique<DeviceArray<float>>(pc.server_num_rows[s] * ROW_DATA_SIZE);
+          GP_CALL(gp_ipc_get_handle(m.handle[k], pc.inbox[s][k]->data()));
+        }
+        send_to_server(ch, s, {Part{&m, sizeof m}});
+      }
+    }
   }
 }
 
@@ -254,6 +405,7 @@ void ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatc
     return;
   }
   Channel &ch = *channels_[channel];
+  if (ipc_reply(ch, client_id, r)) return;
   const int fd = ch.client_fd[client_id];
   GP_CHECK_MSG(fd >= 0, "no connection to client " << client_id);
   const size_t floats = r.num_rows * ROW_DATA_SIZE;
@@ -402,6 +554,7 @@ void ClientLib::finish_virtual_iteration() {
   }
   GP_CALL(gp_device_synchronize());
   decide_fused_init();
+  register_inboxes();
   if (planned > config_.gpu_memory_capacity) {
     std::ostringstream o;
     o << "planned HBM use " << planned << " B exceeds gpu_memory_capacity "
@@ -683,15 +836,29 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
   std::shared_ptr<DeviceArray<float>> oplog;
   std::vector<size_t> starts, counts;
   std::shared_ptr<const std::vector<RowKey>> keys;  // immutable after FinishVirtualIteration
+  size_t pool_id = 0;
+  std::vector<uint8_t> *exported = nullptr;  // app thread only
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[table_id];
     auto it = pc.oplog.find(clock);
     if (it != pc.oplog.end()) oplog = it->second;
-    if (oplog && !config_.read_my_writes) pc.oplog.erase(it);  // reclaim_oplog
     starts = pc.server_row_start;
     counts = pc.server_num_rows;
     keys = pc.row_keys;
+    bool ipc_readers = false;  // a same-node server reads its slice from this oplog
+    for (uint32_t s = 0; s < num_processes_; ++s) ipc_readers |= ipc_to(s) && counts[s] > 0;
+    if (oplog) {
+      for (size_t k = 0; k < pc.oplog_pool.size(); ++k)
+        if (pc.oplog_pool[k] == oplog) pool_id = k;
+      if (pc.exported.size() < pc.oplog_pool.size())
+        pc.exported.resize(pc.oplog_pool.size(), std::vector<uint8_t>(num_processes_, 0));
+      exported = &pc.exported[pool_id];
+      // reclaim_oplog now, unless it must outlive the refresh (read-my-writes
+      // re-apply; same-node servers copying out of it): then recv_row_batch
+      // reclaims it once every server's data age covers the clock.
+      if (!config_.read_my_writes && !ipc_readers) pc.oplog.erase(it);
+    }
   }
   size_t remote_bytes = 0;
   for (uint32_t s = 0; s < num_processes_; ++s) {
@@ -705,7 +872,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
         h.client_id = process_id_;
         h.clock = clock;
         h.table_id = table_id;
-        GP_CHECK(send_frame(ch.server_fd[s], {Part{&h, sizeof h}}));
+        send_to_server(ch, s, {Part{&h, sizeof h}});
       }
       continue;
     }
@@ -721,6 +888,24 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       b.device_rows = oplog->data() + a * ROW_DATA_SIZE;
       b.keepalive = oplog;  // zero-copy: the server reads the oplog slice in place
       ch.server->post_updates(std::move(b));
+    } else if (ipc_to(s)) {
+      // Same-node server: it copies its slice straight out of this oplog.
+      cs_clock_with_updates_batch_msg_t h{};
+      h.cmd = CLOCK_WITH_UPDATES_BATCH;
+      h.client_id = process_id_;
+      h.clock = clock;
+      h.table_id = table_id;
+      IpcRowsRef ref{};
+      ref.buffer_id = pool_id;
+      ref.offset = a * kRowBytes;
+      ref.bytes = n * kRowBytes;
+      if (!(*exported)[s]) {
+        GP_CALL(gp_ipc_get_handle(ref.handle, oplog->data()));
+        ref.has_handle = 1;
+        (*exported)[s] = 1;
+      }
+      send_to_server(ch, s, {Part{&h, sizeof h}, Part{keys->data() + a, n * sizeof(RowKey)},
+                             Part{nullptr, 0}, Part{&ref, sizeof ref}});
     } else {
       const size_t floats = n * ROW_DATA_SIZE;
       if (ch.send_buf.size() < floats) ch.send_buf.resize(floats);
@@ -734,9 +919,8 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       h.client_id = process_id_;
       h.clock = clock;
       h.table_id = table_id;
-      GP_CHECK(send_frame(ch.server_fd[s], {Part{&h, sizeof h},
-                                            Part{keys->data() + a, n * sizeof(RowKey)},
-                                            Part{ch.send_buf.data(), floats * 4}}));
+      send_to_server(ch, s, {Part{&h, sizeof h}, Part{keys->data() + a, n * sizeof(RowKey)},
+                             Part{ch.send_buf.data(), floats * 4}});
       remote_bytes += floats * 4;
     }
   }
@@ -840,7 +1024,7 @@ void ClientLib::shutdown() {
         cs_clock_msg_t h{};
         h.cmd = SHUTDOWN;
         h.client_id = process_id_;
-        GP_CHECK(send_frame(ch.server_fd[s], {Part{&h, sizeof h}}));
+        send_to_server(ch, s, {Part{&h, sizeof h}});
       }
     }
   }
@@ -851,6 +1035,12 @@ void ClientLib::shutdown() {
     for (auto &t : chp->server_readers)
       if (t.joinable()) t.join();
     chp->server->stop();
+    for (auto &m : chp->ipc_oplogs)
+      for (auto &kv : m) gp_ipc_close_handle(kv.second);
+    for (auto &row : chp->inbox_of)
+      for (auto &e : row)
+        if (e.registered)
+          for (void *p : e.slot) gp_ipc_close_handle(p);
     for (int fd : chp->server_fd) close_fd(fd);
     for (int fd : chp->client_fd) close_fd(fd);
     close_fd(chp->listen_fd);

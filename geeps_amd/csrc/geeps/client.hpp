@@ -25,6 +25,7 @@
 // calling thread; device work is ordered on per-channel HIP streams and synced
 // before a call returns data to the app.
 
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <map>
@@ -37,6 +38,7 @@
 
 #include "device.hpp"
 #include "geeps.hpp"
+#include "net.hpp"
 #include "server.hpp"
 #include "wire.hpp"
 
@@ -76,6 +78,18 @@ struct ParamCache {
   iter_t data_age = INITIAL_DATA_AGE;
   std::vector<iter_t> server_clock;
   iter_t server_clock_min = INITIAL_DATA_AGE;
+  // same-node peers: refresh inbox per server (kInboxSlots device buffers the
+  // server writes over IPC), and which oplog buffers each server has mapped
+  std::vector<std::array<std::unique_ptr<DeviceArray<float>>, kInboxSlots>> inbox;
+  std::vector<std::vector<uint8_t>> exported;  // [oplog pool index][server]
+};
+
+// Server-side view of a same-node client's IPC exports.
+struct InboxEntry {
+  void *slot[kInboxSlots] = {};
+  size_t bytes = 0;
+  bool busy[kInboxSlots] = {};
+  bool registered = false;
 };
 
 struct ClientStats {
@@ -110,8 +124,10 @@ struct Channel {
   std::unique_ptr<Stream> stream, recv_stream, send_stream, reply_stream;
   std::unique_ptr<ChannelSink> sink;
   std::unique_ptr<TabletServer> server;
-  // client side: one socket per remote server (-1 = in-process server)
+  // client side: one socket per remote server (-1 = in-process server); the
+  // app thread (pushes) and the reader thread (refresh ACKs) both write to it
   std::vector<int> server_fd;
+  std::vector<std::unique_ptr<std::mutex>> server_send_mu;
   std::vector<std::thread> client_readers;
   PinnedArray<float> send_buf;
   // server side: one socket per remote client
@@ -119,6 +135,11 @@ struct Channel {
   std::vector<int> client_fd;
   std::vector<std::thread> server_readers;
   PinnedArray<float> reply_buf;
+  // server side, same-node clients: mapped oplog buffers and refresh inboxes
+  std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
+  std::vector<std::vector<InboxEntry>> inbox_of;         // [client][table]
+  std::mutex ipc_mu;
+  std::condition_variable ipc_cv;
 };
 
 class ClientLib {
@@ -165,12 +186,17 @@ class ClientLib {
   void server_reader(Channel &ch, uint32_t client_id, int fd);
   void client_reader(Channel &ch, uint32_t server_id, int fd);
   uint16_t port_of(uint32_t process, uint32_t channel) const;
+  bool ipc_to(uint32_t s) const { return s != process_id_ && same_node_[s]; }
+  void register_inboxes();
+  bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r);
+  void send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts);
 
   const uint32_t process_id_;
   const GeePsConfig config_;
   const uint32_t num_processes_;
   const uint32_t num_channels_;
   int device_ = 0;
+  std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)
 
   std::vector<OpInfo> opseq_;
   std::map<std::vector<row_idx_t>, std::unique_ptr<DeviceArray<float>>> local_storage_;

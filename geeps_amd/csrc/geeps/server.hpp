@@ -39,8 +39,9 @@ namespace geeps {
 
 // Rows of one client's clock update for one server: n keys and n RowOpVal.
 // Exactly one of `device_rows` (in-process client: a zero-copy slice of its
-// oplog, kept alive by `keepalive` until applied) or `host_rows` (received
-// from a socket into pinned memory) is set.
+// oplog, kept alive by `keepalive` until applied; or a same-node peer's oplog
+// slice, copied on arrival) or `host_rows` (received from a socket into pinned
+// memory) is set.
 struct UpdateBatch {
   uint32_t client_id = 0;
   iter_t clock = 0;
@@ -51,6 +52,9 @@ struct UpdateBatch {
   size_t num_rows = 0;
   std::shared_ptr<const void> keys_owner;
   const float *device_rows = nullptr;
+  // device_rows points into a same-node peer's HBM (IPC-mapped): stage a copy
+  // on arrival instead of holding the peer's buffer.
+  bool device_remote = false;
   std::shared_ptr<void> keepalive;
   std::shared_ptr<PinnedArray<float>> host_rows;
 };

@@ -70,4 +70,49 @@ struct sc_read_row_batch_msg_t {
   int branch_id;
 };
 
+// ---------------------------------------------------------------------------
+// libgeeps-internal frames for same-node peers (not part of the reference
+// protocol; numbered clear of its Command enum).  Bulk rows move device to
+// device (xGMI between MI355X GPUs, or within one GPU) through IPC-mapped
+// HBM; TCP carries only these small control frames.
+// ---------------------------------------------------------------------------
+constexpr command_t kCmdIpcInbox = 100;    // client -> server: refresh inbox handles
+constexpr command_t kCmdRefreshAck = 101;  // client -> server: inbox slot consumed
+constexpr uint32_t kIpcHandleBytes = 64;
+constexpr uint32_t kInboxSlots = 2;
+
+// 4th part of a CLOCK_WITH_UPDATES_BATCH whose rows stay in the client's oplog.
+struct IpcRowsRef {
+  uint64_t buffer_id;   // the client's oplog buffer (stable per buffer)
+  uint64_t offset;      // bytes from the buffer base to this server's slice
+  uint64_t bytes;
+  uint32_t has_handle;  // first use of buffer_id: `handle` is valid
+  uint32_t pad;
+  uint8_t handle[kIpcHandleBytes];
+};
+
+// Registers the client's refresh inbox (kInboxSlots device buffers) for a table.
+struct IpcInboxMsg {
+  command_t cmd;
+  uint32_t client_id;
+  uint32_t table_id;
+  uint32_t num_slots;
+  uint64_t bytes;  // per slot
+  uint8_t handle[kInboxSlots][kIpcHandleBytes];
+};
+
+// 4th part of a READ_ROW_BATCH whose rows were written into the inbox slot.
+struct IpcRefreshSlot {
+  uint32_t slot;
+  uint32_t pad;
+  uint64_t num_rows;
+};
+
+struct RefreshAckMsg {
+  command_t cmd;
+  uint32_t client_id;
+  uint32_t table_id;
+  uint32_t slot;
+};
+
 #endif  // GEEPS_AMD_WIRE_HPP_

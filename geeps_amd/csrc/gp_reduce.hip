@@ -25,6 +25,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <string>
 
 #include "gp_reduce.h"
@@ -542,6 +543,30 @@ int gp_event_synchronize(gp_event e) {
 int gp_event_elapsed_ms(float *ms, gp_event start, gp_event stop) {
   if (!ms) return set_error(GP_ERR_INVALID, "null pointer");
   GP_HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+  return GP_OK;
+}
+
+static_assert(sizeof(hipIpcMemHandle_t) <= GP_IPC_HANDLE_BYTES, "IPC handle size");
+
+int gp_ipc_get_handle(void *handle_out, void *device_base) {
+  if (!handle_out || !device_base) return set_error(GP_ERR_INVALID, "null pointer");
+  hipIpcMemHandle_t h;
+  GP_HIP_TRY(hipIpcGetMemHandle(&h, device_base));
+  std::memset(handle_out, 0, GP_IPC_HANDLE_BYTES);
+  std::memcpy(handle_out, &h, sizeof h);
+  return GP_OK;
+}
+
+int gp_ipc_open_handle(void **device_ptr, const void *handle) {
+  if (!device_ptr || !handle) return set_error(GP_ERR_INVALID, "null pointer");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof h);
+  GP_HIP_TRY(hipIpcOpenMemHandle(device_ptr, h, hipIpcMemLazyEnablePeerAccess));
+  return GP_OK;
+}
+
+int gp_ipc_close_handle(void *device_ptr) {
+  if (device_ptr) GP_HIP_TRY(hipIpcCloseMemHandle(device_ptr));
   return GP_OK;
 }
 

@@ -61,6 +61,9 @@ _SIGNATURES = {
     "gp_event_record": (_i, [_vp, _vp]),
     "gp_event_synchronize": (_i, [_vp]),
     "gp_event_elapsed_ms": (_i, [_c.POINTER(_c.c_float), _vp, _vp]),
+    "gp_ipc_get_handle": (_i, [_vp, _vp]),
+    "gp_ipc_open_handle": (_i, [_c.POINTER(_vp), _vp]),
+    "gp_ipc_close_handle": (_i, [_vp]),
 }
 
 _lock = threading.Lock()

@@ -166,6 +166,14 @@ int gp_event_record(gp_event e, gp_stream s);
 int gp_event_synchronize(gp_event e);
 int gp_event_elapsed_ms(float *ms, gp_event start, gp_event stop);
 
+/* Inter-process device memory (same node; xGMI between MI355X devices):
+ * export a hipMalloc'd allocation BASE as an opaque 64-byte handle, map a
+ * peer's handle into this process (peer access enabled lazily), unmap. */
+#define GP_IPC_HANDLE_BYTES 64
+int gp_ipc_get_handle(void *handle_out, void *device_base);
+int gp_ipc_open_handle(void **device_ptr, const void *handle);
+int gp_ipc_close_handle(void *device_ptr);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

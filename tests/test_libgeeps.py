@@ -71,13 +71,20 @@ def _ports(n_proc, channels):
     raise RuntimeError("no port range")
 
 
-def _run_app(P, rows, clocks, slack, channels, rmw, mode="int", timeout=240):
+def _env(transport):
+    env = dict(os.environ)
+    env["GEEPS_TRANSPORT"] = transport  # "ipc": same-node rows over IPC-mapped HBM; "tcp": sockets
+    return env
+
+
+def _run_app(P, rows, clocks, slack, channels, rmw, mode="int", timeout=240, transport="ipc"):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, channels)
     procs = [subprocess.Popen([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
                                str(channels), str(rmw), mode],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=_env(transport))
              for p in range(P)]
     outs = []
     try:
@@ -113,19 +120,28 @@ def test_single_process_two_channels(dev):
 
 
 @pytest.mark.gpu
-def test_two_processes_loopback_bsp(dev):
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+def test_two_processes_loopback_bsp(dev, transport):
     # BASELINE config 1: 2 local PS processes over loopback, 1K x 64 fp32 = 512 RowData rows
-    _run_app(2, rows=512, clocks=10, slack=0, channels=1, rmw=0)
+    _run_app(2, rows=512, clocks=10, slack=0, channels=1, rmw=0, transport=transport)
 
 
 @pytest.mark.gpu
-def test_three_processes_two_channels_ssp(dev):
-    _run_app(3, rows=777, clocks=8, slack=1, channels=2, rmw=0)
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+def test_three_processes_two_channels_ssp(dev, transport):
+    _run_app(3, rows=777, clocks=8, slack=1, channels=2, rmw=0, transport=transport)
 
 
 @pytest.mark.gpu
-def test_two_processes_read_my_writes(dev):
-    _run_app(2, rows=300, clocks=6, slack=1, channels=1, rmw=1)
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+def test_two_processes_read_my_writes(dev, transport):
+    _run_app(2, rows=300, clocks=6, slack=1, channels=1, rmw=1, transport=transport)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+def test_four_processes_ssp_slack2(dev, transport):
+    _run_app(4, rows=2048, clocks=12, slack=2, channels=1, rmw=0, transport=transport)
 
 
 # ---- BASELINE configs 4 and 5: layered param tables (Caffe is absent) ---------
@@ -169,25 +185,28 @@ def test_alexnet_table_size():
 
 
 @pytest.mark.gpu
-def test_config4_inception_cifar_two_workers(dev):
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+def test_config4_inception_cifar_two_workers(dev, transport):
     rows, spec = _layer_spec(inception_cifar_blobs())
-    _run_app_layers(2, rows, spec, clocks=5, slack=0)
+    _run_app_layers(2, rows, spec, clocks=5, slack=0, transport=transport)
 
 
 @pytest.mark.gpu
 @pytest.mark.slow
-def test_config5_alexnet_8_workers_8_shards_staleness_1(dev):
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+def test_config5_alexnet_8_workers_8_shards_staleness_1(dev, transport):
     rows, spec = _layer_spec(ALEXNET_BLOBS)
-    _run_app_layers(8, rows, spec, clocks=4, slack=1, timeout=900)
+    _run_app_layers(8, rows, spec, clocks=4, slack=1, timeout=900, transport=transport)
 
 
-def _run_app_layers(P, rows, spec, clocks, slack, timeout=600):
+def _run_app_layers(P, rows, spec, clocks, slack, timeout=600, transport="ipc"):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, 1)
     procs = [subprocess.Popen([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
                                "1", "0", "int", spec],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=_env(transport))
              for p in range(P)]
     outs = []
     try:
