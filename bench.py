@@ -63,6 +63,9 @@ def parse(argv=None):
     p.add_argument("--cpu-rows", type=int, default=1 << 17)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-rowops", action="store_true")
+    p.add_argument("--layout", choices=["arena", "separate"], default="arena",
+                   help="HBM layout of buckets + master: one arena (master last) or one "
+                        "allocation per buffer")
     return p.parse_args(argv)
 
 
@@ -100,15 +103,26 @@ def max_over_ranks(x: float, world: int, dev) -> float:
     return float(t.item())
 
 
-def make_deltas(hosted, n, dev):
+def make_deltas(hosted, n, dev, layout="arena", extra=0):
+    """The hosted clients' delta buffers.  With layout "arena" they are carved
+    from one allocation followed by `extra` floats (the master shard at N = 1),
+    returned as the last element; with "separate" each is its own allocation."""
     g = torch.Generator(device=dev)
+    arena = None
+    if layout == "arena":
+        arena = torch.empty(len(hosted) * n + extra, dtype=torch.float32, device=dev)
     out = []
-    for c in hosted:
+    for j, c in enumerate(hosted):
         g.manual_seed(1000 + c)
-        d = torch.rand(n, generator=g, device=dev)
+        if arena is not None:
+            d = arena[j * n:(j + 1) * n]
+            torch.rand(n, generator=g, device=dev, out=d)
+        else:
+            d = torch.rand(n, generator=g, device=dev)
         d.sub_(0.5)
         out.append(d)
-    return out
+    tail = arena[len(hosted) * n:] if (arena is not None and extra) else None
+    return out, tail
 
 
 def timed_apply(red, steps, warmup, world, dev):
@@ -289,11 +303,17 @@ def main(argv=None, backend="nccl", apply_fn=None):
     geeps_amd.lib()  # the HIP library must be there; no fallback
 
     R, W, C = args.rows, args.width, args.clients
-    red = ShardedReducer(R, W, C, dev, exchange=args.exchange, apply_fn=apply_fn)
+    from geeps_amd.shard import ShardLayout, hosted_clients
+    hosted = hosted_clients(rank, world, C)
+    # At N = 1 the buckets are the hosted clients' own buffers: the master shard
+    # goes in the same arena, after them.
+    master_floats = ShardLayout(R, W, world, rank).max_rows * W if world == 1 else 0
+    deltas, master = make_deltas(hosted, R * W, dev, args.layout, master_floats)
+    red = ShardedReducer(R, W, C, dev, exchange=args.exchange, apply_fn=apply_fn,
+                         master=master, layout=args.layout)
     L = red.layout
     log(f"[rank {rank}] shard rows [{L.row_start}, {L.row_start + L.local_rows}) "
-        f"hosting clients {red.hosted}")
-    deltas = make_deltas(red.hosted, R * W, dev)
+        f"hosting clients {red.hosted}, HBM layout {args.layout}")
     red.push(deltas)  # buckets resident on their shard
     _sync(dev)
 
@@ -316,7 +336,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
         # "rs" (RCCL reduce-scatter, ring-order sum), each + N-way sum + all-gather.
         for kind in (args.exchange, "rs" if args.exchange == "a2a" else "a2a"):
             r = red if kind == args.exchange else ShardedReducer(R, W, C, dev, exchange=kind,
-                                                                 apply_fn=apply_fn)
+                                                                 apply_fn=apply_fn,
+                                                                 layout=args.layout)
             ex = timed_exchange(r, deltas, args.exchange_steps, 1, world, dev)
             ex = max_over_ranks(ex, world, dev) / args.exchange_steps
             result_exchange.append({"ms_per_step": round(ex * 1e3, 3),
@@ -366,6 +387,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
                                    f"device-resident (BASELINE.json north-star / configs[2])",
                        "rows": R, "row_width": W, "clients": C, "shards": world,
                        "exchange": args.exchange if world > 1 else "none (resident)",
+                       "hbm_layout": args.layout,
                        "parallelism": f"row-range shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_min, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",

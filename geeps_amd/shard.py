@@ -92,7 +92,8 @@ class ShardedReducer:
 
     def __init__(self, num_rows: int, row_size: int, num_clients: int, device,
                  group=None, exchange: str = "a2a",
-                 apply_fn: Callable | None = None):
+                 apply_fn: Callable | None = None, master: torch.Tensor | None = None,
+                 layout: str = "arena"):
         if exchange not in ("a2a", "rs"):
             raise ValueError("exchange must be 'a2a' or 'rs'")
         self.group = group
@@ -104,12 +105,32 @@ class ShardedReducer:
         self.exchange = exchange
         self.device = device
         self.apply_fn = apply_fn or _default_apply
+        if layout not in ("arena", "separate"):
+            raise ValueError("layout must be 'arena' or 'separate'")
         L = self.layout
-        # master shard, padded to max_rows so the all-gather counts are equal
-        self.master = torch.zeros(L.max_rows * row_size, dtype=torch.float32, device=device)
+        self.hbm_layout = layout
         self.refreshed = None
         self.recv: list[torch.Tensor] = []
         self._buckets: list[torch.Tensor] = []
+        # HBM layout of the shard: with "arena" the exchange's receive buckets
+        # and the master shard (padded to max_rows so the all-gather counts are
+        # equal) are carved from ONE allocation, master last — the placement
+        # that measured fastest for the N-way sum (profiles/r01/bucket_tune_sweep6_layout.txt).
+        padded = L.max_rows * row_size
+        if master is not None:
+            if master.numel() < padded:
+                raise ValueError("master too small for the shard")
+            self.master = master[:padded]
+            self.master.zero_()
+        elif layout == "arena" and self.world > 1:
+            per = (self.world * L.local_vals) if exchange == "a2a" else padded
+            arena = torch.empty(len(self.hosted) * per + padded, dtype=torch.float32,
+                                device=device)
+            self.recv = [arena[j * per:(j + 1) * per] for j in range(len(self.hosted))]
+            self.master = arena[len(self.hosted) * per:]
+            self.master.zero_()
+        else:
+            self.master = torch.zeros(padded, dtype=torch.float32, device=device)
 
     # -- exchange -----------------------------------------------------------
     def push(self, deltas: Sequence[torch.Tensor]) -> None:
@@ -142,6 +163,7 @@ class ShardedReducer:
             if not self.recv:
                 self.recv = [torch.empty(padded, dtype=torch.float32, device=self.device)
                              for _ in self.hosted]
+            if not hasattr(self, "_send"):
                 self._send = torch.zeros(self.world * padded, dtype=torch.float32,
                                          device=self.device)
             for j, d in enumerate(deltas):
