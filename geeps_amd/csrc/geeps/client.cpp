@@ -896,7 +896,8 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       h.clock = clock;
       h.table_id = table_id;
       IpcRowsRef ref{};
-      ref.buffer_id = pool_id;
+      // unique per client across tables: the server maps buffers by this id
+      ref.buffer_id = ((uint64_t)table_id << 32) | (uint64_t)pool_id;
       ref.offset = a * kRowBytes;
       ref.bytes = n * kRowBytes;
       if (!(*exported)[s]) {

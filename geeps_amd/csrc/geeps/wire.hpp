@@ -83,7 +83,7 @@ constexpr uint32_t kInboxSlots = 2;
 
 // 4th part of a CLOCK_WITH_UPDATES_BATCH whose rows stay in the client's oplog.
 struct IpcRowsRef {
-  uint64_t buffer_id;   // the client's oplog buffer (stable per buffer)
+  uint64_t buffer_id;   // (table << 32) | oplog pool index: stable, unique per client
   uint64_t offset;      // bytes from the buffer base to this server's slice
   uint64_t bytes;
   uint32_t has_handle;  // first use of buffer_id: `handle` is valid

@@ -65,19 +65,30 @@ int main(int argc, char **argv) {
   const double add_b = 3.0 * R * W * 4 + 16.0 * R, gat_b = 2.0 * R * W * 4 + 16.0 * R;
   std::vector<V> vs;
 #define ADD(NAME, B, ...) vs.push_back(V{NAME, B, [&]() { __VA_ARGS__; }, {}})
-  ADD("add L32 R4 pc8 (prod)", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 8)));
-  ADD("add L32 R2 pc8", add_b, (launch<kAddFrom, 32, 2>(y, x, idx, R, W, 8)));
-  ADD("add L32 R8 pc8", add_b, (launch<kAddFrom, 32, 8>(y, x, idx, R, W, 8)));
-  ADD("add L32 R4 pc4", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 4)));
-  ADD("add L32 R4 pc16", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 16)));
-  ADD("add L32 R8 pc4", add_b, (launch<kAddFrom, 32, 8>(y, x, idx, R, W, 4)));
-  ADD("add L16 R4 pc8", add_b, (launch<kAddFrom, 16, 4>(y, x, idx, R, W, 8)));
-  ADD("add L64 R4 pc8", add_b, (launch<kAddFrom, 64, 4>(y, x, idx, R, W, 8)));
-  ADD("add ident L32 R4 pc8", add_b, (launch<kAddFrom, 32, 4>(y, x, ident, R, W, 8)));
-  ADD("gather L32 R8 pc8 (prod)", gat_b, (launch<kAssignTo, 32, 8>(y, x, idx, R, W, 8)));
-  ADD("gather L32 R4 pc8", gat_b, (launch<kAssignTo, 32, 4>(y, x, idx, R, W, 8)));
-  ADD("gather L32 R8 pc4", gat_b, (launch<kAssignTo, 32, 8>(y, x, idx, R, W, 4)));
-  ADD("gather ident L32 R8 pc8", gat_b, (launch<kAssignTo, 32, 8>(y, x, ident, R, W, 8)));
+  ADD("add separate (prod)", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 8)));
+  ADD("gather separate (prod)", gat_b, (launch<kAssignTo, 32, 8>(y, x, idx, R, W, 8)));
+  // one arena per variant: orders of {x, y} (index stays separate: 1 % of bytes)
+  const size_t fb = R * W * 4;
+  struct Lay { const char *add_name, *gat_name; float *x, *y; };
+  std::vector<Lay> lays;
+  {
+    char *a;
+    CK(hipMalloc(&a, 2 * fb));
+    lays.push_back({"add arena [x|y]", "gather arena [x|y]", (float *)a, (float *)(a + fb)});
+  }
+  {
+    char *a;
+    CK(hipMalloc(&a, 2 * fb));
+    lays.push_back({"add arena [y|x]", "gather arena [y|x]", (float *)(a + fb), (float *)a});
+  }
+  for (auto &L : lays) {
+    CK(hipMemset(L.x, 0, fb));
+    CK(hipMemset(L.y, 0, fb));
+    float *xx = L.x, *yy = L.y;
+    vs.push_back(V{L.add_name, add_b, [=]() { launch<kAddFrom, 32, 4>(yy, xx, idx, R, W, 8); }, {}});
+    // gather reads the cache (x role) and writes the op buffer (y role)
+    vs.push_back(V{L.gat_name, gat_b, [=]() { launch<kAssignTo, 32, 8>(yy, xx, idx, R, W, 8); }, {}});
+  }
 
   hipEvent_t a, b;
   CK(hipEventCreate(&a));

@@ -3,6 +3,12 @@
 //
 //   geeps_sum_app <process_id> <num_processes> <base_port> <rows> <clocks>
 //                 <slack> <channels> <read_my_writes> [int|float] [layers]
+//                 [tables] [local] [output_dir]
+//
+// `tables` > 1 assigns blob l to table l % tables (rows numbered per table);
+// `local` = 1 adds a LocalAccess(fetch) / PostLocalAccess(keep) pair whose
+// buffer must carry the previous iteration's contents into the next one;
+// `output_dir` sets GeePsConfig::output_dir (GetStats appends json_stats.<pid>).
 //
 // `layers` (comma-separated row counts, summing to `rows`) switches to a
 // Caffe-like op sequence: a Read per parameter blob in forward order, then per
@@ -79,8 +85,13 @@ int main(int argc, char **argv) {
     return 2;
   }
   const size_t n = rows * ROW_DATA_SIZE;
+  const int T = argc > 11 ? std::atoi(argv[11]) : 1;
+  const bool use_local = argc > 12 && std::atoi(argv[12]) != 0;
+  const std::string out_dir = argc > 13 ? argv[13] : "";
 
   GeePsConfig cfg;
+  cfg.num_tables = T;
+  cfg.output_dir = out_dir;
   for (int i = 0; i < P; ++i) {
     cfg.host_list.push_back("127.0.0.1");
     cfg.port_list.push_back(base + 16 * i);
@@ -97,20 +108,32 @@ int main(int argc, char **argv) {
     return 2;
   }
   const size_t L = layer_rows.size();
-  std::vector<size_t> first(L);
+  std::vector<size_t> first(L), table_of(L), first_in_table(L);
   std::vector<int> h_read(L), h_pre(L), h_post(L), h_upd(L);
-  for (size_t l = 0, r0 = 0; l < L; r0 += layer_rows[l], ++l) first[l] = r0;
+  std::vector<size_t> next_row(T, 0);
+  for (size_t l = 0, r0 = 0; l < L; r0 += layer_rows[l], ++l) {
+    first[l] = r0;  // position in the app's flat value array
+    table_of[l] = l % T;
+    first_in_table[l] = next_row[table_of[l]];
+    next_row[table_of[l]] += layer_rows[l];
+  }
   auto ids_of = [&](size_t l) {
     std::vector<size_t> ids(layer_rows[l]);
-    for (size_t r = 0; r < layer_rows[l]; ++r) ids[r] = first[l] + r;
+    for (size_t r = 0; r < layer_rows[l]; ++r) ids[r] = first_in_table[l] + r;
     return ids;
   };
-  for (size_t l = 0; l < L; ++l) h_read[l] = ps->VirtualRead(0, ids_of(l), slack);
+  const size_t local_rows = 3;
+  std::vector<size_t> local_ids(local_rows);
+  for (size_t r = 0; r < local_rows; ++r) local_ids[r] = 1000 + r;
+  int h_local = -1, h_local_post = -1;
+  if (use_local) h_local = ps->VirtualLocalAccess(local_ids, true);
+  for (size_t l = 0; l < L; ++l) h_read[l] = ps->VirtualRead(table_of[l], ids_of(l), slack);
   for (size_t l = L; l-- > 0;) {
-    h_pre[l] = ps->VirtualPreUpdate(0, ids_of(l));
+    h_pre[l] = ps->VirtualPreUpdate(table_of[l], ids_of(l));
     h_post[l] = ps->VirtualPostRead(h_read[l]);
     h_upd[l] = ps->VirtualUpdate(h_pre[l]);
   }
+  if (use_local) h_local_post = ps->VirtualPostLocalAccess(h_local, true);
   ps->VirtualClock();
   ps->FinishVirtualIteration();
 
@@ -147,7 +170,22 @@ int main(int argc, char **argv) {
   ps->StartIterations();
 
   int bad = 0;
+  std::vector<float> lbuf(local_rows * ROW_DATA_SIZE);
   for (int it = 1; it <= clocks; ++it) {
+    if (use_local) {
+      // Local data persists across iterations: it holds what we wrote last time.
+      RowData *lp = nullptr;
+      ps->LocalAccess(h_local, &lp);
+      HCK(hipMemcpy(lbuf.data(), lp, lbuf.size() * 4, hipMemcpyDeviceToHost));
+      const float want = it == 1 ? 0.0f : (float)(pid * 100 + it - 1);
+      for (size_t i = 0; i < lbuf.size() && bad < 5; ++i)
+        if (lbuf[i] != want) {
+          std::fprintf(stderr, "p%d it%d local %zu: got %g expected %g\n", pid, it, i, lbuf[i], want);
+          ++bad;
+        }
+      for (auto &v : lbuf) v = (float)(pid * 100 + it);
+      HCK(hipMemcpy(lp, lbuf.data(), lbuf.size() * 4, hipMemcpyHostToDevice));
+    }
     for (size_t l = 0; l < L; ++l) {
       RowData *rbuf = nullptr;
       ps->Read(h_read[l], &rbuf);
@@ -174,12 +212,13 @@ int main(int argc, char **argv) {
       }
     }
     push(it, true);
+    if (use_local) ps->PostLocalAccess(h_local_post);
     ps->Clock();
   }
   std::string stats = ps->GetStats();
-  std::printf("%s p%d rows=%zu layers=%zu clocks=%d slack=%d channels=%d rmw=%d %s\n",
-              bad ? "MISMATCH" : "OK", pid, rows, L, clocks, slack, channels, rmw,
-              fl ? "float" : "int");
+  std::printf("%s p%d rows=%zu layers=%zu tables=%d local=%d clocks=%d slack=%d channels=%d rmw=%d %s\n",
+              bad ? "MISMATCH" : "OK", pid, rows, L, T, (int)use_local, clocks, slack, channels,
+              rmw, fl ? "float" : "int");
   std::printf("stats %s\n", stats.c_str());
   std::fflush(stdout);
   ps->Shutdown();

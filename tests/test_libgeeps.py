@@ -199,12 +199,13 @@ def test_config5_alexnet_8_workers_8_shards_staleness_1(dev, transport):
     _run_app_layers(8, rows, spec, clocks=4, slack=1, timeout=900, transport=transport)
 
 
-def _run_app_layers(P, rows, spec, clocks, slack, timeout=600, transport="ipc"):
+def _run_app_layers(P, rows, spec, clocks, slack, timeout=600, transport="ipc", tables=1,
+                    local=0, out_dir=""):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, 1)
     procs = [subprocess.Popen([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
-                               "1", "0", "int", spec],
+                               "1", "0", "int", spec, str(tables), str(local), out_dir],
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                               env=_env(transport))
              for p in range(P)]
@@ -219,3 +220,22 @@ def _run_app_layers(P, rows, spec, clocks, slack, timeout=600, transport="ipc"):
                 pr.kill()
     for p, (rc, o, e) in enumerate(outs):
         assert rc == 0 and o.startswith("OK"), f"process {p} rc={rc}\n{o}\n{e[-3000:]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+def test_two_tables_local_access_and_stats_file(dev, tmp_path, transport):
+    """Blobs alternate between 2 tables (per-table clocks, last writes and
+    servers); a LocalAccess(fetch)/PostLocalAccess(keep) buffer must carry each
+    iteration's contents into the next; GetStats appends json_stats.<pid> to
+    output_dir (clientlib.cpp:226-263)."""
+    import json
+    spec_rows = [5, 7, 3, 9, 4]
+    _run_app_layers(2, sum(spec_rows), ",".join(map(str, spec_rows)), clocks=6, slack=0,
+                    transport=transport, tables=2, local=1, out_dir=str(tmp_path))
+    for pid in range(2):
+        lines = (tmp_path / f"json_stats.{pid}").read_text().strip().splitlines()
+        st = json.loads(lines[-1])
+        assert st["process_id"] == pid
+        assert st["client"]["nr_update"] == 5 * 7      # 5 blobs x (setup clock + 6 clocks)
+        assert st["servers"][0]["nr_refresh"] >= 2 * 6  # 2 tables refresh every clock
