@@ -99,6 +99,7 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->server_fd.assign(num_processes_, -1);
     for (uint32_t s = 0; s < num_processes_; ++s)
       ch->server_send_mu.push_back(std::make_unique<std::mutex>());
+    ch->server_shut.assign(num_processes_, 0);
     ch->client_fd.assign(num_processes_, -1);
     ch->ipc_oplogs.resize(num_processes_);
     ch->inbox_of.assign(num_processes_, std::vector<InboxEntry>(config_.num_tables));
@@ -304,7 +305,7 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
       a.client_id = process_id_;
       a.table_id = h.table_id;
       a.slot = sl.slot;
-      send_to_server(ch, server_id, {Part{&a, sizeof a}});
+      ack_to_server(ch, server_id, a);
       continue;
     }
     const size_t n = parts[1].size / sizeof(RowKey);
@@ -356,7 +357,21 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
 
 void ClientLib::send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts) {
   std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
+  GP_CHECK_MSG(!ch.server_shut[s], "send to server " << s << " after SHUTDOWN");
   GP_CHECK_MSG(send_frame(ch.server_fd[s], parts), "send to server " << s << " failed");
+  if (parts.size() == 1 && parts[0].size == sizeof(cs_clock_msg_t) &&
+      static_cast<const cs_clock_msg_t *>(parts[0].data)->cmd == SHUTDOWN)
+    ch.server_shut[s] = 1;
+}
+
+// The reader thread ACKs a consumed inbox slot.  The last refresh can land after
+// the app thread already sent SHUTDOWN (the server then stops reading that
+// socket and sends no more refreshes), so such an ACK is dropped, not sent.
+void ClientLib::ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a) {
+  std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
+  if (ch.server_shut[s]) return;
+  GP_CHECK_MSG(send_frame(ch.server_fd[s], {Part{&a, sizeof a}}),
+               "refresh ACK to server " << s << " failed");
 }
 
 // Same-node servers get kInboxSlots device buffers per table to write refreshed

@@ -128,6 +128,9 @@ struct Channel {
   // app thread (pushes) and the reader thread (refresh ACKs) both write to it
   std::vector<int> server_fd;
   std::vector<std::unique_ptr<std::mutex>> server_send_mu;
+  // set (under server_send_mu[s]) once SHUTDOWN went to server s: nothing may
+  // follow it on that socket, so late refresh ACKs are dropped
+  std::vector<char> server_shut;
   std::vector<std::thread> client_readers;
   PinnedArray<float> send_buf;
   // server side: one socket per remote client
@@ -190,6 +193,7 @@ class ClientLib {
   void register_inboxes();
   bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r);
   void send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts);
+  void ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a);
 
   const uint32_t process_id_;
   const GeePsConfig config_;

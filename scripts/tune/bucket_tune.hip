@@ -333,63 +333,29 @@ int main(int argc, char **argv) {
 #define ADD(NAME, BYTES, ...) vs.push_back(V{NAME, BYTES, [&]() { __VA_ARGS__; }, {}})
   f4 *s4 = reinterpret_cast<f4 *>(scratch);
   (void)s4;
-  struct Layout { std::string name; Ptrs p; f4 *m; };
-  std::vector<Layout> lays;
-  lays.push_back({"separate hipMalloc x9 (4 GiB each)", P, m4});
-  {  // one arena, streams back to back
-    char *a = nullptr;
-    CK(hipMalloc(&a, 9 * n * 4));
-    Ptrs Q{};
-    for (int k = 0; k < 8; ++k) Q.p[k] = reinterpret_cast<const f4 *>(a + (size_t)k * n * 4);
-    lays.push_back({"one arena x9", Q, reinterpret_cast<f4 *>(a + (size_t)8 * n * 4)});
+  // one arena, buckets then master (the production layout)
+  char *ar = nullptr;
+  CK(hipMalloc(&ar, 9 * n * 4));
+  Ptrs A{};
+  for (int k = 0; k < 8; ++k) {
+    A.p[k] = reinterpret_cast<const f4 *>(ar + (size_t)k * n * 4);
+    fill_k<<<4096, 256>>>(reinterpret_cast<float *>(ar + (size_t)k * n * 4), n, 1000 + k);
   }
-  {  // one arena, master first
-    char *a = nullptr;
-    CK(hipMalloc(&a, 9 * n * 4));
-    Ptrs Q{};
-    for (int k = 0; k < 8; ++k) Q.p[k] = reinterpret_cast<const f4 *>(a + (size_t)(k + 1) * n * 4);
-    lays.push_back({"one arena, master first", Q, reinterpret_cast<f4 *>(a)});
-  }
-  {  // three arenas of three streams
-    Ptrs Q{};
-    f4 *mm = nullptr;
-    for (int g = 0; g < 3; ++g) {
-      char *a = nullptr;
-      CK(hipMalloc(&a, 3 * n * 4));
-      for (int j = 0; j < 3; ++j) {
-        const int k = g * 3 + j;
-        if (k < 8) Q.p[k] = reinterpret_cast<const f4 *>(a + (size_t)j * n * 4);
-        else mm = reinterpret_cast<f4 *>(a + (size_t)j * n * 4);
-      }
-    }
-    lays.push_back({"three arenas x3", Q, mm});
-  }
-  {  // separate allocations, each 4 GiB + 2 MiB (alignment relation broken)
-    Ptrs Q{};
-    f4 *mm = nullptr;
-    for (int k = 0; k < 9; ++k) {
-      char *a = nullptr;
-      CK(hipMalloc(&a, n * 4 + (2u << 20)));
-      if (k < 8) Q.p[k] = reinterpret_cast<const f4 *>(a + (size_t)k * 4096);
-      else mm = reinterpret_cast<f4 *>(a);
-    }
-    lays.push_back({"separate +2MiB, k*4KiB offsets", Q, mm});
-  }
-  for (auto &L : lays) {
-    for (int k = 0; k < 8; ++k)
-      fill_k<<<4096, 256>>>(const_cast<float *>(reinterpret_cast<const float *>(L.p.p[k])), n, 1000 + k);
-    fill_k<<<4096, 256>>>(reinterpret_cast<float *>(L.m), n, 77);
-  }
+  f4 *am = reinterpret_cast<f4 *>(ar + (size_t)8 * n * 4);
+  fill_k<<<4096, 256>>>(reinterpret_cast<float *>(am), n, 77);
   CK(hipDeviceSynchronize());
-  for (size_t li = 0; li < lays.size(); ++li) {
-    f4 *mm = lays[li].m;
-    const Ptrs pp = lays[li].p;
-    const unsigned g2 = grid(2, 4), g8 = grid(8, 1);
-    vs.push_back(V{"sum  " + lays[li].name, sum_bytes,
-                   [=]() { bsum<8, 4, true, false, false><<<g2, kB>>>(mm, mm, pp, n4); }, {}});
-    vs.push_back(V{"read " + lays[li].name, 9.0 * n * 4,
-                   [=]() { read_only<8><<<g8, kB>>>(mm, mm, pp, n4, 0); }, {}});
-  }
+  ADD("arena U4 pc2 (prod)", sum_bytes, (bsum<8, 4, true, false, false><<<grid(2, 4), kB>>>(am, am, A, n4)));
+  ADD("arena U1 pc8", sum_bytes, (bsum<8, 1, true, false, false><<<grid(8, 1), kB>>>(am, am, A, n4)));
+  ADD("arena U2 pc1", sum_bytes, (bsum<8, 2, true, false, false><<<grid(1, 2), kB>>>(am, am, A, n4)));
+  ADD("arena U2 pc2", sum_bytes, (bsum<8, 2, true, false, false><<<grid(2, 2), kB>>>(am, am, A, n4)));
+  ADD("arena U2 pc4", sum_bytes, (bsum<8, 2, true, false, false><<<grid(4, 2), kB>>>(am, am, A, n4)));
+  ADD("arena U4 pc1", sum_bytes, (bsum<8, 4, true, false, false><<<grid(1, 4), kB>>>(am, am, A, n4)));
+  ADD("arena U4 pc3", sum_bytes, (bsum<8, 4, true, false, false><<<grid(3, 4), kB>>>(am, am, A, n4)));
+  ADD("arena U4 pc4", sum_bytes, (bsum<8, 4, true, false, false><<<grid(4, 4), kB>>>(am, am, A, n4)));
+  ADD("arena U8 pc1", sum_bytes, (bsum<8, 8, true, false, false><<<grid(1, 8), kB>>>(am, am, A, n4)));
+  ADD("arena U4 pc2 ntS", sum_bytes, (bsum<8, 4, true, false, true><<<grid(2, 4), kB>>>(am, am, A, n4)));
+  ADD("arena U4 pc2 plain loads", sum_bytes, (bsum<8, 4, false, false, false><<<grid(2, 4), kB>>>(am, am, A, n4)));
+  ADD("arena read9 only pc8", 9.0 * n * 4, (read_only<8><<<grid(8, 1), kB>>>(am, am, A, n4, 0)));
 
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
