@@ -1,6 +1,6 @@
 // geeps_clock_bench — end-to-end clock rate of libgeeps through the public API.
 //
-//   geeps_clock_bench <process_id> <num_processes> <base_port> <rows> <clocks> <warmup>
+//   geeps_clock_bench <process_id> <num_processes> <base_port> <rows> <clocks> <warmup> [slack]
 //
 // One table of `rows` RowData rows; per clock the app does what apps/helloworld
 // does, at scale: Read(all rows) -> PreUpdate(all rows) -> PostRead -> Update
@@ -35,6 +35,7 @@ int main(int argc, char **argv) {
   const int pid = std::atoi(argv[1]), P = std::atoi(argv[2]), base = std::atoi(argv[3]);
   const size_t rows = std::strtoull(argv[4], 0, 10);
   const int clocks = std::atoi(argv[5]), warmup = std::atoi(argv[6]);
+  const int slack = argc > 7 ? std::atoi(argv[7]) : 0;
   GeePsConfig cfg;
   for (int i = 0; i < P; ++i) {
     cfg.host_list.push_back("127.0.0.1");
@@ -43,7 +44,7 @@ int main(int argc, char **argv) {
   GeePs *ps = new GeePs(pid, cfg);
   std::vector<size_t> ids(rows);
   for (size_t r = 0; r < rows; ++r) ids[r] = r;
-  const int hr = ps->VirtualRead(0, ids, 0);
+  const int hr = ps->VirtualRead(0, ids, slack);
   const int hp = ps->VirtualPreUpdate(0, ids);
   const int hpr = ps->VirtualPostRead(hr);
   const int hu = ps->VirtualUpdate(hp);
@@ -80,8 +81,8 @@ int main(int argc, char **argv) {
   const double per = s / clocks;
   const double table_bytes = (double)rows * sizeof(RowData);
   std::printf("{\"process\": %d, \"processes\": %d, \"rows\": %zu, \"table_bytes\": %.0f, "
-              "\"clocks\": %d, \"ms_per_clock\": %.4f, \"delta_GBps\": %.2f, \"probe\": %.1f}\n",
-              pid, P, rows, table_bytes, clocks, per * 1e3, table_bytes / per / 1e9, probe);
+              "\"slack\": %d, \"clocks\": %d, \"ms_per_clock\": %.4f, \"delta_GBps\": %.2f, \"probe\": %.1f}\n",
+              pid, P, rows, table_bytes, slack, clocks, per * 1e3, table_bytes / per / 1e9, probe);
   std::fflush(stdout);
   std::fprintf(stderr, "stats %s\n", ps->GetStats().c_str());
   ps->Shutdown();

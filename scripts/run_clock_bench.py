@@ -1,0 +1,68 @@
+"""Launch geeps_clock_bench as P local processes (one GeePS worker + tablet
+server each) and print one aggregate JSON line.
+
+    python scripts/run_clock_bench.py P ROWS CLOCKS WARMUP SLACK [ipc|tcp] [out.json]
+
+Every worker updates every row each clock, so the job reduces P full delta
+tables per clock: aggregate delta rate = P * rows * 512 B / (slowest worker's
+ms per clock).  All processes share the one GPU of the box (HIP_VISIBLE_DEVICES
+is left alone).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(REPO, "build", "apps", "geeps_clock_bench")
+
+
+def free_base(P):
+    # ports base + 16*p (+channel) must be free; take the OS's pick as a base
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        base = s.getsockname()[1]
+    return max(20000, min(base, 60000 - 16 * P))
+
+
+def main():
+    P, rows, clocks, warmup, slack = (int(a) for a in sys.argv[1:6])
+    transport = sys.argv[6] if len(sys.argv) > 6 else "ipc"
+    out = sys.argv[7] if len(sys.argv) > 7 else None
+    env = dict(os.environ)
+    if transport == "tcp":
+        env["GEEPS_TRANSPORT"] = "tcp"
+    else:
+        env.pop("GEEPS_TRANSPORT", None)
+    base = free_base(P)
+    procs = [subprocess.Popen([BIN, str(p), str(P), str(base), str(rows), str(clocks),
+                               str(warmup), str(slack)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for p in range(P)]
+    results, failed = [], False
+    for p, pr in enumerate(procs):
+        o, e = pr.communicate(timeout=900)
+        if pr.returncode != 0:
+            failed = True
+            sys.stderr.write(f"process {p} rc={pr.returncode}\n{e[-2000:]}\n")
+            continue
+        results.append(json.loads(o.strip().splitlines()[-1]))
+    if failed:
+        sys.exit(1)
+    worst = max(r["ms_per_clock"] for r in results)
+    table = results[0]["table_bytes"]
+    line = {"workers": P, "rows": rows, "table_bytes": table, "slack": slack,
+            "transport": transport, "clocks": clocks, "warmup": warmup,
+            "ms_per_clock_max": worst,
+            "ms_per_clock": [r["ms_per_clock"] for r in results],
+            "aggregate_delta_GBps": round(P * table / (worst * 1e-3) / 1e9, 2),
+            "probe": [r["probe"] for r in results]}
+    print(json.dumps(line))
+    if out:
+        with open(out, "w") as f:
+            f.write(json.dumps(line) + "\n")
+
+
+if __name__ == "__main__":
+    main()
