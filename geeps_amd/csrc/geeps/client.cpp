@@ -194,22 +194,25 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       cs_clock_with_updates_batch_msg_t h;
       std::memcpy(&h, parts[0].data, sizeof h);
       GP_CHECK_EQ(h.client_id, client_id);
-      const size_t n = parts[1].size / sizeof(RowKey);
+      size_t n = parts[1].size / sizeof(RowKey);
       UpdateBatch b;
       b.client_id = h.client_id;
       b.clock = h.clock;
       b.table_id = h.table_id;
-      auto keys = std::make_shared<std::vector<RowKey>>(n);
-      if (n) std::memcpy(keys->data(), parts[1].data, parts[1].size);
-      b.keys = keys->data();
-      b.num_rows = n;
-      b.keys_owner = keys;
+      if (n) {
+        auto keys = std::make_shared<std::vector<RowKey>>(n);
+        std::memcpy(keys->data(), parts[1].data, parts[1].size);
+        b.keys = keys->data();
+        b.keys_owner = keys;
+      }
       if (parts.size() == 4) {
         // Same-node client: the rows stay in its oplog, mapped here over IPC.
         GP_CHECK(parts[2].size == 0 && parts[3].size == sizeof(IpcRowsRef));
         IpcRowsRef ref;
         std::memcpy(&ref, parts[3].data, sizeof ref);
-        GP_CHECK_EQ(ref.bytes, n * kRowBytes);
+        GP_CHECK(ref.bytes % kRowBytes == 0);
+        if (n) GP_CHECK_EQ(ref.bytes, n * kRowBytes);
+        n = ref.bytes / kRowBytes;  // key part omitted after the first message
         auto &mapped = ch.ipc_oplogs[client_id];
         if (ref.has_handle) {
           auto old = mapped.find(ref.buffer_id);
@@ -227,6 +230,7 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
         GP_CHECK_EQ(parts[2].size, n * kRowBytes);
         b.host_rows = ctx.rows;
       }
+      b.num_rows = n;
       ch.server->post_updates(std::move(b));
     } else if (cmd == kCmdIpcInbox) {
       GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(IpcInboxMsg));
@@ -853,6 +857,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
   std::shared_ptr<const std::vector<RowKey>> keys;  // immutable after FinishVirtualIteration
   size_t pool_id = 0;
   std::vector<uint8_t> *exported = nullptr;  // app thread only
+  std::vector<uint8_t> *keys_sent = nullptr;  // app thread only
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[table_id];
@@ -869,6 +874,8 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       if (pc.exported.size() < pc.oplog_pool.size())
         pc.exported.resize(pc.oplog_pool.size(), std::vector<uint8_t>(num_processes_, 0));
       exported = &pc.exported[pool_id];
+      if (pc.ipc_keys_sent.size() < num_processes_) pc.ipc_keys_sent.assign(num_processes_, 0);
+      keys_sent = &pc.ipc_keys_sent;
       // reclaim_oplog now, unless it must outlive the refresh (read-my-writes
       // re-apply; same-node servers copying out of it): then recv_row_batch
       // reclaims it once every server's data age covers the clock.
@@ -920,8 +927,11 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
         ref.has_handle = 1;
         (*exported)[s] = 1;
       }
-      send_to_server(ch, s, {Part{&h, sizeof h}, Part{keys->data() + a, n * sizeof(RowKey)},
+      const bool with_keys = !(*keys_sent)[s];
+      send_to_server(ch, s, {Part{&h, sizeof h},
+                             with_keys ? Part{keys->data() + a, n * sizeof(RowKey)} : Part{nullptr, 0},
                              Part{nullptr, 0}, Part{&ref, sizeof ref}});
+      (*keys_sent)[s] = 1;
     } else {
       const size_t floats = n * ROW_DATA_SIZE;
       if (ch.send_buf.size() < floats) ch.send_buf.resize(floats);

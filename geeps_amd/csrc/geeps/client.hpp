@@ -82,6 +82,7 @@ struct ParamCache {
   // server writes over IPC), and which oplog buffers each server has mapped
   std::vector<std::array<std::unique_ptr<DeviceArray<float>>, kInboxSlots>> inbox;
   std::vector<std::vector<uint8_t>> exported;  // [oplog pool index][server]
+  std::vector<uint8_t> ipc_keys_sent;           // [server]: shard keys already sent
 };
 
 // Server-side view of a same-node client's IPC exports.

@@ -180,6 +180,8 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
   if (t.row_count == 0) {
     // The first message defines the shard: zeroed master, keys copied
     // (tablet-server.cpp:108-114).  Later messages are summed positionally.
+    GP_CHECK_MSG(b.keys, "first update batch of table " << b.table_id << " from client "
+                                                          << b.client_id << " carries no row keys");
     t.row_count = batch_size;
     t.master.resize(batch_size * ROW_DATA_SIZE);
     GP_CALL(gp_zero(t.master.data(), t.master.size(), stream_.get()));

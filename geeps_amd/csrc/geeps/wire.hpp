@@ -82,6 +82,10 @@ constexpr uint32_t kIpcHandleBytes = 64;
 constexpr uint32_t kInboxSlots = 2;
 
 // 4th part of a CLOCK_WITH_UPDATES_BATCH whose rows stay in the client's oplog.
+// The RowKey part is sent on the first such message per (server, table) only:
+// the server takes the shard's keys from its first message and sums later ones
+// positionally (tablet-server.cpp:108-116), so later messages carry an empty
+// key part and the row count is bytes / sizeof(RowData).
 struct IpcRowsRef {
   uint64_t buffer_id;   // (table << 32) | oplog pool index: stable, unique per client
   uint64_t offset;      // bytes from the buffer base to this server's slice

@@ -7,6 +7,9 @@ Every worker updates every row each clock, so the job reduces P full delta
 tables per clock: aggregate delta rate = P * rows * 512 B / (slowest worker's
 ms per clock).  All processes share the one GPU of the box (HIP_VISIBLE_DEVICES
 is left alone).
+
+With CLOCK_BENCH_PROF=<dir> set, each worker runs under
+``rocprofv3 --kernel-trace --memory-copy-trace --stats`` into <dir>/p<id>/.
 """
 import json
 import os
@@ -36,8 +39,17 @@ def main():
     else:
         env.pop("GEEPS_TRANSPORT", None)
     base = free_base(P)
-    procs = [subprocess.Popen([BIN, str(p), str(P), str(base), str(rows), str(clocks),
-                               str(warmup), str(slack)],
+    prof = os.environ.get("CLOCK_BENCH_PROF")
+
+    def cmd(p):
+        c = [BIN, str(p), str(P), str(base), str(rows), str(clocks), str(warmup), str(slack)]
+        if prof:
+            c = ["rocprofv3", "--kernel-trace", "--memory-copy-trace", "--stats",
+                 "--output-format", "csv", "-d", os.path.join(prof, f"p{p}"), "-o", "run",
+                 "--"] + c
+        return c
+
+    procs = [subprocess.Popen(cmd(p),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
              for p in range(P)]
     results, failed = [], False
