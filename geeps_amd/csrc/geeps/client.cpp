@@ -45,7 +45,8 @@ std::string ClientStats::to_json() const {
   std::ostringstream o;
   o << "{\"nr_read\": " << nr_read << ", \"nr_update\": " << nr_update
     << ", \"nr_clock\": " << nr_clock << ", \"nr_push\": " << nr_push
-    << ", \"nr_refresh\": " << nr_refresh << ", \"rows_updated\": " << rows_updated
+    << ", \"nr_refresh\": " << nr_refresh << ", \"nr_refresh_in_place\": " << nr_refresh_in_place
+    << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
     << ", \"update_time\": " << update_time << ", \"push_time\": " << push_time
@@ -103,6 +104,7 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->client_fd.assign(num_processes_, -1);
     ch->ipc_oplogs.resize(num_processes_);
     ch->inbox_of.assign(num_processes_, std::vector<InboxEntry>(config_.num_tables));
+    ch->client_done.assign(num_processes_, 0);
     channels_[c] = std::move(ch);
   }
   start_network();
@@ -260,7 +262,13 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       std::memcpy(&h, parts[0].data, sizeof h);
       ch.server->post_clock(h.client_id, h.clock, h.table_id);
     } else if (cmd == SHUTDOWN) {
-      // The client sends nothing after this (shutdown handshake).
+      // The client sends nothing after this (shutdown handshake): a refresh
+      // waiting for one of its slots to be released would wait forever.
+      {
+        std::lock_guard<std::mutex> lk(ch.ipc_mu);
+        ch.client_done[client_id] = 1;
+      }
+      ch.ipc_cv.notify_all();
       ch.server->post_shutdown(client_id);
       break;
     } else {
@@ -302,20 +310,25 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
       GP_CHECK_LT(sl.slot, kInboxSlots);
       auto &slot = ch.tables[h.table_id].inbox[server_id][sl.slot];
       GP_CHECK(slot);
-      recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock, slot->data(),
-                     sl.num_rows, true);
-      RefreshAckMsg a{};
-      a.cmd = kCmdRefreshAck;
-      a.client_id = process_id_;
-      a.table_id = h.table_id;
-      a.slot = sl.slot;
-      ack_to_server(ch, server_id, a);
+      // The slot becomes the live copy of this shard (read in place by the
+      // segmented gather); the slot it replaces goes back to the server.
+      const int retired = recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age,
+                                         h.self_clock, slot->data(), sl.num_rows, (int)sl.slot);
+      if (retired >= 0) {
+        RefreshAckMsg a{};
+        a.cmd = kCmdRefreshAck;
+        a.client_id = process_id_;
+        a.table_id = h.table_id;
+        a.slot = (uint32_t)retired;
+        ack_to_server(ch, server_id, a);
+      }
       continue;
     }
     const size_t n = parts[1].size / sizeof(RowKey);
     GP_CHECK_EQ(parts[2].size, n * kRowBytes);
-    recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
-                   static_cast<const float *>(parts[2].data), n, false);
+    const int retired = recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
+                                       static_cast<const float *>(parts[2].data), n, -1);
+    GP_CHECK_MSG(retired < 0, "socket refresh replaced an IPC slot of server " << server_id);
   }
 }
 
@@ -331,15 +344,25 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
     if (e.registered) ib = &e;
   }
   if (!ib || r.num_rows == 0) return false;
-  const uint32_t slot = (uint32_t)(((r.data_age % 2) + 2) % 2);
+  // The client reads its live slot in place until the next refresh replaces
+  // it, so at most one slot is held there: wait for a free one.
+  uint32_t slot = 0;
   {
     std::unique_lock<std::mutex> lk(ch.ipc_mu);
-    while (ib->busy[slot]) {
-      if (!ch.ipc_cv.wait_for(lk, std::chrono::milliseconds(kWaitWarnMs),
-                              [&] { return !ib->busy[slot]; }))
+    auto ready = [&] {
+      if (ch.client_done[client_id]) return true;
+      for (uint32_t k = 0; k < kInboxSlots; ++k)
+        if (!ib->busy[k]) return true;
+      return false;
+    };
+    while (!ready()) {
+      if (!ch.ipc_cv.wait_for(lk, std::chrono::milliseconds(kWaitWarnMs), ready))
         std::cerr << "server " << process_id_ << " waiting for client " << client_id
-                  << " to consume refresh slot " << slot << std::endl;
+                  << " to release a refresh slot" << std::endl;
     }
+    // A client that has shut down reads nothing more: the refresh is dropped.
+    if (ch.client_done[client_id]) return true;
+    while (ib->busy[slot]) ++slot;
     ib->busy[slot] = true;
   }
   const size_t bytes = r.num_rows * kRowBytes;
@@ -420,7 +443,7 @@ void ClientLib::remote_shutdown_ack(uint32_t channel, uint32_t client_id) {
 void ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r) {
   if (client_id == process_id_) {
     recv_row_batch(channel, r.server_id, r.table_id, r.data_age, r.self_clock, r.device_rows,
-                   r.num_rows, true);
+                   r.num_rows, -1);
     return;
   }
   Channel &ch = *channels_[channel];
@@ -544,6 +567,7 @@ void ClientLib::finish_virtual_iteration() {
         pc.server_num_rows[i] = div + (i < res ? 1 : 0);
       }
       pc.per_server_data_age.assign(num_processes_, INITIAL_DATA_AGE);
+      pc.live_slot.assign(num_processes_, -1);
       pc.server_clock.assign(num_processes_, INITIAL_DATA_AGE);
     }
     ch.stream->sync();
@@ -709,7 +733,12 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
       }
     }
     waited += now_s() - w0;
-    if (op.ch_size[ch.id])
+    if (op.ch_size[ch.id] && pc.segmented)
+      GP_CALL(gp_gather_rows_segmented(reinterpret_cast<float *>(op.buffer.data()), &pc.segs,
+                                       op.index.data() + op.ch_start[ch.id], op.ch_size[ch.id],
+                                       gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit,
+                                       ch.stream->get()));
+    else if (op.ch_size[ch.id])
       GP_CALL(gp_gather_rows(reinterpret_cast<float *>(op.buffer.data()), pc.data.data(),
                              op.index.data() + op.ch_start[ch.id], op.ch_size[ch.id],
                              gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit,
@@ -799,7 +828,11 @@ void ClientLib::update_batch(int handle) {
         GP_CALL(gp_scatter_add_rows(oplog->data(), pre.buffer.data(), idx, n,
                                     gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
                                     ch.stream->get()));
-      if (config_.read_my_writes)
+      if (config_.read_my_writes && pc.segmented)
+        GP_CALL(gp_scatter_add_rows_segmented(&pc.segs, pre.buffer.data(), idx, n,
+                                              gp_double_index{0, 0}, ROW_DATA_SIZE,
+                                              pre.num_vals_limit, ch.stream->get()));
+      else if (config_.read_my_writes)
         GP_CALL(gp_scatter_add_rows(pc.data.data(), pre.buffer.data(), idx, n,
                                     gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
                                     ch.stream->get()));
@@ -963,11 +996,12 @@ void ClientLib::reclaim_oplogs(ParamCache &pc, iter_t upto) {
 
 // recv_row_batch + recv_row_batch_gpu + server_clock_cbk
 // (clientlib-data.cpp:51-151, clientlib-cbk.cpp:81-104).
-void ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id,
-                               iter_t data_age, iter_t self_clock, const float *rows,
-                               size_t num_rows, bool device) {
+int ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id,
+                              iter_t data_age, iter_t self_clock, const float *rows,
+                              size_t num_rows, int slot) {
   const double t0 = now_s();
   Channel &ch = *channels_[channel];
+  int retired = -1;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     GP_CHECK_LT(table_id, ch.tables.size());
@@ -990,9 +1024,15 @@ void ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t ta
       pc.server_clock_min = min_clock;
     }
     if (num_rows) {
-      float *dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
+      float *dst;
+      if (slot >= 0) {
+        // Already in our inbox slot: it becomes the live copy of the shard.
+        dst = const_cast<float *>(rows);
+      } else {
+        dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
+        GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.recv_stream->get()));
+      }
       const size_t floats = num_rows * ROW_DATA_SIZE;
-      GP_CALL(gp_memcpy_async(dst, rows, floats * 4, ch.recv_stream->get()));
       if (config_.read_my_writes) {
         // Re-apply this client's own not-yet-reflected updates
         // (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
@@ -1004,14 +1044,54 @@ void ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t ta
         }
       }
       ch.recv_stream->sync();
+      const int prev = pc.live_slot[server_id];
+      GP_CHECK_MSG(slot < 0 || prev != slot, "server " << server_id << " rewrote live slot " << slot);
+      if (prev != slot) {
+        pc.live_slot[server_id] = slot;
+        retired = prev;
+        rebuild_segments(pc);
+      }
     }
     pc.data_age = *std::min_element(pc.per_server_data_age.begin(), pc.per_server_data_age.end());
   }
   ch.cv.notify_all();
-  (void)device;
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_refresh++;
+  if (slot >= 0) stats_.nr_refresh_in_place++;
   stats_.refresh_time += now_s() - t0;
+  return retired;
+}
+
+// The cache as row ranges: each server's shard is read from the cache's own
+// `data` or from its live inbox slot; neighbouring ranges of `data` merge.
+void ClientLib::rebuild_segments(ParamCache &pc) {
+  gp_row_segments t{};
+  bool any_slot = false;
+  const float *next_flat = nullptr;  // where a merged `data` range would continue
+  for (uint32_t s = 0; s < num_processes_; ++s) {
+    const size_t n = pc.server_num_rows[s];
+    if (n == 0) continue;
+    const size_t first = pc.server_row_start[s];
+    float *base;
+    if (pc.live_slot[s] >= 0) {
+      base = pc.inbox[s][pc.live_slot[s]]->data();
+      any_slot = true;
+    } else {
+      base = pc.data.data() + first * ROW_DATA_SIZE;
+    }
+    if (t.count && base == next_flat && pc.live_slot[s] < 0) {
+      next_flat = base + n * ROW_DATA_SIZE;
+      continue;
+    }
+    GP_CHECK_MSG(t.count < GP_MAX_SEGMENTS, "param cache split into more than "
+                                                << GP_MAX_SEGMENTS << " segments");
+    t.first_row[t.count] = t.count ? first : 0;
+    t.base[t.count] = base;
+    ++t.count;
+    next_flat = pc.live_slot[s] < 0 ? base + n * ROW_DATA_SIZE : nullptr;
+  }
+  pc.segs = t;
+  pc.segmented = any_slot;
 }
 
 // ---------------------------------------------------------------------------

@@ -83,6 +83,14 @@ struct ParamCache {
   std::vector<std::array<std::unique_ptr<DeviceArray<float>>, kInboxSlots>> inbox;
   std::vector<std::vector<uint8_t>> exported;  // [oplog pool index][server]
   std::vector<uint8_t> ipc_keys_sent;           // [server]: shard keys already sent
+  // Where each server's shard rows are read from: -1 = this cache's own range
+  // of `data`; k = inbox slot k, which the same-node server's last refresh
+  // wrote over IPC and which stays live (un-ACKed) until the next refresh
+  // replaces it.  `segs` describes the resulting split cache for the
+  // segmented gather / scatter-add; `segmented` = some shard lives in a slot.
+  std::vector<int> live_slot;
+  gp_row_segments segs{};
+  bool segmented = false;
 };
 
 // Server-side view of a same-node client's IPC exports.
@@ -95,6 +103,7 @@ struct InboxEntry {
 
 struct ClientStats {
   uint64_t nr_read = 0, nr_update = 0, nr_clock = 0, nr_push = 0, nr_refresh = 0;
+  uint64_t nr_refresh_in_place = 0;  // same-node refreshes read from the inbox slot
   uint64_t rows_updated = 0, rows_read = 0, bytes_pushed_remote = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
@@ -142,6 +151,8 @@ struct Channel {
   // server side, same-node clients: mapped oplog buffers and refresh inboxes
   std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
   std::vector<std::vector<InboxEntry>> inbox_of;         // [client][table]
+  // [client]: its SHUTDOWN arrived (it reads no more, and its ACKs stop)
+  std::vector<uint8_t> client_done;
   std::mutex ipc_mu;
   std::condition_variable ipc_cv;
 };
@@ -167,8 +178,11 @@ class ClientLib {
   void shutdown();
 
   // server -> client refresh (recv_row_batch, clientlib-data.cpp:51-108)
-  void recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id, iter_t data_age,
-                      iter_t self_clock, const float *rows, size_t num_rows, bool device);
+  // `slot` >= 0: the rows are already in our inbox slot `slot` (same-node
+  // server); returns the slot the refresh retired (to ACK), or -1.
+  int recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id, iter_t data_age,
+                     iter_t self_clock, const float *rows, size_t num_rows, int slot);
+  void rebuild_segments(ParamCache &pc);
   void remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r);
   void remote_shutdown_ack(uint32_t channel, uint32_t client_id);
   // Let in-flight device work finish (process exit without Shutdown()).

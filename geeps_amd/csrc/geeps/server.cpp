@@ -190,18 +190,12 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
   GP_CHECK_EQ(t.row_count, batch_size);
 
   Pending p;
-  if (b.device_rows && b.device_remote) {
-    // Same-node peer: one device-to-device copy out of its oplog (xGMI between
-    // GPUs); the peer keeps the slice until our refresh tells it we are done.
-    const double t0 = now_s();
-    auto stage = stage_buffer(t);
-    GP_CALL(gp_memcpy_async(stage->data(), b.device_rows,
-                            batch_size * ROW_DATA_SIZE * sizeof(float), stream_.get()));
-    stream_.sync();
-    stats_.stage_time += now_s() - t0;
-    p.rows = stage->data();
-    p.keepalive = stage;
-  } else if (b.device_rows) {
+  if (b.device_rows) {
+    // In-process client: its oplog slice, read in place (keepalive holds it).
+    // Same-node peer: its oplog slice mapped over IPC, also read in place (over
+    // xGMI when the peer is another GPU).  The peer reclaims an oplog only once
+    // every server's refresh covers its clock (recv_row_batch), and a refresh
+    // leaves here only after apply_pending has consumed the bucket.
     p.rows = b.device_rows;
     p.keepalive = std::move(b.keepalive);
   } else {

@@ -225,6 +225,31 @@ __device__ __forceinline__ void row_endpoints(const gp_double_index &ix,
   }
 }
 
+// Where the cache side of a row op lives.  kFlat: one buffer (x or y as
+// passed).  kSegX / kSegY: the cache rows (`from` of a gather / `to` of a
+// scatter-add) are split over the buffers of a gp_row_segments table, passed
+// by value as a kernel argument.
+enum SegMode : int { kFlat = 0, kSegX = 1, kSegY = 2 };
+
+template <int SEG>
+struct SegArg {};
+template <>
+struct SegArg<kSegX> {
+  gp_row_segments t;
+};
+template <>
+struct SegArg<kSegY> {
+  gp_row_segments t;
+};
+
+// Segment i holding cache row `row` (first_row ascending, first_row[0] == 0).
+__device__ __forceinline__ float *seg_row(const gp_row_segments &t, uint64_t row,
+                                          size_t row_size) {
+  uint32_t s = 0;
+  for (uint32_t i = 1; i < t.count; ++i) s += (t.first_row[i] <= row) ? 1u : 0u;
+  return t.base[s] + (row - t.first_row[s]) * row_size;
+}
+
 // T = f4 (VEC 4) or float (VEC 1).  A group of LPR consecutive lanes owns a
 // row; each group handles RPG rows per iteration, all their loads issued
 // before the first store.  `vw` = row_size / VEC (vectors per row).
@@ -308,42 +333,121 @@ __global__ __launch_bounds__(kBlock) void row_op_kernel(
   }
 }
 
-template <typename T, int VEC, int OP, int LPR>
+// Segmented form (kSegX: gather from the segmented cache; kSegY: scatter-add
+// into it): the same lane/row mapping, with each cache-side row resolved to a
+// pointer through the segment table once per row.  A separate kernel so the
+// flat kernels above keep their register budget.
+template <typename T, int VEC, int OP, int LPR, int RPG, int SEG>
+__global__ __launch_bounds__(kBlock) void row_op_seg_kernel(
+    float *__restrict__ y, const float *__restrict__ x,
+    const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
+    uint64_t off1, size_t row_size, size_t vw, size_t limit, const SegArg<SEG> seg) {
+  static_assert(SEG == kSegX || SEG == kSegY, "segmented side");
+  constexpr int kGroups = kBlock / LPR;
+  const int lane = threadIdx.x % LPR;
+  const size_t group = (size_t)blockIdx.x * kGroups + threadIdx.x / LPR;
+  const size_t gstride = (size_t)gridDim.x * kGroups * RPG;
+
+  for (size_t r0 = group * RPG; r0 < num_rows; r0 += gstride) {
+    uint64_t guarded[RPG];
+    const float *xr[RPG];
+    float *yr[RPG];
+    bool live[RPG], whole[RPG];
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+      const size_t r = r0 + k;
+      live[k] = r < num_rows;
+      guarded[k] = 0;
+      xr[k] = x;
+      yr[k] = y;
+      whole[k] = false;
+      if (live[k]) {
+        const gp_double_index ix = index[r];
+        uint64_t from, to;
+        row_endpoints<OP>(ix, off0, off1, from, to);
+        guarded[k] = (OP == kAssignTo) ? to : from;
+        whole[k] = (guarded[k] + 1) * row_size <= limit;
+        xr[k] = SEG == kSegX ? seg_row(seg.t, from, row_size) : x + from * row_size;
+        yr[k] = SEG == kSegY ? seg_row(seg.t, to, row_size) : y + to * row_size;
+      }
+    }
+    bool all_whole = true;
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) all_whole = all_whole && (whole[k] || !live[k]);
+
+    if (all_whole) {
+      for (size_t j = lane; j < vw; j += LPR) {
+        T xs[RPG], ys[RPG];
+#pragma unroll
+        for (int k = 0; k < RPG; ++k)
+          if (live[k]) xs[k] = reinterpret_cast<const T *>(xr[k])[j];
+        if (OP == kAddFrom) {
+#pragma unroll
+          for (int k = 0; k < RPG; ++k)
+            if (live[k]) ys[k] = reinterpret_cast<const T *>(yr[k])[j];
+        }
+#pragma unroll
+        for (int k = 0; k < RPG; ++k)
+          if (live[k])
+            reinterpret_cast<T *>(yr[k])[j] = OP == kAddFrom ? ys[k] + xs[k] : xs[k];
+      }
+    } else {
+#pragma unroll 1
+      for (int k = 0; k < RPG; ++k) {
+        if (!live[k]) continue;
+        for (size_t e = lane; e < row_size; e += LPR)
+          if (guarded[k] * row_size + e < limit) {
+            if (OP == kAddFrom)
+              yr[k][e] += xr[k][e];
+            else
+              yr[k][e] = xr[k][e];
+          }
+      }
+    }
+  }
+}
+
+template <typename T, int VEC, int OP, int SEG, int LPR>
 void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
                        size_t n, uint64_t off0, uint64_t off1, size_t row_size,
-                       size_t limit, hipStream_t s) {
+                       size_t limit, const SegArg<SEG> &seg, hipStream_t s) {
   // Keep ~8 independent 16-B loads per lane in flight.
   constexpr int RPG = (OP == kAddFrom) ? 4 : 8;
   constexpr int kGroups = kBlock / LPR;
   const size_t groups = (n + RPG - 1) / RPG;
   size_t grid = (groups + kGroups - 1) / kGroups;
   if (grid > grid_cap()) grid = grid_cap();
-  hipLaunchKernelGGL((row_op_kernel<T, VEC, OP, LPR, RPG>), dim3((unsigned)grid),
-                     dim3(kBlock), 0, s, y, x, idx, n, off0, off1, row_size,
-                     row_size / VEC, limit);
+  if constexpr (SEG == kFlat)
+    hipLaunchKernelGGL((row_op_kernel<T, VEC, OP, LPR, RPG>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, y, x, idx, n, off0, off1, row_size,
+                       row_size / VEC, limit);
+  else
+    hipLaunchKernelGGL((row_op_seg_kernel<T, VEC, OP, LPR, RPG, SEG>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, y, x, idx, n, off0, off1, row_size,
+                       row_size / VEC, limit, seg);
 }
 
-template <typename T, int VEC, int OP>
+template <typename T, int VEC, int OP, int SEG>
 void launch_row_op_t(float *y, const float *x, const gp_double_index *idx,
                      size_t n, uint64_t off0, uint64_t off1, size_t row_size,
-                     size_t limit, hipStream_t s) {
+                     size_t limit, const SegArg<SEG> &seg, hipStream_t s) {
   const size_t vw = row_size / VEC;
   // Lanes per row: the smallest power of two covering the row, capped at a
   // wave; short rows (64 / 128 floats) pack 4 / 2 rows into one wave.
   if (vw <= 1)
-    launch_row_op_lpr<T, VEC, OP, 1>(y, x, idx, n, off0, off1, row_size, limit, s);
+    launch_row_op_lpr<T, VEC, OP, SEG, 1>(y, x, idx, n, off0, off1, row_size, limit, seg, s);
   else if (vw <= 2)
-    launch_row_op_lpr<T, VEC, OP, 2>(y, x, idx, n, off0, off1, row_size, limit, s);
+    launch_row_op_lpr<T, VEC, OP, SEG, 2>(y, x, idx, n, off0, off1, row_size, limit, seg, s);
   else if (vw <= 4)
-    launch_row_op_lpr<T, VEC, OP, 4>(y, x, idx, n, off0, off1, row_size, limit, s);
+    launch_row_op_lpr<T, VEC, OP, SEG, 4>(y, x, idx, n, off0, off1, row_size, limit, seg, s);
   else if (vw <= 8)
-    launch_row_op_lpr<T, VEC, OP, 8>(y, x, idx, n, off0, off1, row_size, limit, s);
+    launch_row_op_lpr<T, VEC, OP, SEG, 8>(y, x, idx, n, off0, off1, row_size, limit, seg, s);
   else if (vw <= 16)
-    launch_row_op_lpr<T, VEC, OP, 16>(y, x, idx, n, off0, off1, row_size, limit, s);
+    launch_row_op_lpr<T, VEC, OP, SEG, 16>(y, x, idx, n, off0, off1, row_size, limit, seg, s);
   else if (vw <= 32)
-    launch_row_op_lpr<T, VEC, OP, 32>(y, x, idx, n, off0, off1, row_size, limit, s);
+    launch_row_op_lpr<T, VEC, OP, SEG, 32>(y, x, idx, n, off0, off1, row_size, limit, seg, s);
   else
-    launch_row_op_lpr<T, VEC, OP, 64>(y, x, idx, n, off0, off1, row_size, limit, s);
+    launch_row_op_lpr<T, VEC, OP, SEG, 64>(y, x, idx, n, off0, off1, row_size, limit, seg, s);
 }
 
 template <int OP>
@@ -353,10 +457,51 @@ int launch_row_op(float *y, const float *x, const gp_double_index *idx,
   if (n == 0) return GP_OK;
   if (!y || !x || !idx) return set_error(GP_ERR_INVALID, "null pointer");
   if (row_size == 0) return set_error(GP_ERR_INVALID, "row_size == 0");
+  const SegArg<kFlat> flat{};
   if (row_size % 4 == 0 && aligned16(y) && aligned16(x))
-    launch_row_op_t<f4, 4, OP>(y, x, idx, n, off.id0, off.id1, row_size, limit, s);
+    launch_row_op_t<f4, 4, OP, kFlat>(y, x, idx, n, off.id0, off.id1, row_size, limit, flat, s);
   else
-    launch_row_op_t<float, 1, OP>(y, x, idx, n, off.id0, off.id1, row_size, limit, s);
+    launch_row_op_t<float, 1, OP, kFlat>(y, x, idx, n, off.id0, off.id1, row_size, limit, flat, s);
+  GP_HIP_TRY(hipGetLastError());
+  return GP_OK;
+}
+
+int check_segments(const gp_row_segments *t, size_t row_size, bool *aligned) {
+  if (!t) return set_error(GP_ERR_INVALID, "null segment table");
+  if (t->count < 1 || t->count > GP_MAX_SEGMENTS)
+    return set_error(GP_ERR_INVALID, "segment count out of range");
+  if (t->first_row[0] != 0) return set_error(GP_ERR_INVALID, "first_row[0] != 0");
+  *aligned = row_size % 4 == 0;
+  for (uint32_t i = 0; i < t->count; ++i) {
+    if (!t->base[i]) return set_error(GP_ERR_INVALID, "null segment base");
+    if (i && t->first_row[i] <= t->first_row[i - 1])
+      return set_error(GP_ERR_INVALID, "segment first_row not ascending");
+    *aligned = *aligned && aligned16(t->base[i]);
+  }
+  return GP_OK;
+}
+
+// Segmented cache side: OP kAssignTo reads it (kSegX), kAddFrom writes it (kSegY).
+template <int OP, int SEG>
+int launch_row_op_seg(float *flat_ptr, const gp_row_segments *t,
+                      const gp_double_index *idx, size_t n, gp_double_index off,
+                      size_t row_size, size_t limit, hipStream_t s) {
+  if (n == 0) return GP_OK;
+  if (!flat_ptr || !idx) return set_error(GP_ERR_INVALID, "null pointer");
+  if (row_size == 0) return set_error(GP_ERR_INVALID, "row_size == 0");
+  bool vec = false;
+  const int rc = check_segments(t, row_size, &vec);
+  if (rc != GP_OK) return rc;
+  vec = vec && aligned16(flat_ptr);
+  SegArg<SEG> seg;
+  seg.t = *t;
+  // the flat side is y for a gather (kSegX) and x for a scatter-add (kSegY)
+  float *y = SEG == kSegX ? flat_ptr : nullptr;
+  const float *x = SEG == kSegY ? flat_ptr : nullptr;
+  if (vec)
+    launch_row_op_t<f4, 4, OP, SEG>(y, x, idx, n, off.id0, off.id1, row_size, limit, seg, s);
+  else
+    launch_row_op_t<float, 1, OP, SEG>(y, x, idx, n, off.id0, off.id1, row_size, limit, seg, s);
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;
 }
@@ -398,6 +543,22 @@ int gp_scatter_init_rows(float *y, const float *x, const gp_double_index *index,
                          size_t num_vals_limit, gp_stream s) {
   return launch_row_op<kInitFrom>(y, x, index, num_rows, offset, row_size,
                                   num_vals_limit, (hipStream_t)s);
+}
+
+int gp_gather_rows_segmented(float *y, const gp_row_segments *x_segments,
+                             const gp_double_index *index, size_t num_rows,
+                             gp_double_index offset, size_t row_size,
+                             size_t num_vals_limit, gp_stream s) {
+  return launch_row_op_seg<kAssignTo, kSegX>(y, x_segments, index, num_rows, offset, row_size,
+                                             num_vals_limit, (hipStream_t)s);
+}
+
+int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float *x,
+                                  const gp_double_index *index, size_t num_rows,
+                                  gp_double_index offset, size_t row_size,
+                                  size_t num_vals_limit, gp_stream s) {
+  return launch_row_op_seg<kAddFrom, kSegY>(const_cast<float *>(x), y_segments, index, num_rows,
+                                            offset, row_size, num_vals_limit, (hipStream_t)s);
 }
 
 int gp_bucket_sum_apply(float *master, const float *const *buckets,

@@ -16,6 +16,11 @@ LIB_PATH = os.path.join(_HERE, "lib", "libgp_reduce.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gp_reduce.h")
 
 GP_OK = 0
+GP_ERR_INVALID = 1
+GP_ERR_HIP = 2
+
+
+ABI_VERSION = 2  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -26,6 +31,17 @@ class DoubleIndex(ctypes.Structure):
     """``gp_double_index`` == reference ``DoubleIndex`` (src/common/row-op-util.hpp:40-44)."""
 
     _fields_ = [("id0", ctypes.c_uint64), ("id1", ctypes.c_uint64)]
+
+
+GP_MAX_SEGMENTS = 64  # include/gp_reduce.h
+
+
+class RowSegments(ctypes.Structure):
+    """``gp_row_segments``: a param cache split over up to 64 row-range buffers."""
+
+    _fields_ = [("count", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("first_row", ctypes.c_uint64 * GP_MAX_SEGMENTS),
+                ("base", ctypes.c_void_p * GP_MAX_SEGMENTS)]
 
 
 _c = ctypes
@@ -40,6 +56,10 @@ _SIGNATURES = {
     "gp_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_init_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
+    "gp_gather_rows_segmented": (_i, [_vp, _c.POINTER(RowSegments), _vp, _sz, DoubleIndex, _sz,
+                                      _sz, _vp]),
+    "gp_scatter_add_rows_segmented": (_i, [_c.POINTER(RowSegments), _vp, _vp, _sz, DoubleIndex,
+                                           _sz, _sz, _vp]),
     "gp_bucket_sum_apply": (_i, [_vp, _c.POINTER(_vp), _i, _sz, _vp]),
     "gp_add": (_i, [_sz, _vp, _vp, _vp, _vp]),
     "gp_zero": (_i, [_vp, _sz, _vp]),
@@ -94,7 +114,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)  # AttributeError = missing export: loud
             fn.restype = restype
             fn.argtypes = argtypes
-        if handle.gp_abi_version() != 1:
+        if handle.gp_abi_version() != ABI_VERSION:
             raise ImportError("geeps_amd: libgp_reduce.so ABI version mismatch")
         _lib = handle
         return _lib

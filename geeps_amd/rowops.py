@@ -15,6 +15,10 @@ gpu_add                            cpu_add, src/common/gpu-util/math_functions.h
 zerofy_data_gpu                    DataStorage::zerofy_data_gpu, common-util.hpp:445-456
 apply_updates                      TabletStorage::apply_updates x N in arrival order,
                                    src/server/tablet-server.cpp:119-134
+gather_rows_segmented              assign_rows_to_double_index_gpu over a param cache
+                                   split into row-range buffers (libgeeps refresh slots)
+add_rows_segmented                 add_rows_from_double_index_gpu into such a cache
+                                   (read-my-writes, clientlib-data.cpp:387-392)
 =================================  ===============================================
 
 Differences from the reference (deliberate, documented in DESIGN.md): launches
@@ -160,6 +164,86 @@ def assign_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, inde
     """``y[(id1+off1)*W + v] = x[(id0+off0)*W + v]`` where ``(id0+off0)*W+v < limit``."""
     _row_op("assign_from", rows_y, rows_x, index, num_rows, index_offset, row_size,
             num_vals_limit, stream, validate)
+
+
+def _segments(segments, row_size):
+    """[(first_row, tensor), ...] -> (RowSegments, row ranges) with checks."""
+    if not 1 <= len(segments) <= native.GP_MAX_SEGMENTS:
+        raise ValueError(f"1..{native.GP_MAX_SEGMENTS} segments required")
+    t = native.RowSegments()
+    t.count = len(segments)
+    ranges = []
+    for i, (first, buf) in enumerate(segments):
+        _dev_f32(buf, f"segments[{i}]")
+        first = int(first)
+        if i == 0 and first != 0:
+            raise ValueError("segments[0] must start at row 0")
+        if i and first <= ranges[-1][0]:
+            raise ValueError("segment first rows must ascend")
+        t.first_row[i] = first
+        t.base[i] = buf.data_ptr()
+        ranges.append((first, buf.numel() // row_size))
+    return t, ranges
+
+
+def _validate_segment_rows(rows: torch.Tensor, ranges) -> None:
+    """Every cache row maps into its segment's buffer."""
+    if rows.numel() == 0:
+        return
+    firsts = torch.tensor([f for f, _ in ranges], device=rows.device, dtype=torch.int64)
+    sizes = torch.tensor([n for _, n in ranges], device=rows.device, dtype=torch.int64)
+    seg = torch.searchsorted(firsts, rows, right=True) - 1
+    if bool(((rows - firsts[seg]) >= sizes[seg]).any()):
+        raise ValueError("cache row past the end of its segment buffer")
+
+
+def gather_rows_segmented(rows_y, segments, index, num_rows=None, index_offset=None,
+                          row_size=ROW_DATA_SIZE, num_vals_limit=None, stream=None,
+                          validate=True) -> None:
+    """``assign_rows_to_double_index_gpu`` reading a segmented cache:
+    ``segments`` = [(first_row, tensor), ...]; cache row c of the segment
+    starting at f is row c - f of its tensor."""
+    _dev_f32(rows_y, "rows_y")
+    t, ranges = _segments(segments, row_size)
+    n = int(index.shape[0]) if num_rows is None else int(num_rows)
+    if n == 0:
+        return
+    off = _as_offset(index_offset)
+    limit = (1 << 64) - 1 if num_vals_limit is None else int(num_vals_limit)
+    if validate:
+        idx = index[:n]
+        to = idx[:, 0] + off.id0
+        active = to * row_size < limit
+        _validate_segment_rows((idx[:, 1] + off.id1)[active], ranges)
+        if bool(active.any()) and min((int(to[active].max()) + 1) * row_size, limit) > rows_y.numel():
+            raise ValueError("destination row out of range for rows_y")
+    check(native.lib().gp_gather_rows_segmented(rows_y.data_ptr(), ctypes.byref(t), index.data_ptr(),
+                                                n, off, row_size, limit, _stream_ptr(stream)),
+          "gp_gather_rows_segmented")
+
+
+def add_rows_segmented(segments, rows_x, index, num_rows=None, index_offset=None,
+                       row_size=ROW_DATA_SIZE, num_vals_limit=None, stream=None,
+                       validate=True) -> None:
+    """``add_rows_from_double_index_gpu`` into a segmented cache."""
+    _dev_f32(rows_x, "rows_x")
+    t, ranges = _segments(segments, row_size)
+    n = int(index.shape[0]) if num_rows is None else int(num_rows)
+    if n == 0:
+        return
+    off = _as_offset(index_offset)
+    limit = (1 << 64) - 1 if num_vals_limit is None else int(num_vals_limit)
+    if validate:
+        idx = index[:n]
+        frm = idx[:, 0] + off.id0
+        active = frm * row_size < limit
+        _validate_segment_rows((idx[:, 1] + off.id1)[active], ranges)
+        if bool(active.any()) and min((int(frm[active].max()) + 1) * row_size, limit) > rows_x.numel():
+            raise ValueError("source row out of range for rows_x")
+    check(native.lib().gp_scatter_add_rows_segmented(ctypes.byref(t), rows_x.data_ptr(),
+                                                     index.data_ptr(), n, off, row_size, limit,
+                                                     _stream_ptr(stream)),
+          "gp_scatter_add_rows_segmented")
 
 
 def bucket_sum_apply(master: torch.Tensor, buckets: Sequence[torch.Tensor],

@@ -40,7 +40,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 1
+#define GP_ABI_VERSION 2
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -114,6 +114,40 @@ int gp_gather_rows(float *y, const float *x, const gp_double_index *index,
 int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
                     size_t num_rows, gp_double_index offset, size_t row_size,
                     size_t num_vals_limit, gp_stream s);
+
+/* ---------------------------------------------------------------------------
+ * Segmented param cache.  The cache rows of one table are split into up to
+ * GP_MAX_SEGMENTS contiguous row ranges, each living in its own buffer: range
+ * i is rows [first_row[i], first_row[i+1]) (the last one open-ended) and cache
+ * row c of range i is at base[i][(c - first_row[i]) * row_size].  libgeeps
+ * uses it so a same-node server's refresh is read where the server wrote it
+ * (the client's IPC inbox slot) instead of being copied into one contiguous
+ * cache first; the reference has one contiguous cache (ParamCache::data_cache, clientlib.hpp:338-341).
+ * first_row[0] must be 0 and first_row strictly ascending.
+ * ------------------------------------------------------------------------- */
+#define GP_MAX_SEGMENTS 64
+
+typedef struct gp_row_segments {
+  uint32_t count; /* 1 .. GP_MAX_SEGMENTS */
+  uint32_t reserved;
+  uint64_t first_row[GP_MAX_SEGMENTS];
+  float *base[GP_MAX_SEGMENTS];
+} gp_row_segments;
+
+/* gp_gather_rows with x = the segmented cache: `from` (id1 + offset.id1) is a
+ * cache row resolved through `x_segments`. */
+int gp_gather_rows_segmented(float *y, const gp_row_segments *x_segments,
+                             const gp_double_index *index, size_t num_rows,
+                             gp_double_index offset, size_t row_size,
+                             size_t num_vals_limit, gp_stream s);
+
+/* gp_scatter_add_rows with y = the segmented cache: `to` (id1 + offset.id1)
+ * is a cache row resolved through `y_segments` (read-my-writes: the update
+ * also lands in the param cache, clientlib-data.cpp:387-392). */
+int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float *x,
+                                  const gp_double_index *index, size_t num_rows,
+                                  gp_double_index offset, size_t row_size,
+                                  size_t num_vals_limit, gp_stream s);
 
 /* ---------------------------------------------------------------------------
  * Dense reductions (server side).

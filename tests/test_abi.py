@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == 1
+    assert L.gp_abi_version() == native.ABI_VERSION == 2
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -52,6 +52,39 @@ def test_invalid_arguments_rejected_without_device():
     # zero-size calls are no-ops that never touch the device
     assert L.gp_bucket_sum_apply(None, None, 0, 16, None) == 0
     assert L.gp_scatter_add_rows(None, None, None, 0, native.DoubleIndex(0, 0), 128, 0, None) == 0
+
+
+def test_segment_tables_rejected_without_device():
+    L = native.lib()
+    p = ctypes.c_void_p(4096)
+    idx = ctypes.c_void_p(4096)
+    t = native.RowSegments()
+
+    def gather():
+        return L.gp_gather_rows_segmented(p, t, idx, 4, native.DoubleIndex(0, 0), 128, 1 << 40, None)
+
+    def add():
+        return L.gp_scatter_add_rows_segmented(t, p, idx, 4, native.DoubleIndex(0, 0), 128, 1 << 40,
+                                               None)
+
+    t.count = 0
+    assert gather() == native.GP_ERR_INVALID and b"count" in L.gp_last_error()
+    t.count = native.GP_MAX_SEGMENTS + 1
+    assert add() == native.GP_ERR_INVALID and b"count" in L.gp_last_error()
+    t.count = 2
+    t.first_row[0], t.first_row[1] = 1, 5
+    t.base[0] = t.base[1] = 4096
+    assert gather() == native.GP_ERR_INVALID and b"first_row[0]" in L.gp_last_error()
+    t.first_row[0], t.first_row[1] = 0, 0
+    assert add() == native.GP_ERR_INVALID and b"ascending" in L.gp_last_error()
+    t.first_row[1] = 5
+    t.base[1] = None
+    assert gather() == native.GP_ERR_INVALID and b"null" in L.gp_last_error()
+    assert L.gp_gather_rows_segmented(p, None, idx, 4, native.DoubleIndex(0, 0), 128, 1, None) \
+        == native.GP_ERR_INVALID
+    # zero rows: a no-op before any check
+    assert L.gp_gather_rows_segmented(None, None, None, 0, native.DoubleIndex(0, 0), 128, 1,
+                                      None) == native.GP_OK
 
 
 def test_product_does_not_import_oracle():

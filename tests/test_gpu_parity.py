@@ -282,3 +282,83 @@ def test_scatter_init_equals_zero_then_add(dev, W, limit_frac, shift):
                                            n_op, (0, 0), W, limit)
     torch.cuda.synchronize()
     assert np.array_equal(bits(ty.cpu().numpy()), bits(e))
+
+
+# ---- segmented param cache (libgeeps refresh slots) --------------------------------
+
+def _split(rng, n_cache, k):
+    cuts = np.sort(rng.choice(np.arange(1, n_cache), k - 1, replace=False)) if k > 1 else []
+    return [0] + [int(c) for c in cuts] + [n_cache]
+
+
+@pytest.mark.parametrize("W", [1, 3, 4, 64, 128, 1000])
+@pytest.mark.parametrize("nseg", [1, 2, 8, 64])
+def test_segmented_gather_and_add(dev, W, nseg):
+    """Gather from / scatter-add into a cache split over separate buffers equals
+    the flat-cache oracle bit for bit (offsets, num_vals_limit tails included)."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(W * 131 + nseg)
+    n_cache = max(nseg + 1, 200000 // (W * 4))
+    n_op = max(1, n_cache // 2)
+    bounds = _split(rng, n_cache, nseg)
+    cache = rng.standard_normal(n_cache * W).astype(np.float32)
+    # odd starting offsets: the buffers are views one float into a larger one,
+    # so for W % 4 == 0 the scalar (unaligned) path runs for half the cases
+    pad = 1 if (W * nseg) % 2 else 0
+
+    def seg_tensors(c):
+        out = []
+        for i in range(nseg):
+            a, b = bounds[i], bounds[i + 1]
+            big = torch.empty((b - a) * W + pad, dtype=torch.float32, device=dev)
+            t = big[pad:]
+            t.copy_(T(c[a * W:b * W], dev))
+            out.append((a, t))
+        return out
+
+    off1 = 3
+    idx = np.stack([rng.permutation(n_op), rng.choice(n_cache - off1, n_op, replace=False)], 1)
+    idx = idx.astype(np.int64)
+    for limit in (None, int(n_op * W * 0.7) + 1):
+        # gather: y[id0] = cache[id1 + off1]
+        y = rng.standard_normal(n_op * W).astype(np.float32)
+        e = y.copy()
+        oracle.assign_rows_to_double_index(e, cache, idx, (0, off1), W, limit)
+        ty = T(y, dev)
+        rowops.gather_rows_segmented(ty, seg_tensors(cache), T(idx, dev), n_op, (0, off1), W, limit)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("gather", limit)
+        # scatter-add: cache[id1 + off1] += x[id0]
+        x = rng.standard_normal(n_op * W).astype(np.float32)
+        e = cache.copy()
+        oracle.add_rows_from_double_index(e, x, idx, (0, off1), W, limit)
+        segs = seg_tensors(cache)
+        rowops.add_rows_segmented(segs, T(x, dev), T(idx, dev), n_op, (0, off1), W, limit)
+        torch.cuda.synchronize()
+        got = np.concatenate([t.cpu().numpy() for _, t in segs])
+        assert np.array_equal(bits(got), bits(e)), ("add", limit)
+
+
+def test_segmented_rejects_bad_tables(dev):
+    from geeps_amd import native, rowops
+    y = torch.zeros(128 * 4, device=dev)
+    c = torch.zeros(128 * 4, device=dev)
+    idx = torch.tensor([[0, 0]], dtype=torch.int64, device=dev)
+    with pytest.raises(ValueError):
+        rowops.gather_rows_segmented(y, [(1, c)], idx)
+    with pytest.raises(ValueError):
+        rowops.gather_rows_segmented(y, [(0, c), (0, c)], idx)
+    with pytest.raises(ValueError):
+        rowops.gather_rows_segmented(y, [(0, c)] + [(i + 1, c) for i in range(64)], idx)
+    # the C-ABI itself rejects them too (no host validation in between)
+    t = native.RowSegments()
+    t.count = 2
+    t.first_row[0], t.first_row[1] = 0, 0
+    t.base[0] = t.base[1] = c.data_ptr()
+    rc = native.lib().gp_gather_rows_segmented(y.data_ptr(), t, idx.data_ptr(), 1,
+                                               native.DoubleIndex(0, 0), 128, 1 << 40, None)
+    assert rc == native.GP_ERR_INVALID
+    t.count = 0
+    rc = native.lib().gp_scatter_add_rows_segmented(t, y.data_ptr(), idx.data_ptr(), 1,
+                                                    native.DoubleIndex(0, 0), 128, 1 << 40, None)
+    assert rc == native.GP_ERR_INVALID
