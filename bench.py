@@ -63,6 +63,7 @@ def parse(argv=None):
     p.add_argument("--cpu-rows", type=int, default=1 << 17)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-rowops", action="store_true")
+    p.add_argument("--no-hbm-probe", action="store_true")
     p.add_argument("--layout", choices=["arena", "separate"], default="arena",
                    help="HBM layout of buckets + master: one arena (master last) or one "
                         "allocation per buffer")
@@ -152,6 +153,36 @@ def timed_apply(red, steps, warmup, world, dev):
     wall = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     return wall, kernel_ms
+
+
+def hbm_copy_probe(src, dst, reps=5):
+    """Same-box context for roofline.frac: a device-to-device copy of one 4 GiB
+    bucket (gp_memcpy_async = hipMemcpyAsync, 1 read + 1 write stream), timed
+    with HIP events on the launch stream.  HBM boxes differ by several percent
+    (DESIGN.md §5), and a write stream costs more than a read one, so this
+    says how much of the spec peak the same box gives a plain copy."""
+    from geeps_amd import native
+    lib = native.lib()
+    stream = torch.cuda.current_stream()
+    nbytes = src.numel() * src.element_size()
+
+    def one():
+        native.check(lib.gp_memcpy_async(dst.data_ptr(), src.data_ptr(), nbytes,
+                                         stream.cuda_stream), "gp_memcpy_async")
+
+    one()
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        one()
+        b.record(stream)
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    avg = sum(ms) / len(ms)
+    return {"copy_GBps": round(2 * nbytes / (avg / 1e3) / 1e9, 1), "bytes": 2 * nbytes,
+            "avg_ms": round(avg, 4),
+            "note": "same-box D2D copy of one bucket (hipMemcpyAsync: 1 read + 1 write stream)"}
 
 
 def timed_exchange(red, deltas, steps, warmup, world, dev):
@@ -352,7 +383,13 @@ def main(argv=None, backend="nccl", apply_fn=None):
     host_inc = None
     cpu = None
     rowops_res = None
+    probe = None
     if rank == 0 and world == 1 and dev.type == "cuda":
+        if not args.no_hbm_probe:
+            log("[rank 0] HBM copy probe")
+            scratch = torch.empty_like(deltas[0])
+            probe = hbm_copy_probe(deltas[0], scratch)
+            del scratch
         del deltas
         red = None
         torch.cuda.empty_cache()
@@ -402,6 +439,9 @@ def main(argv=None, backend="nccl", apply_fn=None):
         if result_exchange:
             line["exchange_inclusive"] = result_exchange[0]
             line["exchange_inclusive_alt"] = result_exchange[1]
+        if probe:
+            line["roofline"]["same_box_copy_GBps"] = probe["copy_GBps"]
+            line["hbm_probe"] = probe
         if host_inc:
             line["host_inclusive"] = host_inc
         if rowops_res:
