@@ -96,7 +96,7 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->reply_stream = std::make_unique<Stream>();
     ch->sink = std::make_unique<ChannelSink>(this, c);
     ch->server = std::make_unique<TabletServer>(process_id_, c, num_processes_,
-                                                config_.num_tables, ch->sink.get());
+                                                config_.num_tables, ch->sink.get(), device_);
     ch->server_fd.assign(num_processes_, -1);
     for (uint32_t s = 0; s < num_processes_; ++s)
       ch->server_send_mu.push_back(std::make_unique<std::mutex>());

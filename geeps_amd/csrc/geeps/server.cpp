@@ -30,8 +30,12 @@ std::string ServerStats::to_json() const {
 }
 
 TabletServer::TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num_clients,
-                           uint32_t num_tables, ClientSink *sink)
-    : server_id_(server_id), channel_id_(channel_id), num_clients_(num_clients), sink_(sink) {
+                           uint32_t num_tables, ClientSink *sink, int device)
+    : server_id_(server_id),
+      channel_id_(channel_id),
+      num_clients_(num_clients),
+      sink_(sink),
+      device_(device) {
   GP_CHECK(sink_);
   GP_CHECK(num_clients_ > 0);
   tables_.resize(num_tables);
@@ -116,6 +120,7 @@ void TabletServer::stop() {
 }
 
 void TabletServer::run() {
+  GP_CALL(gp_set_device(device_));
   for (;;) {
     Msg m{Msg::kStop, UpdateBatch{}};
     {

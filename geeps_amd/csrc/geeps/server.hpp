@@ -98,8 +98,11 @@ class TabletServer {
  public:
   static constexpr size_t kMaxPendingBuckets = 8;
 
+  // `device`: the HIP device the owning process works on.  The server thread
+  // selects it before its first HIP call, so the master shard, the staging
+  // buffers and every launch land on that GPU (a new thread starts on device 0).
   TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num_clients,
-               uint32_t num_tables, ClientSink *sink);
+               uint32_t num_tables, ClientSink *sink, int device);
   ~TabletServer();
   TabletServer(const TabletServer &) = delete;
   TabletServer &operator=(const TabletServer &) = delete;
@@ -151,6 +154,7 @@ class TabletServer {
 
   const uint32_t server_id_, channel_id_, num_clients_;
   ClientSink *sink_;
+  const int device_;
   std::vector<DataTable> tables_;
   Stream stream_;
   ServerStats stats_;
