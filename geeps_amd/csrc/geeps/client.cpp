@@ -54,8 +54,8 @@ std::string ClientStats::to_json() const {
   return o.str();
 }
 
-void ChannelSink::read_row_batch_reply(uint32_t client_id, const RowBatchReply &r) {
-  lib_->remote_reply(channel_, client_id, r);
+bool ChannelSink::read_row_batch_reply(uint32_t client_id, const RowBatchReply &r) {
+  return lib_->remote_reply(channel_, client_id, r);
 }
 
 void ChannelSink::shutdown_ack(uint32_t client_id) { lib_->remote_shutdown_ack(channel_, client_id); }
@@ -103,7 +103,8 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->server_shut.assign(num_processes_, 0);
     ch->client_fd.assign(num_processes_, -1);
     ch->ipc_oplogs.resize(num_processes_);
-    ch->inbox_of.assign(num_processes_, std::vector<InboxEntry>(config_.num_tables));
+    ch->ipc_client.assign(num_processes_, 0);
+    ch->version_sent.assign(num_processes_, std::vector<std::set<int>>(config_.num_tables));
     ch->client_done.assign(num_processes_, 0);
     channels_[c] = std::move(ch);
   }
@@ -140,7 +141,8 @@ void ClientLib::start_network() {
       std::string err;
       const int fd = connect_tcp(config_.host_list[s], port_of(s, ch.id), kConnectTimeoutS, &err);
       GP_CHECK_MSG(fd >= 0, err);
-      const uint32_t hello[2] = {kHelloCmd, process_id_};
+      // third word: this client takes same-node refreshes in place (IPC)
+      const uint32_t hello[3] = {kHelloCmd, process_id_, ipc_to(s) ? 1u : 0u};
       GP_CHECK(send_frame(fd, {Part{hello, sizeof hello}}));
       ch.server_fd[s] = fd;
       ch.client_readers.emplace_back([this, &ch, s, fd] { client_reader(ch, s, fd); });
@@ -156,13 +158,14 @@ void ClientLib::server_accept_loop(Channel &ch, int expected) {
     std::vector<RecvPart> parts;
     std::vector<std::vector<char>> scratch;
     GP_CHECK(recv_frame(fd, parts, scratch, nullptr, nullptr));
-    GP_CHECK(parts.size() == 1 && parts[0].size == 8);
-    uint32_t hello[2];
-    std::memcpy(hello, parts[0].data, 8);
+    GP_CHECK(parts.size() == 1 && parts[0].size == 12);
+    uint32_t hello[3];
+    std::memcpy(hello, parts[0].data, 12);
     GP_CHECK_EQ(hello[0], kHelloCmd);
     GP_CHECK_LT(hello[1], num_processes_);
     GP_CHECK_MSG(ch.client_fd[hello[1]] < 0, "duplicate client " << hello[1]);
     ch.client_fd[hello[1]] = fd;
+    ch.ipc_client[hello[1]] = hello[2] && ipc_to(hello[1]);
     const uint32_t cid = hello[1];
     ch.server_readers.emplace_back([this, &ch, cid, fd] { server_reader(ch, cid, fd); });
   }
@@ -234,41 +237,25 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       }
       b.num_rows = n;
       ch.server->post_updates(std::move(b));
-    } else if (cmd == kCmdIpcInbox) {
-      GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(IpcInboxMsg));
-      IpcInboxMsg m;
-      std::memcpy(&m, parts[0].data, sizeof m);
-      GP_CHECK_EQ(m.client_id, client_id);
-      GP_CHECK(m.table_id < config_.num_tables && m.num_slots == kInboxSlots);
-      InboxEntry e;
-      for (uint32_t k = 0; k < kInboxSlots; ++k) GP_CALL(gp_ipc_open_handle(&e.slot[k], m.handle[k]));
-      e.bytes = m.bytes;
-      e.registered = true;
-      std::lock_guard<std::mutex> lk(ch.ipc_mu);
-      ch.inbox_of[client_id][m.table_id] = e;
     } else if (cmd == kCmdRefreshAck) {
       GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(RefreshAckMsg));
       RefreshAckMsg a;
       std::memcpy(&a, parts[0].data, sizeof a);
-      GP_CHECK(a.table_id < config_.num_tables && a.slot < kInboxSlots);
-      {
-        std::lock_guard<std::mutex> lk(ch.ipc_mu);
-        ch.inbox_of[client_id][a.table_id].busy[a.slot] = false;
-      }
-      ch.ipc_cv.notify_all();
+      GP_CHECK_EQ(a.client_id, client_id);
+      ch.server->release(client_id, a.table_id, a.version);
     } else if (cmd == CLOCK) {
       GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(cs_clock_msg_t));
       cs_clock_msg_t h;
       std::memcpy(&h, parts[0].data, sizeof h);
       ch.server->post_clock(h.client_id, h.clock, h.table_id);
     } else if (cmd == SHUTDOWN) {
-      // The client sends nothing after this (shutdown handshake): a refresh
-      // waiting for one of its slots to be released would wait forever.
+      // The client sends nothing after this (shutdown handshake) and reads no
+      // more: later refreshes to it are dropped and its holds end here.
       {
         std::lock_guard<std::mutex> lk(ch.ipc_mu);
         ch.client_done[client_id] = 1;
       }
-      ch.ipc_cv.notify_all();
+      ch.server->release_all(client_id);
       ch.server->post_shutdown(client_id);
       break;
     } else {
@@ -303,82 +290,81 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
     GP_CHECK_EQ(h.server_id, server_id);
     GP_CHECK_LT(h.table_id, config_.num_tables);
     if (parts.size() == 4) {
-      // Same-node server wrote the shard into our inbox slot over IPC.
-      GP_CHECK(parts[3].size == sizeof(IpcRefreshSlot));
-      IpcRefreshSlot sl;
-      std::memcpy(&sl, parts[3].data, sizeof sl);
-      GP_CHECK_LT(sl.slot, kInboxSlots);
-      auto &slot = ch.tables[h.table_id].inbox[server_id][sl.slot];
-      GP_CHECK(slot);
-      // The slot becomes the live copy of this shard (read in place by the
-      // segmented gather); the slot it replaces goes back to the server.
-      const int retired = recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age,
-                                         h.self_clock, slot->data(), sl.num_rows, (int)sl.slot);
-      if (retired >= 0) {
+      // Same-node server: the shard is one of its master versions, read in
+      // place through an IPC mapping of that version's buffer.
+      GP_CHECK(parts[3].size == sizeof(IpcRefreshVersion));
+      IpcRefreshVersion rv;
+      std::memcpy(&rv, parts[3].data, sizeof rv);
+      GP_CHECK(rv.version >= 0);
+      void *ptr = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(ch.mu);
+        auto &mapped = ch.tables[h.table_id].server_versions[server_id];
+        if (rv.has_handle) {
+          GP_CHECK_MSG(!mapped.count(rv.version), "version " << rv.version << " mapped twice");
+          GP_CALL(gp_ipc_open_handle(&ptr, rv.handle));
+          mapped[rv.version] = ptr;
+        } else {
+          auto it = mapped.find(rv.version);
+          GP_CHECK_MSG(it != mapped.end(), "unmapped master version " << rv.version);
+          ptr = it->second;
+        }
+      }
+      const std::vector<int> released =
+          recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
+                         static_cast<const float *>(ptr), rv.num_rows, rv.version);
+      for (int v : released) {
         RefreshAckMsg a{};
         a.cmd = kCmdRefreshAck;
         a.client_id = process_id_;
         a.table_id = h.table_id;
-        a.slot = (uint32_t)retired;
+        a.version = v;
         ack_to_server(ch, server_id, a);
       }
       continue;
     }
     const size_t n = parts[1].size / sizeof(RowKey);
     GP_CHECK_EQ(parts[2].size, n * kRowBytes);
-    const int retired = recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
-                                       static_cast<const float *>(parts[2].data), n, -1);
-    GP_CHECK_MSG(retired < 0, "socket refresh replaced an IPC slot of server " << server_id);
+    const std::vector<int> released =
+        recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
+                       static_cast<const float *>(parts[2].data), n, -1);
+    GP_CHECK_MSG(released.empty(), "socket refresh replaced an in-place shard of server " << server_id);
   }
 }
 
-// Refresh to a same-node client: copy the shard device to device into the
-// client's inbox slot (data_age parity), then a 4-part control frame.  A slot is
-// rewritten only after the client ACKed consuming it, so the client's copy into
-// its param cache (under its channel lock) never races this write.
-bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r) {
-  InboxEntry *ib = nullptr;
+// Refresh to a same-node client: no rows move.  The frame names the master
+// version the client reads in place from now on (with the version buffer's IPC
+// handle the first time this client sees it); the client releases the version
+// it read before.  Returns false when the refresh must go as a copied frame;
+// `*held`: the client now holds r.version.
+bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r, bool *held) {
+  *held = false;
+  if (!ch.ipc_client[client_id] || r.version < 0 || r.num_rows == 0) return false;
   {
     std::lock_guard<std::mutex> lk(ch.ipc_mu);
-    InboxEntry &e = ch.inbox_of[client_id][r.table_id];
-    if (e.registered) ib = &e;
-  }
-  if (!ib || r.num_rows == 0) return false;
-  // The client reads its live slot in place until the next refresh replaces
-  // it, so at most one slot is held there: wait for a free one.
-  uint32_t slot = 0;
-  {
-    std::unique_lock<std::mutex> lk(ch.ipc_mu);
-    auto ready = [&] {
-      if (ch.client_done[client_id]) return true;
-      for (uint32_t k = 0; k < kInboxSlots; ++k)
-        if (!ib->busy[k]) return true;
-      return false;
-    };
-    while (!ready()) {
-      if (!ch.ipc_cv.wait_for(lk, std::chrono::milliseconds(kWaitWarnMs), ready))
-        std::cerr << "server " << process_id_ << " waiting for client " << client_id
-                  << " to release a refresh slot" << std::endl;
-    }
-    // A client that has shut down reads nothing more: the refresh is dropped.
+    // A client that has shut down reads nothing more: the refresh is dropped
+    // (and holds nothing: its SHUTDOWN released everything it held).
     if (ch.client_done[client_id]) return true;
-    while (ib->busy[slot]) ++slot;
-    ib->busy[slot] = true;
   }
-  const size_t bytes = r.num_rows * kRowBytes;
-  GP_CHECK_LE(bytes, ib->bytes);
-  GP_CALL(gp_memcpy_async(ib->slot[slot], r.device_rows, bytes, ch.reply_stream->get()));
-  ch.reply_stream->sync();
+  IpcRefreshVersion rv{};
+  rv.version = r.version;
+  rv.num_rows = r.num_rows;
+  auto &sent = ch.version_sent[client_id][r.table_id];
+  if (!sent.count(r.version)) {
+    GP_CALL(gp_ipc_get_handle(rv.handle, const_cast<float *>(r.device_rows)));
+    rv.has_handle = 1;
+    sent.insert(r.version);
+  }
   sc_read_row_batch_msg_t h{};
   h.cmd = READ_ROW_BATCH;
   h.server_id = r.server_id;
   h.data_age = r.data_age;
   h.self_clock = r.self_clock;
   h.table_id = r.table_id;
-  IpcRefreshSlot sl{slot, 0, r.num_rows};
   GP_CHECK_MSG(send_frame(ch.client_fd[client_id], {Part{&h, sizeof h}, Part{nullptr, 0},
-                                                    Part{nullptr, 0}, Part{&sl, sizeof sl}}),
+                                                    Part{nullptr, 0}, Part{&rv, sizeof rv}}),
                "send to client " << client_id << " failed");
+  *held = true;
   return true;
 }
 
@@ -391,40 +377,15 @@ void ClientLib::send_to_server(Channel &ch, uint32_t s, const std::vector<Part> 
     ch.server_shut[s] = 1;
 }
 
-// The reader thread ACKs a consumed inbox slot.  The last refresh can land after
-// the app thread already sent SHUTDOWN (the server then stops reading that
-// socket and sends no more refreshes), so such an ACK is dropped, not sent.
+// The reader thread releases a master version it no longer reads.  The last
+// refresh can land after the app thread already sent SHUTDOWN (the server then
+// stops reading that socket, and its SHUTDOWN handling released every hold),
+// so such a release is dropped, not sent.
 void ClientLib::ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a) {
   std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
   if (ch.server_shut[s]) return;
   GP_CHECK_MSG(send_frame(ch.server_fd[s], {Part{&a, sizeof a}}),
                "refresh ACK to server " << s << " failed");
-}
-
-// Same-node servers get kInboxSlots device buffers per table to write refreshed
-// shards into (FinishVirtualIteration, once the shard sizes are known).
-void ClientLib::register_inboxes() {
-  for (auto &chp : channels_) {
-    Channel &ch = *chp;
-    for (uint32_t t = 0; t < config_.num_tables; ++t) {
-      ParamCache &pc = ch.tables[t];
-      pc.inbox.resize(num_processes_);
-      for (uint32_t s = 0; s < num_processes_; ++s) {
-        if (!ipc_to(s) || pc.server_num_rows[s] == 0) continue;
-        IpcInboxMsg m{};
-        m.cmd = kCmdIpcInbox;
-        m.client_id = process_id_;
-        m.table_id = t;
-        m.num_slots = kInboxSlots;
-        m.bytes = pc.server_num_rows[s] * kRowBytes;
-        for (uint32_t k = 0; k < kInboxSlots; ++k) {
-          pc.inbox[s][k] = std::make_unique<DeviceArray<float>>(pc.server_num_rows[s] * ROW_DATA_SIZE);
-          GP_CALL(gp_ipc_get_handle(m.handle[k], pc.inbox[s][k]->data()));
-        }
-        send_to_server(ch, s, {Part{&m, sizeof m}});
-      }
-    }
-  }
 }
 
 void ClientLib::remote_shutdown_ack(uint32_t channel, uint32_t client_id) {
@@ -438,16 +399,19 @@ void ClientLib::remote_shutdown_ack(uint32_t channel, uint32_t client_id) {
 }
 
 // The tablet server's reply to one client (read_row_batch_reply,
-// server-encoder-decoder.cpp:228-250): in-process -> device copy, remote ->
-// D2H into pinned memory and one frame on the client's socket.
-void ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r) {
+// server-encoder-decoder.cpp:228-250): in-process -> the client takes the
+// master version in place (or copies it), same node -> the version by IPC,
+// remote -> D2H into pinned memory and one frame on the client's socket.
+bool ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r) {
   if (client_id == process_id_) {
-    recv_row_batch(channel, r.server_id, r.table_id, r.data_age, r.self_clock, r.device_rows,
-                   r.num_rows, -1);
-    return;
+    for (int v : recv_row_batch(channel, r.server_id, r.table_id, r.data_age, r.self_clock,
+                                r.device_rows, r.num_rows, r.version))
+      channels_[channel]->server->release(process_id_, r.table_id, v);
+    return r.version >= 0;
   }
   Channel &ch = *channels_[channel];
-  if (ipc_reply(ch, client_id, r)) return;
+  bool held = false;
+  if (ipc_reply(ch, client_id, r, &held)) return held;
   const int fd = ch.client_fd[client_id];
   GP_CHECK_MSG(fd >= 0, "no connection to client " << client_id);
   const size_t floats = r.num_rows * ROW_DATA_SIZE;
@@ -465,6 +429,7 @@ void ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatc
   GP_CHECK_MSG(send_frame(fd, {Part{&h, sizeof h}, Part{r.keys, r.num_rows * sizeof(RowKey)},
                                Part{ch.reply_buf.data(), floats * 4}}),
                "send to client " << client_id << " failed");
+  return false;
 }
 
 // ---------------------------------------------------------------------------
@@ -567,7 +532,9 @@ void ClientLib::finish_virtual_iteration() {
         pc.server_num_rows[i] = div + (i < res ? 1 : 0);
       }
       pc.per_server_data_age.assign(num_processes_, INITIAL_DATA_AGE);
-      pc.live_slot.assign(num_processes_, -1);
+      pc.live_ver.assign(num_processes_, -1);
+      pc.live_ptr.assign(num_processes_, nullptr);
+      pc.server_versions.resize(num_processes_);
       pc.server_clock.assign(num_processes_, INITIAL_DATA_AGE);
     }
     ch.stream->sync();
@@ -597,7 +564,6 @@ void ClientLib::finish_virtual_iteration() {
   }
   GP_CALL(gp_device_synchronize());
   decide_fused_init();
-  register_inboxes();
   if (planned > config_.gpu_memory_capacity) {
     std::ostringstream o;
     o << "planned HBM use " << planned << " B exceeds gpu_memory_capacity "
@@ -996,12 +962,13 @@ void ClientLib::reclaim_oplogs(ParamCache &pc, iter_t upto) {
 
 // recv_row_batch + recv_row_batch_gpu + server_clock_cbk
 // (clientlib-data.cpp:51-151, clientlib-cbk.cpp:81-104).
-int ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id,
-                              iter_t data_age, iter_t self_clock, const float *rows,
-                              size_t num_rows, int slot) {
+std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
+                                           uint32_t table_id, iter_t data_age, iter_t self_clock,
+                                           const float *rows, size_t num_rows, int version) {
   const double t0 = now_s();
   Channel &ch = *channels_[channel];
-  int retired = -1;
+  std::vector<int> released;
+  bool in_place = false;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     GP_CHECK_LT(table_id, ch.tables.size());
@@ -1024,32 +991,42 @@ int ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t tab
       pc.server_clock_min = min_clock;
     }
     if (num_rows) {
-      float *dst;
-      if (slot >= 0) {
-        // Already in our inbox slot: it becomes the live copy of the shard.
-        dst = const_cast<float *>(rows);
-      } else {
-        dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
-        GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.recv_stream->get()));
-      }
-      const size_t floats = num_rows * ROW_DATA_SIZE;
-      if (config_.read_my_writes) {
-        // Re-apply this client's own not-yet-reflected updates
-        // (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
-        for (iter_t c = self_clock + 1, fc = fast_clock_.load(); c <= fc; ++c) {
-          auto it = pc.oplog.find(c);
-          if (it == pc.oplog.end()) continue;
-          const float *op = it->second->data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
-          GP_CALL(gp_add(floats, dst, op, dst, ch.recv_stream->get()));
+      const int prev = pc.live_ver[server_id];
+      if (version >= 0 && !config_.read_my_writes) {
+        // The server's published master version becomes the live copy of
+        // this shard, read in place by the segmented gather: no copy.  It is
+        // never rewritten while we hold it; the one it replaces goes back.
+        in_place = true;
+        if (prev != version) {
+          if (prev >= 0) released.push_back(prev);
+          pc.live_ver[server_id] = version;
+          pc.live_ptr[server_id] = rows;
+          rebuild_segments(pc);
         }
-      }
-      ch.recv_stream->sync();
-      const int prev = pc.live_slot[server_id];
-      GP_CHECK_MSG(slot < 0 || prev != slot, "server " << server_id << " rewrote live slot " << slot);
-      if (prev != slot) {
-        pc.live_slot[server_id] = slot;
-        retired = prev;
-        rebuild_segments(pc);
+      } else {
+        // Copy into the cache (recv_row_batch_gpu, clientlib-data.cpp:110-151):
+        // rows from a socket, or read-my-writes, which re-applies this
+        // client's own not-yet-reflected updates on top of the shard and so
+        // needs a private copy (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
+        float *dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
+        const size_t floats = num_rows * ROW_DATA_SIZE;
+        GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.recv_stream->get()));
+        if (config_.read_my_writes) {
+          for (iter_t c = self_clock + 1, fc = fast_clock_.load(); c <= fc; ++c) {
+            auto it = pc.oplog.find(c);
+            if (it == pc.oplog.end()) continue;
+            const float *op = it->second->data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
+            GP_CALL(gp_add(floats, dst, op, dst, ch.recv_stream->get()));
+          }
+        }
+        ch.recv_stream->sync();
+        if (version >= 0) released.push_back(version);  // copied: give it back now
+        if (prev >= 0) {
+          released.push_back(prev);
+          pc.live_ver[server_id] = -1;
+          pc.live_ptr[server_id] = nullptr;
+          rebuild_segments(pc);
+        }
       }
     }
     pc.data_age = *std::min_element(pc.per_server_data_age.begin(), pc.per_server_data_age.end());
@@ -1057,41 +1034,38 @@ int ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t tab
   ch.cv.notify_all();
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_refresh++;
-  if (slot >= 0) stats_.nr_refresh_in_place++;
+  if (in_place) stats_.nr_refresh_in_place++;
   stats_.refresh_time += now_s() - t0;
-  return retired;
+  return released;
 }
 
 // The cache as row ranges: each server's shard is read from the cache's own
-// `data` or from its live inbox slot; neighbouring ranges of `data` merge.
+// `data` or in place from the server's live master version; neighbouring
+// ranges of `data` merge.
 void ClientLib::rebuild_segments(ParamCache &pc) {
   gp_row_segments t{};
-  bool any_slot = false;
+  bool any_in_place = false;
   const float *next_flat = nullptr;  // where a merged `data` range would continue
   for (uint32_t s = 0; s < num_processes_; ++s) {
     const size_t n = pc.server_num_rows[s];
     if (n == 0) continue;
     const size_t first = pc.server_row_start[s];
-    float *base;
-    if (pc.live_slot[s] >= 0) {
-      base = pc.inbox[s][pc.live_slot[s]]->data();
-      any_slot = true;
-    } else {
-      base = pc.data.data() + first * ROW_DATA_SIZE;
-    }
-    if (t.count && base == next_flat && pc.live_slot[s] < 0) {
+    const bool in_place = pc.live_ver[s] >= 0;
+    const float *base = in_place ? pc.live_ptr[s] : pc.data.data() + first * ROW_DATA_SIZE;
+    any_in_place = any_in_place || in_place;
+    if (t.count && base == next_flat && !in_place) {
       next_flat = base + n * ROW_DATA_SIZE;
       continue;
     }
     GP_CHECK_MSG(t.count < GP_MAX_SEGMENTS, "param cache split into more than "
                                                 << GP_MAX_SEGMENTS << " segments");
     t.first_row[t.count] = t.count ? first : 0;
-    t.base[t.count] = base;
+    t.base[t.count] = const_cast<float *>(base);
     ++t.count;
-    next_flat = pc.live_slot[s] < 0 ? base + n * ROW_DATA_SIZE : nullptr;
+    next_flat = in_place ? nullptr : base + n * ROW_DATA_SIZE;
   }
   pc.segs = t;
-  pc.segmented = any_slot;
+  pc.segmented = any_in_place;
 }
 
 // ---------------------------------------------------------------------------
@@ -1143,10 +1117,9 @@ void ClientLib::shutdown() {
     chp->server->stop();
     for (auto &m : chp->ipc_oplogs)
       for (auto &kv : m) gp_ipc_close_handle(kv.second);
-    for (auto &row : chp->inbox_of)
-      for (auto &e : row)
-        if (e.registered)
-          for (void *p : e.slot) gp_ipc_close_handle(p);
+    for (auto &pc : chp->tables)
+      for (auto &per_server : pc.server_versions)
+        for (auto &kv : per_server) gp_ipc_close_handle(kv.second);
     for (int fd : chp->server_fd) close_fd(fd);
     for (int fd : chp->client_fd) close_fd(fd);
     close_fd(chp->listen_fd);

@@ -29,6 +29,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -78,32 +79,26 @@ struct ParamCache {
   iter_t data_age = INITIAL_DATA_AGE;
   std::vector<iter_t> server_clock;
   iter_t server_clock_min = INITIAL_DATA_AGE;
-  // same-node peers: refresh inbox per server (kInboxSlots device buffers the
-  // server writes over IPC), and which oplog buffers each server has mapped
-  std::vector<std::array<std::unique_ptr<DeviceArray<float>>, kInboxSlots>> inbox;
+  // which oplog buffers each same-node server has mapped, and whether it has
+  // the shard's keys
   std::vector<std::vector<uint8_t>> exported;  // [oplog pool index][server]
   std::vector<uint8_t> ipc_keys_sent;           // [server]: shard keys already sent
-  // Where each server's shard rows are read from: -1 = this cache's own range
-  // of `data`; k = inbox slot k, which the same-node server's last refresh
-  // wrote over IPC and which stays live (un-ACKed) until the next refresh
-  // replaces it.  `segs` describes the resulting split cache for the
-  // segmented gather / scatter-add; `segmented` = some shard lives in a slot.
-  std::vector<int> live_slot;
+  // Where each server's shard rows are read from: live_ver[s] = -1: this
+  // cache's own range of `data` (a copied refresh); v >= 0: server s's master
+  // version v, read in place at live_ptr[s] (same process: its buffer; same
+  // node: its IPC mapping, kept in server_versions[s]) until the next refresh
+  // replaces it.  `segs` describes the resulting split cache for the segmented
+  // gather; `segmented` = some shard is read in place.
+  std::vector<int> live_ver;
+  std::vector<const float *> live_ptr;
+  std::vector<std::map<int, void *>> server_versions;  // [server]: IPC-mapped versions
   gp_row_segments segs{};
   bool segmented = false;
 };
 
-// Server-side view of a same-node client's IPC exports.
-struct InboxEntry {
-  void *slot[kInboxSlots] = {};
-  size_t bytes = 0;
-  bool busy[kInboxSlots] = {};
-  bool registered = false;
-};
-
 struct ClientStats {
   uint64_t nr_read = 0, nr_update = 0, nr_clock = 0, nr_push = 0, nr_refresh = 0;
-  uint64_t nr_refresh_in_place = 0;  // same-node refreshes read from the inbox slot
+  uint64_t nr_refresh_in_place = 0;  // refreshes read in place from the server's master version
   uint64_t rows_updated = 0, rows_read = 0, bytes_pushed_remote = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
@@ -115,7 +110,7 @@ class ClientLib;
 class ChannelSink : public ClientSink {
  public:
   ChannelSink(ClientLib *lib, uint32_t channel) : lib_(lib), channel_(channel) {}
-  void read_row_batch_reply(uint32_t client_id, const RowBatchReply &reply) override;
+  bool read_row_batch_reply(uint32_t client_id, const RowBatchReply &reply) override;
   void shutdown_ack(uint32_t client_id) override;
 
  private:
@@ -148,13 +143,15 @@ struct Channel {
   std::vector<int> client_fd;
   std::vector<std::thread> server_readers;
   PinnedArray<float> reply_buf;
-  // server side, same-node clients: mapped oplog buffers and refresh inboxes
+  // server side, same-node clients: mapped oplog buffers, whether the client
+  // takes refreshes in place (its hello said so), and which master versions'
+  // IPC handles it already has
   std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
-  std::vector<std::vector<InboxEntry>> inbox_of;         // [client][table]
+  std::vector<uint8_t> ipc_client;                       // [client]
+  std::vector<std::vector<std::set<int>>> version_sent;  // [client][table]
   // [client]: its SHUTDOWN arrived (it reads no more, and its ACKs stop)
   std::vector<uint8_t> client_done;
   std::mutex ipc_mu;
-  std::condition_variable ipc_cv;
 };
 
 class ClientLib {
@@ -177,13 +174,16 @@ class ClientLib {
   std::string json_stats();
   void shutdown();
 
-  // server -> client refresh (recv_row_batch, clientlib-data.cpp:51-108)
-  // `slot` >= 0: the rows are already in our inbox slot `slot` (same-node
-  // server); returns the slot the refresh retired (to ACK), or -1.
-  int recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id, iter_t data_age,
-                     iter_t self_clock, const float *rows, size_t num_rows, int slot);
+  // server -> client refresh (recv_row_batch, clientlib-data.cpp:51-108).
+  // `version` >= 0: `rows` is that master version of the server's shard, which
+  // this client may read in place; -1: `rows` is only valid during the call.
+  // Returns the master versions this client gives back to the server.
+  std::vector<int> recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id,
+                                  iter_t data_age, iter_t self_clock, const float *rows,
+                                  size_t num_rows, int version);
   void rebuild_segments(ParamCache &pc);
-  void remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r);
+  // Returns true if the client holds reply.version after the call.
+  bool remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r);
   void remote_shutdown_ack(uint32_t channel, uint32_t client_id);
   // Let in-flight device work finish (process exit without Shutdown()).
   void quiesce();
@@ -205,8 +205,7 @@ class ClientLib {
   void client_reader(Channel &ch, uint32_t server_id, int fd);
   uint16_t port_of(uint32_t process, uint32_t channel) const;
   bool ipc_to(uint32_t s) const { return s != process_id_ && same_node_[s]; }
-  void register_inboxes();
-  bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r);
+  bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r, bool *held);
   void send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts);
   void ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a);
 

@@ -23,7 +23,9 @@ std::string ServerStats::to_json() const {
   o << "{\"nr_update\": " << nr_update << ", \"nr_local_update\": " << nr_local_update
     << ", \"nr_clock\": " << nr_clock << ", \"nr_refresh\": " << nr_refresh
     << ", \"nr_apply_launches\": " << nr_apply_launches
+    << ", \"nr_apply_out_of_place\": " << nr_apply_out_of_place
     << ", \"nr_buckets_applied\": " << nr_buckets_applied
+    << ", \"nr_versions\": " << nr_versions
     << ", \"apply_time\": " << apply_time << ", \"stage_time\": " << stage_time
     << ", \"refresh_time\": " << refresh_time << "}";
   return o.str();
@@ -74,6 +76,24 @@ void TabletServer::post_shutdown(uint32_t client_id) {
     queue_.push_back(std::move(m));
   }
   cv_.notify_one();
+}
+
+void TabletServer::release(uint32_t client_id, uint32_t table_id, int version) {
+  std::lock_guard<std::mutex> lk(hold_mu_);
+  GP_CHECK_LT(table_id, tables_.size());
+  GP_CHECK_LT(client_id, num_clients_);
+  DataTable &t = tables_[table_id];
+  GP_CHECK_MSG(version >= 0 && (size_t)version < t.holders.size() && t.holders[version][client_id],
+               "client " << client_id << " releases master version " << version << " of table "
+                         << table_id << " it does not hold");
+  t.holders[version][client_id] = 0;
+}
+
+void TabletServer::release_all(uint32_t client_id) {
+  std::lock_guard<std::mutex> lk(hold_mu_);
+  GP_CHECK_LT(client_id, num_clients_);
+  for (auto &t : tables_)
+    for (auto &h : t.holders) h[client_id] = 0;
 }
 
 void TabletServer::wait_shutdown() {
@@ -188,8 +208,9 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
     GP_CHECK_MSG(b.keys, "first update batch of table " << b.table_id << " from client "
                                                           << b.client_id << " carries no row keys");
     t.row_count = batch_size;
-    t.master.resize(batch_size * ROW_DATA_SIZE);
-    GP_CALL(gp_zero(t.master.data(), t.master.size(), stream_.get()));
+    t.cur = free_version(t);
+    t.cur_published = false;
+    GP_CALL(gp_zero(t.versions[t.cur]->data(), batch_size * ROW_DATA_SIZE, stream_.get()));
     t.row_keys.assign(b.keys, b.keys + batch_size);
   }
   GP_CHECK_EQ(t.row_count, batch_size);
@@ -218,15 +239,48 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
   if (t.pending.size() >= kMaxPendingBuckets) apply_pending(t);
 }
 
+// A version no client holds, other than the current one; a new one when
+// every version is held.
+int TabletServer::free_version(DataTable &t) {
+  std::lock_guard<std::mutex> lk(hold_mu_);
+  for (size_t v = 0; v < t.versions.size(); ++v) {
+    if ((int)v == t.cur) continue;
+    bool held = false;
+    for (uint8_t h : t.holders[v]) held = held || h;
+    if (!held) return (int)v;
+  }
+  GP_CHECK_MSG(t.versions.size() < (size_t)num_clients_ + 2,
+               "every master version is held: clients hold more than one version each");
+  t.versions.push_back(std::make_unique<DeviceArray<float>>(t.row_count * ROW_DATA_SIZE));
+  t.holders.emplace_back(num_clients_, 0);
+  stats_.nr_versions++;
+  return (int)t.versions.size() - 1;
+}
+
 // All queued buckets in arrival order, one launch: master = ((m + b0) + b1) ...
+// in place, or into a fresh version when clients may be reading the current
+// one (same bits: gp_bucket_sum_into).
 void TabletServer::apply_pending(DataTable &t) {
   if (t.pending.empty()) return;
   const double t0 = now_s();
   std::vector<const float *> ptrs;
   ptrs.reserve(t.pending.size());
   for (auto &p : t.pending) ptrs.push_back(p.rows);
-  GP_CALL(gp_bucket_sum_apply(t.master.data(), ptrs.data(), (int)ptrs.size(),
-                              t.row_count * ROW_DATA_SIZE, stream_.get()));
+  const float *in = t.versions[t.cur]->data();
+  if (t.cur_published) {
+    bool held = false;
+    {
+      std::lock_guard<std::mutex> lk(hold_mu_);
+      for (uint8_t h : t.holders[t.cur]) held = held || h;
+    }
+    if (held) {  // some client reads it in place: build the next version beside it
+      t.cur = free_version(t);
+      stats_.nr_apply_out_of_place++;
+    }
+    t.cur_published = false;
+  }
+  GP_CALL(gp_bucket_sum_into(t.versions[t.cur]->data(), in, ptrs.data(), (int)ptrs.size(),
+                             t.row_count * ROW_DATA_SIZE, stream_.get()));
   stream_.sync();
   stats_.nr_apply_launches++;
   stats_.nr_buckets_applied += ptrs.size();
@@ -258,11 +312,23 @@ void TabletServer::send_refresh(uint32_t table_id) {
   const double t0 = now_s();
   const iter_t n = (iter_t)num_clients_;
   const uint32_t start = (uint32_t)(((t.global_clock % n) + n) % n);
+  const int ver = t.row_count ? t.cur : -1;
+  const float *rows = ver >= 0 ? t.versions[ver]->data() : nullptr;
+  if (ver >= 0) t.cur_published = true;
   for (uint32_t i = 0; i < num_clients_; ++i) {
     const uint32_t c = (start + i) % num_clients_;
     RowBatchReply r{server_id_, t.global_clock, t.vec_clock[c], table_id,
-                    t.row_keys.data(), t.master.data(), t.row_count};
-    sink_->read_row_batch_reply(c, r);
+                    t.row_keys.data(), rows, t.row_count, ver};
+    // Record the hold before the client can release it (a same-node client's
+    // release arrives on another thread as soon as the frame is out).
+    if (ver >= 0) {
+      std::lock_guard<std::mutex> lk(hold_mu_);
+      t.holders[ver][c] = 1;
+    }
+    if (!sink_->read_row_batch_reply(c, r) && ver >= 0) {
+      std::lock_guard<std::mutex> lk(hold_mu_);
+      t.holders[ver][c] = 0;
+    }
   }
   stats_.nr_refresh++;
   stats_.refresh_time += now_s() - t0;

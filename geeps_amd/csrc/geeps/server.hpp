@@ -16,12 +16,23 @@
 // The reference adds every arriving update into the CPU master immediately
 // (TabletStorage::apply_updates -> cpu_add, src/server/tablet-server.cpp:119-134).
 // Here arriving update batches queue as device buckets in arrival order and
-// are summed into the master by ONE gp_bucket_sum_apply launch right before the
-// master is observed (the refresh sent when the global clock advances), or
-// when the queue reaches kMaxPendingBuckets.  The per-element order of fp32
-// adds is the arrival order in both cases, so the master is bit-identical to
-// the reference's; the device reads each bucket once and the master once per
+// are summed into the master by ONE bucket-sum launch right before the master
+// is observed (the refresh sent when the global clock advances), or when the
+// queue reaches kMaxPendingBuckets.  The per-element order of fp32 adds is the
+// arrival order in both cases, so the master is bit-identical to the
+// reference's; the device reads each bucket once and the master once per
 // refresh instead of once per client.
+//
+// Versions.  The reference replies a COPY of the shard to every client
+// (server-encoder-decoder.cpp:228-250).  Here a refresh publishes the current
+// master version, and same-process / same-node clients read it in place (over
+// IPC-mapped HBM) until a later refresh replaces it; they release it then.  A
+// published version is never written again while any client holds it: the
+// next apply writes a new version out of place (gp_bucket_sum_into: same
+// bytes as the in-place sum), into a version no client holds, allocating one
+// when none is free.  Each client holds at most one version per table at a
+// time (two during a switch), so at most clients + 2 versions ever exist and
+// the server never waits for a release.
 
 #include <condition_variable>
 #include <deque>
@@ -60,7 +71,9 @@ struct UpdateBatch {
 };
 
 // The refreshed shard, as the server hands it to a client sink.  `device_rows`
-// stays valid only for the duration of the sink call.
+// is master version `version` (-1: no rows yet).  It stays valid after the
+// sink call only if the sink reports that the client holds it; the client
+// then gives it back through TabletServer::release().
 struct RowBatchReply {
   uint32_t server_id;
   iter_t data_age;
@@ -69,6 +82,7 @@ struct RowBatchReply {
   const RowKey *keys;
   const float *device_rows;
   size_t num_rows;
+  int version;
 };
 
 // Where the server sends refreshed shards (ServerClientEncode::read_row_batch_reply,
@@ -76,7 +90,9 @@ struct RowBatchReply {
 class ClientSink {
  public:
   virtual ~ClientSink() = default;
-  virtual void read_row_batch_reply(uint32_t client_id, const RowBatchReply &reply) = 0;
+  // Returns true if the client keeps reading reply.device_rows after the call
+  // (it will release reply.version).
+  virtual bool read_row_batch_reply(uint32_t client_id, const RowBatchReply &reply) = 0;
   // Every client has said SHUTDOWN: nothing more will be sent to `client_id`.
   virtual void shutdown_ack(uint32_t client_id) = 0;
 };
@@ -87,7 +103,9 @@ struct ServerStats {
   uint64_t nr_clock = 0;
   uint64_t nr_refresh = 0;
   uint64_t nr_apply_launches = 0;
+  uint64_t nr_apply_out_of_place = 0;  // applies that built a new master version
   uint64_t nr_buckets_applied = 0;
+  uint64_t nr_versions = 0;            // master versions allocated (all tables)
   double apply_time = 0;         // s, including the launch sync
   double stage_time = 0;         // s, H2D of socket-delivered buckets
   double refresh_time = 0;       // s, sending refreshed shards
@@ -113,6 +131,11 @@ class TabletServer {
   // Client `client_id` will send nothing more.  Once every client has said so,
   // each is acknowledged through ClientSink::shutdown_ack.
   void post_shutdown(uint32_t client_id);
+  // Client `client_id` no longer reads master version `version` of table
+  // `table_id` in place.  Thread-safe; any thread.
+  void release(uint32_t client_id, uint32_t table_id, int version);
+  // ... nor any version of any table (its SHUTDOWN arrived).
+  void release_all(uint32_t client_id);
   // Blocks until every client has sent SHUTDOWN and all were acknowledged.
   void wait_shutdown();
   // Blocks until every message posted before it has been processed.
@@ -132,7 +155,13 @@ class TabletServer {
     iter_t global_clock = INITIAL_DATA_AGE;
     size_t row_count = 0;
     std::vector<RowKey> row_keys;
-    DeviceArray<float> master;
+    // master versions; `cur` is the latest, `cur_published` once a refresh
+    // has handed it out (from then on it is only read)
+    std::vector<std::unique_ptr<DeviceArray<float>>> versions;
+    int cur = -1;
+    bool cur_published = false;
+    // [version][client]: the client reads that version in place (hold_mu_)
+    std::vector<std::vector<uint8_t>> holders;
     std::vector<Pending> pending;
     std::vector<std::shared_ptr<DeviceArray<float>>> stage_pool;
   };
@@ -151,6 +180,7 @@ class TabletServer {
   void apply_pending(DataTable &t);
   void send_refresh(uint32_t table_id);
   std::shared_ptr<DeviceArray<float>> stage_buffer(DataTable &t);
+  int free_version(DataTable &t);
 
   const uint32_t server_id_, channel_id_, num_clients_;
   ClientSink *sink_;
@@ -162,6 +192,7 @@ class TabletServer {
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Msg> queue_;
+  std::mutex hold_mu_;  // DataTable::holders (and the versions vector's size)
   uint32_t shutdown_count_ = 0;  // server thread only
   bool shutdown_done_ = false;    // guarded by mu_
   std::condition_variable shutdown_cv_;

@@ -76,10 +76,8 @@ struct sc_read_row_batch_msg_t {
 // device (xGMI between MI355X GPUs, or within one GPU) through IPC-mapped
 // HBM; TCP carries only these small control frames.
 // ---------------------------------------------------------------------------
-constexpr command_t kCmdIpcInbox = 100;    // client -> server: refresh inbox handles
-constexpr command_t kCmdRefreshAck = 101;  // client -> server: inbox slot consumed
+constexpr command_t kCmdRefreshAck = 101;  // client -> server: master version released
 constexpr uint32_t kIpcHandleBytes = 64;
-constexpr uint32_t kInboxSlots = 2;
 
 // 4th part of a CLOCK_WITH_UPDATES_BATCH whose rows stay in the client's oplog.
 // The RowKey part is sent on the first such message per (server, table) only:
@@ -95,28 +93,23 @@ struct IpcRowsRef {
   uint8_t handle[kIpcHandleBytes];
 };
 
-// Registers the client's refresh inbox (kInboxSlots device buffers) for a table.
-struct IpcInboxMsg {
-  command_t cmd;
-  uint32_t client_id;
-  uint32_t table_id;
-  uint32_t num_slots;
-  uint64_t bytes;  // per slot
-  uint8_t handle[kInboxSlots][kIpcHandleBytes];
-};
-
-// 4th part of a READ_ROW_BATCH whose rows were written into the inbox slot.
-struct IpcRefreshSlot {
-  uint32_t slot;
-  uint32_t pad;
+// 4th part of a READ_ROW_BATCH from a same-node server: the shard is the
+// server's master version `version`, which the client reads in place through
+// the IPC mapping of that version's buffer (the handle rides along the first
+// time a version is named to this client) until a later refresh replaces it.
+struct IpcRefreshVersion {
+  int32_t version;
+  uint32_t has_handle;
   uint64_t num_rows;
+  uint8_t handle[kIpcHandleBytes];
 };
 
+// The client no longer reads master version `version` of `table_id` in place.
 struct RefreshAckMsg {
   command_t cmd;
   uint32_t client_id;
   uint32_t table_id;
-  uint32_t slot;
+  int32_t version;
 };
 
 #endif  // GEEPS_AMD_WIRE_HPP_

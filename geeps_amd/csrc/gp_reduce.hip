@@ -581,6 +581,34 @@ int gp_bucket_sum_apply(float *master, const float *const *buckets,
   return GP_OK;
 }
 
+int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
+                       int num_buckets, size_t num_vals, gp_stream s) {
+  if (num_vals == 0) return GP_OK;
+  if (num_buckets < 0) return set_error(GP_ERR_INVALID, "num_buckets < 0");
+  if (!out || !in || (num_buckets && !buckets)) return set_error(GP_ERR_INVALID, "null pointer");
+  if (out != in && out < in + num_vals && in < out + num_vals)
+    return set_error(GP_ERR_INVALID, "out and in overlap");
+  for (int k = 0; k < num_buckets; ++k)
+    if (!buckets[k]) return set_error(GP_ERR_INVALID, "null bucket pointer");
+  if (num_buckets == 0) {
+    if (out != in)
+      GP_HIP_TRY(hipMemcpyAsync(out, in, num_vals * sizeof(float), hipMemcpyDeviceToDevice,
+                                (hipStream_t)s));
+    return GP_OK;
+  }
+  // The first launch reads `in` and writes `out`; any further launches (more
+  // than kMaxBucketsPerLaunch buckets) continue in place on `out`.
+  const float *src = in;
+  for (int k0 = 0; k0 < num_buckets; k0 += kMaxBucketsPerLaunch) {
+    const int nb = num_buckets - k0 < kMaxBucketsPerLaunch ? num_buckets - k0
+                                                           : kMaxBucketsPerLaunch;
+    const int rc = launch_bucket_sum(out, src, buckets + k0, nb, num_vals, (hipStream_t)s);
+    if (rc != GP_OK) return rc;
+    src = out;
+  }
+  return GP_OK;
+}
+
 int gp_add(size_t n, const float *a, const float *b, float *y, gp_stream s) {
   if (n == 0) return GP_OK;
   if (!a || !b || !y) return set_error(GP_ERR_INVALID, "null pointer");

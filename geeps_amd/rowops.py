@@ -266,6 +266,27 @@ def bucket_sum_apply(master: torch.Tensor, buckets: Sequence[torch.Tensor],
                                            _stream_ptr(stream)), "gp_bucket_sum_apply")
 
 
+def bucket_sum_into(out: torch.Tensor, master: torch.Tensor, buckets: Sequence[torch.Tensor],
+                    num_vals: int | None = None, stream=None) -> None:
+    """``out = ((master + b[0]) + b[1]) + ...`` with ``master`` left unchanged:
+    the next version of a shard built beside the published one (gp_bucket_sum_into)."""
+    _dev_f32(master, "master")
+    _dev_f32(out, "out")
+    n = master.numel() if num_vals is None else int(num_vals)
+    if n > master.numel() or n > out.numel():
+        raise ValueError("num_vals exceeds master / out size")
+    ptrs = (ctypes.c_void_p * max(1, len(buckets)))()
+    for k, b in enumerate(buckets):
+        _dev_f32(b, f"buckets[{k}]")
+        if b.numel() < n:
+            raise ValueError(f"buckets[{k}] smaller than num_vals")
+        if b.device != master.device or out.device != master.device:
+            raise ValueError("buffers on different devices")
+        ptrs[k] = b.data_ptr()
+    check(native.lib().gp_bucket_sum_into(out.data_ptr(), master.data_ptr(), ptrs, len(buckets), n,
+                                          _stream_ptr(stream)), "gp_bucket_sum_into")
+
+
 def apply_updates(master: torch.Tensor, updates: Sequence[torch.Tensor], stream=None) -> None:
     """The server's N-way sum: the reference's per-message ``apply_updates`` for
     each update in arrival order, as one device pass."""

@@ -40,7 +40,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 2
+#define GP_ABI_VERSION 3
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -166,6 +166,18 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
  * byte once: (N + 1) * num_vals * 4 B read, num_vals * 4 B written. */
 int gp_bucket_sum_apply(float *master, const float *const *buckets,
                         int num_buckets, size_t num_vals, gp_stream s);
+
+/* Out-of-place form of gp_bucket_sum_apply:
+ *     out[i] = (((in[i] + b[0][i]) + b[1][i]) + ...) + b[N-1][i]
+ * with `in` left unchanged (same bits as applying the N buckets to a copy of
+ * `in`).  libgeeps' tablet server uses it to build the next version of a
+ * shard while clients still read the last published one in place (the
+ * refresh the reference sends as a copy, server-encoder-decoder.cpp:228-250).
+ * `out` and `in` must not overlap unless equal (then it is
+ * gp_bucket_sum_apply).  Same traffic as the in-place form.
+ * num_buckets == 0 copies `in` to `out`. */
+int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
+                       int num_buckets, size_t num_vals, gp_stream s);
 
 /* y[i] = a[i] + b[i] — device form of cpu_add / vsAdd
  * (src/common/gpu-util/math_functions.hpp:60-61, mkl_alternate.hpp:59-74).

@@ -12,7 +12,8 @@ from geeps_amd import native
 def test_header_declares_expected_entry_points():
     syms = native.declared_symbols()
     for s in ("gp_scatter_add_rows", "gp_gather_rows", "gp_scatter_rows",
-              "gp_bucket_sum_apply", "gp_add", "gp_zero", "gp_last_error"):
+              "gp_bucket_sum_apply", "gp_bucket_sum_into", "gp_add", "gp_zero",
+              "gp_last_error"):
         assert s in syms
     # every declared symbol has a ctypes signature and vice versa
     assert set(syms) == set(native._SIGNATURES)
@@ -29,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 2
+    assert L.gp_abi_version() == native.ABI_VERSION == 3
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -51,6 +52,12 @@ def test_invalid_arguments_rejected_without_device():
     assert rc == 1 and b"row_size" in L.gp_last_error()
     # zero-size calls are no-ops that never touch the device
     assert L.gp_bucket_sum_apply(None, None, 0, 16, None) == 0
+    # out-of-place form: nulls and overlapping out / in are rejected before any launch
+    assert L.gp_bucket_sum_into(None, ctypes.c_void_p(4096), None, 1, 16, None) == 1
+    assert L.gp_bucket_sum_into(ctypes.c_void_p(4096 + 16), ctypes.c_void_p(4096), None, 0, 16,
+                                None) == 1
+    assert b"overlap" in L.gp_last_error()
+    assert L.gp_bucket_sum_into(None, None, None, 1, 0, None) == 0
     assert L.gp_scatter_add_rows(None, None, None, 0, native.DoubleIndex(0, 0), 128, 0, None) == 0
 
 

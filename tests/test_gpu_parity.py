@@ -124,6 +124,24 @@ def test_bucket_sum_n_way(dev, N):
     assert np.array_equal(bits(m.cpu().numpy()), bits(e))
 
 
+@pytest.mark.parametrize("N", [0, 1, 3, 8, 9, 17])
+def test_bucket_sum_into_leaves_master(dev, N):
+    """Out-of-place sum (the tablet server's next shard version): `out` equals the
+    in-place result bit for bit, `master` is untouched, chained launches past 8."""
+    from geeps_amd import rowops
+    n = 40961 + N
+    ups = [oracle.synthetic_delta(100 + c, n) for c in range(N)]
+    m0 = np.random.default_rng(7 + N).standard_normal(n).astype(np.float32)
+    e = m0.copy()
+    oracle.apply_updates(e, ups)
+    m = T(m0, dev)
+    out = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+    rowops.bucket_sum_into(out, m, [T(u, dev) for u in ups])
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()), bits(e))
+    assert np.array_equal(bits(m.cpu().numpy()), bits(m0))
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 255, 256, 257, 1023, 1024 * 256 + 3])
 def test_bucket_sum_sizes_and_alignment(dev, n):
     from geeps_amd import rowops
