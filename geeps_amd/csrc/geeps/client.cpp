@@ -91,12 +91,11 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->id = c;
     ch->tables.resize(config_.num_tables);
     ch->stream = std::make_unique<Stream>();
-    ch->recv_stream = std::make_unique<Stream>();
-    ch->send_stream = std::make_unique<Stream>();
-    ch->reply_stream = std::make_unique<Stream>();
+    ch->svc_stream = std::make_unique<Stream>();
     ch->sink = std::make_unique<ChannelSink>(this, c);
     ch->server = std::make_unique<TabletServer>(process_id_, c, num_processes_,
-                                                config_.num_tables, ch->sink.get(), device_);
+                                                config_.num_tables, ch->sink.get(), device_,
+                                                ch->svc_stream->get());
     ch->server_fd.assign(num_processes_, -1);
     for (uint32_t s = 0; s < num_processes_; ++s)
       ch->server_send_mu.push_back(std::make_unique<std::mutex>());
@@ -417,8 +416,8 @@ bool ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatc
   const size_t floats = r.num_rows * ROW_DATA_SIZE;
   if (ch.reply_buf.size() < floats) ch.reply_buf.resize(floats);
   if (floats) {
-    GP_CALL(gp_memcpy_async(ch.reply_buf.data(), r.device_rows, floats * 4, ch.reply_stream->get()));
-    ch.reply_stream->sync();
+    GP_CALL(gp_memcpy_async(ch.reply_buf.data(), r.device_rows, floats * 4, ch.svc_stream->get()));
+    ch.svc_stream->sync();
   }
   sc_read_row_batch_msg_t h{};
   h.cmd = READ_ROW_BATCH;
@@ -551,14 +550,14 @@ void ClientLib::finish_virtual_iteration() {
       auto &slot = local_storage_[op.rows];
       if (!slot) {
         slot = std::make_unique<DeviceArray<float>>(std::max<size_t>(1, op.rows.size()) * ROW_DATA_SIZE);
-        GP_CALL(gp_zero(slot->data(), slot->size(), nullptr));
+        GP_CALL(gp_zero(slot->data(), slot->size(), channels_[0]->stream->get()));
         planned += slot->bytes();
       }
       op.local_ptr = slot->data();
       continue;
     }
     op.buffer.resize(std::max<size_t>(1, op.rows.size()) * ROW_DATA_SIZE);
-    GP_CALL(gp_zero(op.buffer.data(), op.buffer.size(), nullptr));
+    GP_CALL(gp_zero(op.buffer.data(), op.buffer.size(), channels_[0]->stream->get()));
     planned += op.buffer.bytes();
     create_double_index(op);
   }
@@ -650,8 +649,8 @@ void ClientLib::create_double_index(OpInfo &op) {
   op.index.resize(std::max<size_t>(1, flat.size()));
   if (!flat.empty())
     GP_CALL(gp_memcpy_async(op.index.data(), flat.data(), flat.size() * sizeof(gp_double_index),
-                            nullptr));
-  GP_CALL(gp_device_synchronize());
+                            channels_[0]->stream->get()));
+  channels_[0]->stream->sync();
 }
 
 void ClientLib::start_iterations() {
@@ -936,8 +935,8 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       if (ch.send_buf.size() < floats) ch.send_buf.resize(floats);
       if (floats) {
         GP_CALL(gp_memcpy_async(ch.send_buf.data(), oplog->data() + a * ROW_DATA_SIZE, floats * 4,
-                                ch.send_stream->get()));
-        ch.send_stream->sync();
+                                ch.stream->get()));
+        ch.stream->sync();
       }
       cs_clock_with_updates_batch_msg_t h{};
       h.cmd = CLOCK_WITH_UPDATES_BATCH;
@@ -1010,16 +1009,16 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
         // needs a private copy (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
         float *dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
         const size_t floats = num_rows * ROW_DATA_SIZE;
-        GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.recv_stream->get()));
+        GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.svc_stream->get()));
         if (config_.read_my_writes) {
           for (iter_t c = self_clock + 1, fc = fast_clock_.load(); c <= fc; ++c) {
             auto it = pc.oplog.find(c);
             if (it == pc.oplog.end()) continue;
             const float *op = it->second->data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
-            GP_CALL(gp_add(floats, dst, op, dst, ch.recv_stream->get()));
+            GP_CALL(gp_add(floats, dst, op, dst, ch.svc_stream->get()));
           }
         }
-        ch.recv_stream->sync();
+        ch.svc_stream->sync();
         if (version >= 0) released.push_back(version);  // copied: give it back now
         if (prev >= 0) {
           released.push_back(prev);

@@ -126,7 +126,13 @@ struct Channel {
   // Per table: the clock's update ops write every oplog row of this channel
   // exactly once, so the first touch may be gp_scatter_init_rows (fused zero).
   std::vector<bool> init_ok;
-  std::unique_ptr<Stream> stream, recv_stream, send_stream, reply_stream;
+  // Two HIP streams per channel: `stream` for the app thread's work (Read
+  // gathers, Update scatters, push copies) and `svc_stream` for the service
+  // side (this channel's tablet server and its socket reader threads).  Every
+  // stream takes a hardware queue (GPU_MAX_HW_QUEUES per process, default 4);
+  // several processes sharing one GPU beyond the hardware's queue slots are
+  // time-sliced, which cost an 8-process clock 10x.
+  std::unique_ptr<Stream> stream, svc_stream;
   std::unique_ptr<ChannelSink> sink;
   std::unique_ptr<TabletServer> server;
   // client side: one socket per remote server (-1 = in-process server); the

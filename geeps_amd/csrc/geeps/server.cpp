@@ -32,12 +32,14 @@ std::string ServerStats::to_json() const {
 }
 
 TabletServer::TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num_clients,
-                           uint32_t num_tables, ClientSink *sink, int device)
+                           uint32_t num_tables, ClientSink *sink, int device,
+                           gp_stream stream)
     : server_id_(server_id),
       channel_id_(channel_id),
       num_clients_(num_clients),
       sink_(sink),
-      device_(device) {
+      device_(device),
+      stream_(stream) {
   GP_CHECK(sink_);
   GP_CHECK(num_clients_ > 0);
   tables_.resize(num_tables);
@@ -210,7 +212,7 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
     t.row_count = batch_size;
     t.cur = free_version(t);
     t.cur_published = false;
-    GP_CALL(gp_zero(t.versions[t.cur]->data(), batch_size * ROW_DATA_SIZE, stream_.get()));
+    GP_CALL(gp_zero(t.versions[t.cur]->data(), batch_size * ROW_DATA_SIZE, stream_));
     t.row_keys.assign(b.keys, b.keys + batch_size);
   }
   GP_CHECK_EQ(t.row_count, batch_size);
@@ -229,8 +231,8 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
     const double t0 = now_s();
     auto stage = stage_buffer(t);
     GP_CALL(gp_memcpy_async(stage->data(), b.host_rows->data(),
-                            batch_size * ROW_DATA_SIZE * sizeof(float), stream_.get()));
-    stream_.sync();  // host buffer is released when `b` dies
+                            batch_size * ROW_DATA_SIZE * sizeof(float), stream_));
+    GP_CALL(gp_stream_synchronize(stream_));  // host buffer is released when `b` dies
     stats_.stage_time += now_s() - t0;
     p.rows = stage->data();
     p.keepalive = stage;
@@ -280,8 +282,8 @@ void TabletServer::apply_pending(DataTable &t) {
     t.cur_published = false;
   }
   GP_CALL(gp_bucket_sum_into(t.versions[t.cur]->data(), in, ptrs.data(), (int)ptrs.size(),
-                             t.row_count * ROW_DATA_SIZE, stream_.get()));
-  stream_.sync();
+                             t.row_count * ROW_DATA_SIZE, stream_));
+  GP_CALL(gp_stream_synchronize(stream_));
   stats_.nr_apply_launches++;
   stats_.nr_buckets_applied += ptrs.size();
   t.pending.clear();  // releases oplog slices / staging buffers

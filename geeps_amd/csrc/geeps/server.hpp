@@ -119,8 +119,10 @@ class TabletServer {
   // `device`: the HIP device the owning process works on.  The server thread
   // selects it before its first HIP call, so the master shard, the staging
   // buffers and every launch land on that GPU (a new thread starts on device 0).
+  // `stream`: the HIP stream all of this server's device work goes to (not
+  // owned; the channel's service stream).
   TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num_clients,
-               uint32_t num_tables, ClientSink *sink, int device);
+               uint32_t num_tables, ClientSink *sink, int device, gp_stream stream);
   ~TabletServer();
   TabletServer(const TabletServer &) = delete;
   TabletServer &operator=(const TabletServer &) = delete;
@@ -186,7 +188,7 @@ class TabletServer {
   ClientSink *sink_;
   const int device_;
   std::vector<DataTable> tables_;
-  Stream stream_;
+  const gp_stream stream_;
   ServerStats stats_;
 
   std::mutex mu_;
