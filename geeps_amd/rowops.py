@@ -16,7 +16,7 @@ zerofy_data_gpu                    DataStorage::zerofy_data_gpu, common-util.hpp
 apply_updates                      TabletStorage::apply_updates x N in arrival order,
                                    src/server/tablet-server.cpp:119-134
 gather_rows_segmented              assign_rows_to_double_index_gpu over a param cache
-                                   split into row-range buffers (libgeeps refresh slots)
+                                   split into row-range buffers (libgeeps in-place refreshes)
 add_rows_segmented                 add_rows_from_double_index_gpu into such a cache
                                    (read-my-writes, clientlib-data.cpp:387-392)
 =================================  ===============================================

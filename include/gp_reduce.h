@@ -120,9 +120,10 @@ int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
  * GP_MAX_SEGMENTS contiguous row ranges, each living in its own buffer: range
  * i is rows [first_row[i], first_row[i+1]) (the last one open-ended) and cache
  * row c of range i is at base[i][(c - first_row[i]) * row_size].  libgeeps
- * uses it so a same-node server's refresh is read where the server wrote it
- * (the client's IPC inbox slot) instead of being copied into one contiguous
- * cache first; the reference has one contiguous cache (ParamCache::data_cache, clientlib.hpp:338-341).
+ * uses it so a refreshed shard is read in place from the server's published
+ * master version (its own buffer, or an IPC mapping of a same-node server's)
+ * instead of being copied into one contiguous cache first; the reference has
+ * one contiguous cache (ParamCache::data_cache, clientlib.hpp:338-341).
  * first_row[0] must be 0 and first_row strictly ascending.
  * ------------------------------------------------------------------------- */
 #define GP_MAX_SEGMENTS 64
