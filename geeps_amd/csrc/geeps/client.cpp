@@ -26,7 +26,13 @@ double now_s() {
 }
 
 constexpr size_t kRowBytes = sizeof(RowData);
-constexpr double kConnectTimeoutS = 300.0;
+// How long a client retries connecting to a server that is not listening yet
+// (processes start at different times); GEEPS_CONNECT_TIMEOUT_S overrides.
+double connect_timeout_s() {
+  const char *e = std::getenv("GEEPS_CONNECT_TIMEOUT_S");
+  const double v = e ? std::atof(e) : 0.0;
+  return v > 0 ? v : 300.0;
+}
 constexpr int kWaitWarnMs = 12000;  // the reference's 12 s timed_wait warnings
 
 struct PinnedPool {
@@ -138,7 +144,7 @@ void ClientLib::start_network() {
     for (uint32_t s = 0; s < num_processes_; ++s) {
       if (s == process_id_) continue;
       std::string err;
-      const int fd = connect_tcp(config_.host_list[s], port_of(s, ch.id), kConnectTimeoutS, &err);
+      const int fd = connect_tcp(config_.host_list[s], port_of(s, ch.id), connect_timeout_s(), &err);
       GP_CHECK_MSG(fd >= 0, err);
       // third word: this client takes same-node refreshes in place (IPC)
       const uint32_t hello[3] = {kHelloCmd, process_id_, ipc_to(s) ? 1u : 0u};

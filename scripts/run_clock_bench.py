@@ -21,12 +21,37 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(REPO, "build", "apps", "geeps_clock_bench")
 
 
+def free_port_base(n_proc, channels, lo=20000, hi=32000):
+    """A base port with every port base + 16 p + c (p < n_proc, c < channels)
+    bindable right now, chosen BELOW the kernel's ephemeral range (32768-60999
+    here): outgoing connections take ephemeral ports, so a base picked there can
+    collide with one of them between this check and the processes' bind."""
+    import random
+    import socket
+    rng = random.Random()
+    span = 16 * n_proc + channels
+    for _ in range(200):
+        base = rng.randrange(lo, hi - span)
+        ok = True
+        for p in range(n_proc):
+            for c in range(channels):
+                with socket.socket() as s:
+                    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                    try:
+                        s.bind(("127.0.0.1", base + 16 * p + c))
+                    except OSError:
+                        ok = False
+                if not ok:
+                    break
+            if not ok:
+                break
+        if ok:
+            return base
+    raise RuntimeError("no free port range")
+
+
 def free_base(P):
-    # ports base + 16*p (+channel) must be free; take the OS's pick as a base
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        base = s.getsockname()[1]
-    return max(20000, min(base, 60000 - 16 * P))
+    return free_port_base(P, 1)
 
 
 def main():

@@ -4,7 +4,7 @@
 # time limit.  Usage: run_sum_app.sh OUTDIR SECONDS TRANSPORT P rows clocks slack channels rmw mode [spec]
 out=$1; lim=$2; tr=$3; P=$4; shift 4
 mkdir -p "$out"
-base=$(( 20000 + (RANDOM % 2000) * 16 ))
+base=$(( 20000 + (RANDOM % 700) * 16 ))  # below the ephemeral port range (32768+)
 pids=()
 for ((p = 0; p < P; p++)); do
   GEEPS_TRANSPORT=$tr timeout -k 5 "$lim" "$GRAFT_REPO_ROOT/build/tests/geeps_sum_app" "$p" "$P" "$base" "$@" \

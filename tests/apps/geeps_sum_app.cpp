@@ -9,6 +9,10 @@
 // `local` = 1 adds a LocalAccess(fetch) / PostLocalAccess(keep) pair whose
 // buffer must carry the previous iteration's contents into the next one;
 // `output_dir` sets GeePsConfig::output_dir (GetStats appends json_stats.<pid>).
+// GEEPS_TEST_JITTER_US=J in the environment: before every Read and every Clock
+// the process sleeps a pseudo-random 0..J us (seeded by its id), so processes
+// drift apart and refreshes, master-version switches and releases interleave
+// differently from run to run.
 //
 // `layers` (comma-separated row counts, summing to `rows`) switches to a
 // Caffe-like op sequence: a Read per parameter blob in forward order, then per
@@ -27,7 +31,9 @@
 // i-slack-1 and through clock i+slack (deltas are positive).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -171,6 +177,16 @@ int main(int argc, char **argv) {
 
   int bad = 0;
   std::vector<float> lbuf(local_rows * ROW_DATA_SIZE);
+  const char *jit = std::getenv("GEEPS_TEST_JITTER_US");
+  const unsigned jitter_us = jit ? (unsigned)std::strtoul(jit, nullptr, 10) : 0;
+  uint32_t jstate = 0x9e3779b9u ^ (uint32_t)(pid * 7919 + 1);
+  auto jitter = [&] {
+    if (!jitter_us) return;
+    jstate ^= jstate << 13;
+    jstate ^= jstate >> 17;
+    jstate ^= jstate << 5;
+    std::this_thread::sleep_for(std::chrono::microseconds(jstate % (jitter_us + 1)));
+  };
   for (int it = 1; it <= clocks; ++it) {
     if (use_local) {
       // Local data persists across iterations: it holds what we wrote last time.
@@ -188,6 +204,7 @@ int main(int argc, char **argv) {
     }
     for (size_t l = 0; l < L; ++l) {
       RowData *rbuf = nullptr;
+      jitter();
       ps->Read(h_read[l], &rbuf);
       const size_t e0 = first[l] * ROW_DATA_SIZE, ne = layer_rows[l] * ROW_DATA_SIZE;
       HCK(hipMemcpy(got.data() + e0, rbuf, ne * 4, hipMemcpyDeviceToHost));
@@ -213,6 +230,7 @@ int main(int argc, char **argv) {
     }
     push(it, true);
     if (use_local) ps->PostLocalAccess(h_local_post);
+    jitter();
     ps->Clock();
   }
   std::string stats = ps->GetStats();

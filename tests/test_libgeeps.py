@@ -10,6 +10,8 @@ PS processes over loopback"), BSP and SSP, 1-2 channels, read-my-writes.
 import os
 import socket
 import subprocess
+import tempfile
+import time
 
 import pytest
 
@@ -60,44 +62,100 @@ def test_app_links_with_public_header_only(tmp_path):
                     "-L", os.path.dirname(LIB), "-lgeeps", "-o", str(tmp_path / "app")], check=True)
 
 
+def _free_port_base(n_proc, channels, lo=20000, hi=32000):
+    """A base port with every port base + 16 p + c (p < n_proc, c < channels)
+    bindable right now, chosen BELOW the kernel's ephemeral range (32768-60999
+    here): outgoing connections take ephemeral ports, so a base picked there can
+    collide with one of them between this check and the processes' bind."""
+    import random
+    import socket
+    rng = random.Random()
+    span = 16 * n_proc + channels
+    for _ in range(200):
+        base = rng.randrange(lo, hi - span)
+        ok = True
+        for p in range(n_proc):
+            for c in range(channels):
+                with socket.socket() as s:
+                    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                    try:
+                        s.bind(("127.0.0.1", base + 16 * p + c))
+                    except OSError:
+                        ok = False
+                if not ok:
+                    break
+            if not ok:
+                break
+        if ok:
+            return base
+    raise RuntimeError("no free port range")
+
+
 def _ports(n_proc, channels):
     """A base port with n_proc * 16 free ports above it (port_list[p] = base + 16 p)."""
-    for _ in range(50):
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            base = s.getsockname()[1]
-        if base + 16 * n_proc + channels < 65000:
-            return base
-    raise RuntimeError("no port range")
+    return _free_port_base(n_proc, channels)
 
 
-def _env(transport):
+def _env(transport, jitter_us=0):
     env = dict(os.environ)
     env["GEEPS_TRANSPORT"] = transport  # "ipc": same-node rows over IPC-mapped HBM; "tcp": sockets
+    # a peer that dies before listening fails the others in a minute, not five
+    env.setdefault("GEEPS_CONNECT_TIMEOUT_S", "60")
+    if jitter_us:
+        env["GEEPS_TEST_JITTER_US"] = str(jitter_us)
     return env
 
 
-def _run_app(P, rows, clocks, slack, channels, rmw, mode="int", timeout=240, transport="ipc"):
+def _spawn(cmd, env):
+    """One app process with stdout / stderr in temporary files (a full pipe can
+    never stall it while the test waits on another process)."""
+    out, err = tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")
+    pr = subprocess.Popen(cmd, stdout=out, stderr=err, text=True, env=env)
+    pr.out_file, pr.err_file = out, err
+    return pr
+
+
+def _collect(procs, timeout):
+    """Wait for every process under one deadline; on a failure or a hang, kill
+    the rest and report EVERY process's output (a hang in one process usually
+    starts as an abort in another)."""
+    deadline = time.monotonic() + timeout
+    for pr in procs:
+        try:
+            pr.wait(timeout=max(0.1, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            break
+    hung = [p for p, pr in enumerate(procs) if pr.poll() is None]
+    for pr in procs:
+        if pr.poll() is None:
+            pr.kill()
+    outs = []
+    for pr in procs:
+        pr.wait()
+        streams = []
+        for f in (pr.out_file, pr.err_file):
+            f.seek(0)
+            streams.append(f.read())
+            f.close()
+        outs.append((pr.returncode, streams[0], streams[1]))
+    failed = hung or any(rc != 0 or not o.startswith("OK") for rc, o, _ in outs)
+    if failed:
+        report = [f"hung (killed after {timeout} s): {hung}"] if hung else []
+        for p, (rc, o, e) in enumerate(outs):
+            report.append(f"--- process {p} rc={rc}\n{o[-1500:]}\n{e[-2500:]}")
+        raise AssertionError("\n".join(report))
+    return outs
+
+
+def _run_app(P, rows, clocks, slack, channels, rmw, mode="int", timeout=240, transport="ipc",
+             jitter_us=0):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, channels)
-    procs = [subprocess.Popen([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
-                               str(channels), str(rmw), mode],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                              env=_env(transport))
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
+                     str(channels), str(rmw), mode], _env(transport, jitter_us))
              for p in range(P)]
-    outs = []
-    try:
-        for pr in procs:
-            o, e = pr.communicate(timeout=timeout)
-            outs.append((pr.returncode, o, e))
-    finally:
-        for pr in procs:
-            if pr.poll() is None:
-                pr.kill()
-    for p, (rc, o, e) in enumerate(outs):
-        assert rc == 0 and o.startswith("OK"), f"process {p} rc={rc}\n{o}\n{e[-3000:]}"
-    return outs
+    return _collect(procs, timeout)
 
 
 @pytest.mark.gpu
@@ -142,6 +200,23 @@ def test_two_processes_read_my_writes(dev, transport):
 @pytest.mark.parametrize("transport", ["ipc", "tcp"])
 def test_four_processes_ssp_slack2(dev, transport):
     _run_app(4, rows=2048, clocks=12, slack=2, channels=1, rmw=0, transport=transport)
+
+
+# ---- desynchronized processes: refreshes, master-version switches and releases
+# interleave differently (every Read and Clock preceded by a random sleep) ------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+@pytest.mark.parametrize("slack", [0, 1, 3])
+def test_jittered_processes(dev, transport, slack):
+    _run_app(4, rows=1500, clocks=25, slack=slack, channels=2, rmw=0, transport=transport,
+             jitter_us=3000, timeout=120)
+
+
+@pytest.mark.gpu
+def test_jittered_read_my_writes(dev):
+    _run_app(3, rows=640, clocks=20, slack=2, channels=1, rmw=1, transport="ipc", jitter_us=3000,
+             timeout=120)
 
 
 # ---- BASELINE configs 4 and 5: layered param tables (Caffe is absent) ---------
@@ -204,22 +279,10 @@ def _run_app_layers(P, rows, spec, clocks, slack, timeout=600, transport="ipc", 
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, 1)
-    procs = [subprocess.Popen([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
-                               "1", "0", "int", spec, str(tables), str(local), out_dir],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                              env=_env(transport))
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
+                     "1", "0", "int", spec, str(tables), str(local), out_dir], _env(transport))
              for p in range(P)]
-    outs = []
-    try:
-        for pr in procs:
-            o, e = pr.communicate(timeout=timeout)
-            outs.append((pr.returncode, o, e))
-    finally:
-        for pr in procs:
-            if pr.poll() is None:
-                pr.kill()
-    for p, (rc, o, e) in enumerate(outs):
-        assert rc == 0 and o.startswith("OK"), f"process {p} rc={rc}\n{o}\n{e[-3000:]}"
+    _collect(procs, timeout)
 
 
 @pytest.mark.gpu
