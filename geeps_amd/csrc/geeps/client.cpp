@@ -526,9 +526,17 @@ void ClientLib::finish_virtual_iteration() {
         pc.index[r] = pc.num_rows++;
         pc.row_keys->emplace_back(t, r);
       }
-      pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
-      if (pc.num_rows) GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.stream->get()));
-      planned += pc.num_rows * kRowBytes * (1 + entries);
+      // The cache's own rows are needed only for refreshes that arrive as
+      // copies (socket peers, read-my-writes, which also scatters into it).
+      // When every server's shard will be read in place, it is never touched
+      // (a Read waits for every server's first refresh) and is not allocated.
+      bool copies = config_.read_my_writes;
+      for (uint32_t s = 0; s < num_processes_; ++s) copies = copies || (s != process_id_ && !ipc_to(s));
+      if (copies) {
+        pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
+        if (pc.num_rows) GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.stream->get()));
+      }
+      planned += pc.num_rows * kRowBytes * ((copies ? 1 : 0) + entries);
       pc.server_row_start.resize(num_processes_);
       pc.server_num_rows.resize(num_processes_);
       const size_t div = pc.num_rows / num_processes_, res = pc.num_rows % num_processes_;
@@ -995,6 +1003,14 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
       reclaim_oplogs(pc, min_clock);
       pc.server_clock_min = min_clock;
     }
+    if (num_rows == 0 && pc.num_rows && pc.data.size() == 0) {
+      // An empty shard reads as zeros from the cache's own rows, which a
+      // cache that takes every refresh in place has not allocated yet.
+      pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
+      GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.svc_stream->get()));
+      ch.svc_stream->sync();
+      rebuild_segments(pc);
+    }
     if (num_rows) {
       const int prev = pc.live_ver[server_id];
       if (version >= 0 && !config_.read_my_writes) {
@@ -1013,6 +1029,8 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
         // rows from a socket, or read-my-writes, which re-applies this
         // client's own not-yet-reflected updates on top of the shard and so
         // needs a private copy (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
+        GP_CHECK_MSG(pc.data.size() == pc.num_rows * ROW_DATA_SIZE,
+                     "copied refresh from server " << server_id << " into an unallocated cache");
         float *dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
         const size_t floats = num_rows * ROW_DATA_SIZE;
         GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.svc_stream->get()));
@@ -1056,7 +1074,9 @@ void ClientLib::rebuild_segments(ParamCache &pc) {
     if (n == 0) continue;
     const size_t first = pc.server_row_start[s];
     const bool in_place = pc.live_ver[s] >= 0;
-    const float *base = in_place ? pc.live_ptr[s] : pc.data.data() + first * ROW_DATA_SIZE;
+    // (a shard neither in place nor copied yet is never read: see Read's wait)
+    const float *base = in_place ? pc.live_ptr[s]
+                                 : pc.data.data() ? pc.data.data() + first * ROW_DATA_SIZE : nullptr;
     any_in_place = any_in_place || in_place;
     if (t.count && base == next_flat && !in_place) {
       next_flat = base + n * ROW_DATA_SIZE;

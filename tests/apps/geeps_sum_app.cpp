@@ -13,6 +13,8 @@
 // the process sleeps a pseudo-random 0..J us (seeded by its id), so processes
 // drift apart and refreshes, master-version switches and releases interleave
 // differently from run to run.
+// GEEPS_TEST_EMPTY_SETUP=1: the setup clock (clock 0) carries no updates, so
+// every server's first refresh is an empty shard (all zeros).
 //
 // `layers` (comma-separated row counts, summing to `rows`) switches to a
 // Caffe-like op sequence: a Read per parameter blob in forward order, then per
@@ -158,9 +160,11 @@ int main(int argc, char **argv) {
   };
   // Expected sums through clock k, over all processes, in the order the
   // single-process server applies them (k = -1: zeros).
+  const bool empty_setup = std::getenv("GEEPS_TEST_EMPTY_SETUP") != nullptr;
   std::vector<std::vector<float>> through(clocks + 2, std::vector<float>(n, 0.0f));
   for (int k = 0; k <= clocks; ++k) {
     through[k + 1] = through[k];
+    if (k == 0 && empty_setup) continue;
     for (int p = 0; p < P; ++p)
       for (size_t e = 0; e < n; ++e) through[k + 1][e] += delta(p, k, e, fl);
   }
@@ -171,7 +175,7 @@ int main(int argc, char **argv) {
   };
 
   // Setup clock (clock 0) before StartIterations, as apps/helloworld does.
-  push(0, false);
+  if (!empty_setup) push(0, false);
   ps->Clock();
   ps->StartIterations();
 

@@ -96,8 +96,10 @@ def _ports(n_proc, channels):
     return _free_port_base(n_proc, channels)
 
 
-def _env(transport, jitter_us=0):
+def _env(transport, jitter_us=0, empty_setup=False):
     env = dict(os.environ)
+    if empty_setup:
+        env["GEEPS_TEST_EMPTY_SETUP"] = "1"  # first refreshes are empty shards
     env["GEEPS_TRANSPORT"] = transport  # "ipc": same-node rows over IPC-mapped HBM; "tcp": sockets
     # a peer that dies before listening fails the others in a minute, not five
     env.setdefault("GEEPS_CONNECT_TIMEOUT_S", "60")
@@ -148,12 +150,12 @@ def _collect(procs, timeout):
 
 
 def _run_app(P, rows, clocks, slack, channels, rmw, mode="int", timeout=240, transport="ipc",
-             jitter_us=0):
+             jitter_us=0, empty_setup=False):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, channels)
     procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
-                     str(channels), str(rmw), mode], _env(transport, jitter_us))
+                     str(channels), str(rmw), mode], _env(transport, jitter_us, empty_setup))
              for p in range(P)]
     return _collect(procs, timeout)
 
@@ -211,6 +213,15 @@ def test_four_processes_ssp_slack2(dev, transport):
 def test_jittered_processes(dev, transport, slack):
     _run_app(4, rows=1500, clocks=25, slack=slack, channels=2, rmw=0, transport=transport,
              jitter_us=3000, timeout=120)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 3])
+def test_setup_clock_without_updates(dev, P):
+    # every server's first refresh is an empty shard: Reads see zeros from the
+    # cache's own rows, allocated on that refresh when all later ones are in place
+    _run_app(P, rows=500, clocks=6, slack=0, channels=1, rmw=0, transport="ipc", empty_setup=True,
+             timeout=120)
 
 
 @pytest.mark.gpu
