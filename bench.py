@@ -10,17 +10,20 @@ hosted on rank c % N; its delta buffer is uniform in [-0.5, 0.5) (seed 1000+c).
 
 A *step* is one device-resident N-way reduction: each shard adds the 8 client
 buckets for its rows into its master copy in client order 0..7 with one
-gp_bucket_sum_apply launch (the reference's TabletStorage::apply_updates x 8,
-src/server/tablet-server.cpp:119-134).  At N > 1 the buckets were first moved
+gp_bucket_sum_apply call (the reference's TabletStorage::apply_updates x 8,
+src/server/tablet-server.cpp:119-134); for a 4 GiB shard that call issues 32
+launches of the phase-separated kernel, each summing 128 MiB of the shard.  At N > 1 the buckets were first moved
 to their shard by RCCL all-to-all (untimed here; the exchange-inclusive step
 exchange + apply + all-gather refresh is timed separately and reported as
 `exchange_inclusive`).  Total work is fixed as N grows: scaling "strong".
 
 value = gradient (delta) bytes reduced per second, whole job:
         clients * rows * width * 4 B / max-over-ranks step time.
-roofline.achieved = algorithmic HBM bytes of one launch ((clients + 2) * shard
-        bytes: 8 bucket reads + master read + master write) / its average
-        duration from HIP events on the launch stream.
+roofline.achieved = algorithmic HBM bytes of one step ((clients + 2) * shard
+        bytes: 8 bucket reads + master read + master write) / the step's
+        average kernel time from HIP events around its launches on their
+        stream; per launch, the same ratio (avg_launch_ms is what rocprofv3
+        reports for the kernel).
 cpu_baseline = the oracle's restatement of the reference server arithmetic
         (sequential vsAdd per client, gcc -O3) on rank 0's host cores, on a
         bounded 128K-row sample.
@@ -41,7 +44,21 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roofline"
-KERNEL_NAME = "bucket_sum_vec_kernel"
+# Launch plan of gp_bucket_sum_apply (geeps_amd/csrc/gp_reduce.hip): shards of at
+# least one full phase-separated launch (4 chunks of 2 blocks/CU x 64 KiB) go to
+# bucket_sum_phased_kernel, kPhaseChunks chunks per launch; smaller ones to
+# bucket_sum_vec_kernel in one launch.
+PHASE_LDS_F4, PHASE_BLOCKS_PER_CU, PHASE_CHUNKS, TILE_F4 = 4096, 2, 4, 1024
+
+
+def sum_launch_plan(num_vals: int, num_cus: int):
+    """(dominant kernel name, its launches per step) for one N-way sum of num_vals floats."""
+    n4_tiles = num_vals // 4 // TILE_F4 * TILE_F4
+    chunk_f4 = num_cus * PHASE_BLOCKS_PER_CU * PHASE_LDS_F4
+    if n4_tiles >= chunk_f4 * PHASE_CHUNKS:
+        chunks = -(-n4_tiles // chunk_f4)
+        return "bucket_sum_phased_kernel", -(-chunks // PHASE_CHUNKS)
+    return "bucket_sum_vec_kernel", 1
 
 
 def log(*a):
@@ -352,6 +369,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
     wall = max_over_ranks(wall, world, dev)
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     avg_kernel_ms_max = max_over_ranks(avg_kernel_ms, world, dev)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
+    kernel_name, launches = sum_launch_plan(L.local_vals, cus)
     step_s = wall / args.steps
     delta_bytes = C * R * W * 4
     value = delta_bytes / step_s / 1e9
@@ -430,9 +449,14 @@ def main(argv=None, backend="nccl", apply_fn=None):
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_min / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "kernel": KERNEL_NAME,
+                         "kernel": kernel_name,
+                         "launches_per_step": launches,
+                         # HIP events around each step's launches on their stream
                          "avg_kernel_ms": round(avg_kernel_ms_max, 4),
-                         "algorithmic_bytes_per_launch": algo_bytes},
+                         # per launch, comparable with rocprofv3's average for the kernel
+                         "avg_launch_ms": round(avg_kernel_ms_max / launches, 5),
+                         "algorithmic_bytes_per_step": algo_bytes,
+                         "algorithmic_bytes_per_launch": algo_bytes // launches},
             "hbm_GBps_algorithmic": round((C + 2) * R * W * 4 / step_s / 1e9, 1),
             "cpu_baseline": cpu,
         }

@@ -150,35 +150,129 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
   }
 }
 
+// Phase-separated form for large shards.  Every byte still moves once, but a
+// CU first READS a chunk (master + NB buckets, summed into LDS), then WRITES
+// it back, instead of interleaving its loads and stores.  Measured on MI355X
+// (scripts/tune/alloc_tune.hip, phase_tune.hip; profiles/r01b/): the nine
+// read streams of an 8-way sum alone run at 6.8-6.9 TB/s and the master's
+// write stream alone at 5.1-5.3 TB/s on every allocation, while the mixed
+// stream loses 10-25 % to read/write interleaving on HBM, most on
+// allocations whose pages mix badly.  Holding results in LDS until the
+// chunk's reads are done cut the 8-way sum from 7.25-8.25 ms to 7.17-7.64 ms
+// over the same allocations, and 2- and 4-way sums by 8-10 %.
+//
+// No grid barrier: a launch covers kPhaseChunks chunks, and its blocks stay
+// roughly in phase because they do identical work and start together (a
+// launch boundary re-aligns them; 4 chunks per launch measured best of 1-4).
+// Chunk c of a launch covers f4 [lo, lo + G * kPhaseLdsF4); block g takes its
+// 16-KiB tiles g, g + G, ...  Only whole tiles: the caller passes
+// n4_tiles, a multiple of kBlock * 4, and sums any rest with the mixed form.
+// The order of the adds per element is the bucket order, as in every form.
+constexpr int kPhaseLdsF4 = 4096;  // 64 KiB of results per block, 2 blocks per CU
+constexpr int kPhaseBlocksPerCU = 2;
+constexpr int kPhaseChunks = 4;    // chunks per launch
+
+template <int NB>
+__global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
+    f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
+    size_t chunk0) {
+  constexpr int U = 4;
+  constexpr int kTile = kBlock * U;
+  constexpr int kTilesPerBlock = kPhaseLdsF4 / kTile;
+  __shared__ f4 res[kPhaseLdsF4];
+  const f4 *bp[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) bp[k] = reinterpret_cast<const f4 *>(b.p[k]);
+  const size_t G = gridDim.x;
+  const size_t chunk_f4 = G * kPhaseLdsF4;
+  for (int kc = 0; kc < kPhaseChunks; ++kc) {
+    const size_t lo = (chunk0 + kc) * chunk_f4;
+    if (lo >= n4_tiles) return;  // grid-uniform: no block skips a barrier another waits at
+    // read phase: sum the chunk's tiles into LDS
+    for (int t = 0; t < kTilesPerBlock; ++t) {
+      const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kTile;
+      if (tile0 >= n4_tiles) break;  // block-uniform
+      const size_t base = tile0 + threadIdx.x;
+      f4 acc[U];
+      f4 v[NB][U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = in[base + u * kBlock];
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[k][u] = ld_stream(bp[k] + base + u * kBlock);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) acc[u] += v[k][u];  // bucket order 0..NB-1
+        res[t * kTile + u * kBlock + threadIdx.x] = acc[u];
+      }
+    }
+    __syncthreads();
+    // write phase
+    for (int t = 0; t < kTilesPerBlock; ++t) {
+      const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kTile;
+      if (tile0 >= n4_tiles) break;
+      const size_t base = tile0 + threadIdx.x;
+#pragma unroll
+      for (int u = 0; u < U; ++u) out[base + u * kBlock] = res[t * kTile + u * kBlock + threadIdx.x];
+    }
+    __syncthreads();
+  }
+}
+
+// Buckets advanced by `off` floats.
+template <int NB>
+BucketPtrs offset_buckets(const BucketPtrs &b, size_t off) {
+  BucketPtrs t = {};
+  for (int k = 0; k < NB; ++k) t.p[k] = b.p[k] + off;
+  return t;
+}
+
+// out[i] = in[i] + b0[i] + ... over i < n: the phase-separated form over the
+// whole 16-KiB tiles of a large shard, the mixed dwordx4 form over what is
+// left of the 16-B-aligned part, the scalar form over the rest.
 template <int NB>
 int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
                          size_t n, hipStream_t s) {
   bool vec = aligned16(out) && aligned16(in);
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
-  size_t done = 0;
-  if (vec && n >= 4) {
+  size_t done = 0;  // floats summed so far
+  if (vec) {
+    const size_t tile = (size_t)kBlock * 4;
+    const size_t n4_tiles = n / 4 / tile * tile;
+    const size_t G = (size_t)num_cus() * kPhaseBlocksPerCU;
+    const size_t chunk_f4 = G * kPhaseLdsF4;
+    if (n4_tiles >= chunk_f4 * kPhaseChunks) {  // at least one full launch (128 MiB on 256 CUs)
+      const size_t chunks = (n4_tiles + chunk_f4 - 1) / chunk_f4;
+      for (size_t c = 0; c < chunks; c += kPhaseChunks)
+        hipLaunchKernelGGL((bucket_sum_phased_kernel<NB>), dim3((unsigned)G), dim3(kBlock), 0, s,
+                           reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
+                           n4_tiles, c);
+      done = n4_tiles * 4;
+    }
+  }
+  if (vec && n - done >= 4) {
     // 4 block-strides per thread at 2 blocks per CU: (NB + 1) * 4 dwordx4 loads
     // in flight per lane.  Measured on MI355X at 8 x 4 GiB buckets: +2-3 % over
     // 1 stride at 8 blocks/CU (profiles/r01/bucket_tune_sweep*.txt).
     constexpr int U = 4;
     constexpr int kPerCU = NB <= 2 ? 4 : 2;
-    const size_t n4 = n / 4;
+    const size_t n4 = (n - done) / 4;
     const size_t tiles = (n4 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
     const size_t cap = (size_t)num_cus() * kPerCU;
     const size_t grid = tiles < cap ? tiles : cap;
     hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out),
-                       reinterpret_cast<const f4 *>(in), b, n4);
-    done = n4 * 4;
+                       dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out + done),
+                       reinterpret_cast<const f4 *>(in + done), offset_buckets<NB>(b, done), n4);
+    done += n4 * 4;
   }
   if (done < n) {
-    BucketPtrs t;
-    for (int k = 0; k < NB; ++k) t.p[k] = b.p[k] + done;
     const size_t rem = n - done;
     size_t grid = (rem + kBlock - 1) / kBlock;
     if (grid > grid_cap()) grid = grid_cap();
     hipLaunchKernelGGL((bucket_sum_scalar_kernel<NB>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, s, out + done, in + done, t, rem);
+                       dim3(kBlock), 0, s, out + done, in + done, offset_buckets<NB>(b, done), rem);
   }
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;

@@ -38,6 +38,39 @@ __global__ void fill_k(float *p, size_t n, unsigned seed) {
 }
 
 
+
+// Diagnostics per arena: the nine read streams alone (no store), and the
+// master's write stream alone.
+__global__ __launch_bounds__(kBlock) void read9(const f4 *__restrict__ m, BucketPtrs b, size_t n4,
+                                                f4 *__restrict__ sink, int flag) {
+  constexpr int U = 4;
+  const size_t tile = (size_t)kBlock * U;
+  const size_t stride = (size_t)gridDim.x * tile;
+  f4 tot = {0, 0, 0, 0};
+  for (size_t base = (size_t)blockIdx.x * tile + threadIdx.x; base + (U - 1) * kBlock < n4;
+       base += stride) {
+    f4 v[9][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[8][u] = m[base + u * kBlock];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[k][u] = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(b.p[k]) + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) tot += v[k][u];
+  }
+  if (flag) sink[blockIdx.x * kBlock + threadIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void write1(f4 *__restrict__ m, size_t n4) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  const f4 z = {1, 2, 3, 4};
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) m[i] = z;
+}
+
 struct Set {
   std::string name;
   BucketPtrs b;
@@ -86,10 +119,18 @@ int main(int argc, char **argv) {
     std::vector<float> ms;
   };
   std::vector<V> vs;
+  const unsigned grid2 = (unsigned)num_cus() * 2, grid8 = (unsigned)num_cus() * 8;
+  std::vector<double> vbytes;
   for (auto &s : sets) {
     std::vector<const float *> bv(s.b.p, s.b.p + 8);
     float *m = s.master;
-    vs.push_back(V{s.name, [=]() { gp_bucket_sum_apply(m, bv.data(), 8, kN, nullptr); }, {}});
+    BucketPtrs bp = s.b;
+    vs.push_back(V{s.name + " sum", [=]() { gp_bucket_sum_apply(m, bv.data(), 8, kN, nullptr); }, {}});
+    vbytes.push_back(10.0 * kN * 4);
+    vs.push_back(V{s.name + " read9", [=]() { read9<<<grid2, kBlock>>>(reinterpret_cast<const f4 *>(m), bp, kN / 4, reinterpret_cast<f4 *>(m), 0); }, {}});
+    vbytes.push_back(9.0 * kN * 4);
+    vs.push_back(V{s.name + " write1", [=]() { write1<<<grid8, kBlock>>>(reinterpret_cast<f4 *>(m), kN / 4); }, {}});
+    vbytes.push_back(1.0 * kN * 4);
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -107,13 +148,14 @@ int main(int argc, char **argv) {
       v.ms.push_back(ms);
     }
   }
-  const double sum_b = 10.0 * kN * 4;
-  std::printf("%-28s %10s %10s %10s %8s\n", "allocation", "med_ms", "min_ms", "GB/s", "frac8T");
-  for (auto &v : vs) {
+  std::printf("%-34s %10s %10s %10s %8s\n", "allocation / kernel", "med_ms", "min_ms", "GB/s", "frac8T");
+  for (size_t i = 0; i < vs.size(); ++i) {
+    auto &v = vs[i];
+    const double sum_b = vbytes[i];
     std::sort(v.ms.begin(), v.ms.end());
     const double med = v.ms[v.ms.size() / 2];
     const double gbs = sum_b / (med * 1e-3) / 1e9;
-    std::printf("%-28s %10.4f %10.4f %10.1f %8.4f\n", v.name.c_str(), med, v.ms[0], gbs, gbs / 8000.0);
+    std::printf("%-34s %10.4f %10.4f %10.1f %8.4f\n", v.name.c_str(), med, v.ms[0], gbs, gbs / 8000.0);
   }
   return 0;
 }

@@ -142,6 +142,33 @@ def test_bucket_sum_into_leaves_master(dev, N):
     assert np.array_equal(bits(m.cpu().numpy()), bits(m0))
 
 
+@pytest.mark.parametrize("N,out_of_place", [(1, False), (3, False), (8, False), (8, True), (11, True)])
+def test_bucket_sum_phase_separated_path(dev, N, out_of_place):
+    """Shards of >= 128 MiB take the phase-separated kernel (reads summed into LDS
+    per chunk, then written) over their whole 16-KiB tiles; the rest goes to the
+    mixed and scalar forms.  This size gives 4 full chunks + a partial one (two
+    launches), 3 leftover tiles' worth of dwordx4 plus a 7-float scalar tail:
+    every element checked bit for bit."""
+    from geeps_amd import rowops
+    n = (32 << 20) + 1024 * 4 * 3 + 7
+    ups = [oracle.synthetic_delta(300 + c, n) for c in range(N)]
+    m0 = np.random.default_rng(N).standard_normal(n).astype(np.float32)
+    e = m0.copy()
+    oracle.apply_updates(e, ups)
+    m = T(m0, dev)
+    tb = [T(u, dev) for u in ups]
+    if out_of_place:
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+        rowops.bucket_sum_into(out, m, tb)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(m.cpu().numpy()), bits(m0))
+    else:
+        rowops.bucket_sum_apply(m, tb)
+        out = m
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()), bits(e))
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 255, 256, 257, 1023, 1024 * 256 + 3])
 def test_bucket_sum_sizes_and_alignment(dev, n):
     from geeps_amd import rowops
