@@ -4,13 +4,15 @@
 // Two kernel families, both HBM-bandwidth bound (elementwise fp32 add; no
 // MFMA — there is no contraction here):
 //
-//  * bucket_sum_kernel  — the server's N-way sum of client delta buckets into
+//  * bucket_sum_*_kernel — the server's N-way sum of client delta buckets into
 //    the master shard (reference: TabletStorage::apply_updates,
 //    src/server/tablet-server.cpp:119-134, applied once per client message).
 //    The reference makes N sequential passes over the shard (3 streams x 4 B
 //    per element per client); here one pass reads master + N buckets once and
 //    writes master once, summing in bucket order so every element is
-//    bit-identical to the sequential form.
+//    bit-identical to the sequential form.  Large shards use the
+//    phase-separated form (reads of a chunk summed into LDS, then written),
+//    smaller ones and leftovers the mixed dwordx4 form, then a scalar tail.
 //
 //  * row_op_kernel — the row-indexed scatter-add / gather / scatter-assign
 //    over a DoubleIndex (reference: src/common/row-op-util.cu:39-142).  The
