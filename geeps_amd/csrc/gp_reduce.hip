@@ -163,16 +163,22 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
 // chunk's reads are done cut the 8-way sum from 7.25-8.25 ms to 7.17-7.64 ms
 // over the same allocations, and 2- and 4-way sums by 8-10 %.
 //
-// No grid barrier: a launch covers kPhaseChunks chunks, and its blocks stay
-// roughly in phase because they do identical work and start together (a
-// launch boundary re-aligns them; 4 chunks per launch measured best of 1-4).
+// No grid barrier: a launch covers K chunks, and its blocks stay roughly in
+// phase because they do identical work and start together (a launch boundary
+// re-aligns them).  K = 2 for 8 buckets and 4 below measured best of 1-4.
+// Every access is non-temporal here (master loads and stores too, unlike the
+// mixed form): +1.5-3 % at 1-8 buckets over plain master accesses, which
+// otherwise linger in the caches and drain to HBM during the next read phase.
 // Chunk c of a launch covers f4 [lo, lo + G * kPhaseLdsF4); block g takes its
 // 16-KiB tiles g, g + G, ...  Only whole tiles: the caller passes
 // n4_tiles, a multiple of kBlock * 4, and sums any rest with the mixed form.
 // The order of the adds per element is the bucket order, as in every form.
 constexpr int kPhaseLdsF4 = 4096;  // 64 KiB of results per block, 2 blocks per CU
 constexpr int kPhaseBlocksPerCU = 2;
-constexpr int kPhaseChunks = 4;    // chunks per launch
+constexpr int kPhaseMinChunks = 4;  // shards below 4 chunks (128 MiB on 256 CUs): mixed form
+
+template <int NB>
+constexpr int phase_chunks_per_launch() { return NB >= 8 ? 2 : 4; }
 
 template <int NB>
 __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
@@ -187,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
   for (int k = 0; k < NB; ++k) bp[k] = reinterpret_cast<const f4 *>(b.p[k]);
   const size_t G = gridDim.x;
   const size_t chunk_f4 = G * kPhaseLdsF4;
-  for (int kc = 0; kc < kPhaseChunks; ++kc) {
+  for (int kc = 0; kc < phase_chunks_per_launch<NB>(); ++kc) {
     const size_t lo = (chunk0 + kc) * chunk_f4;
     if (lo >= n4_tiles) return;  // grid-uniform: no block skips a barrier another waits at
     // read phase: sum the chunk's tiles into LDS
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
       f4 acc[U];
       f4 v[NB][U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] = in[base + u * kBlock];
+      for (int u = 0; u < U; ++u) acc[u] = ld_stream(in + base + u * kBlock);
 #pragma unroll
       for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -217,7 +223,8 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
       if (tile0 >= n4_tiles) break;
       const size_t base = tile0 + threadIdx.x;
 #pragma unroll
-      for (int u = 0; u < U; ++u) out[base + u * kBlock] = res[t * kTile + u * kBlock + threadIdx.x];
+      for (int u = 0; u < U; ++u)
+        __builtin_nontemporal_store(res[t * kTile + u * kBlock + threadIdx.x], out + base + u * kBlock);
     }
     __syncthreads();
   }
@@ -245,9 +252,9 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     const size_t n4_tiles = n / 4 / tile * tile;
     const size_t G = (size_t)num_cus() * kPhaseBlocksPerCU;
     const size_t chunk_f4 = G * kPhaseLdsF4;
-    if (n4_tiles >= chunk_f4 * kPhaseChunks) {  // at least one full launch (128 MiB on 256 CUs)
+    if (n4_tiles >= chunk_f4 * kPhaseMinChunks) {
       const size_t chunks = (n4_tiles + chunk_f4 - 1) / chunk_f4;
-      for (size_t c = 0; c < chunks; c += kPhaseChunks)
+      for (size_t c = 0; c < chunks; c += phase_chunks_per_launch<NB>())
         hipLaunchKernelGGL((bucket_sum_phased_kernel<NB>), dim3((unsigned)G), dim3(kBlock), 0, s,
                            reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
                            n4_tiles, c);

@@ -32,7 +32,7 @@ constexpr size_t kN = (1ull << 20) * 1024;  // floats per buffer (4 GiB)
 // One block per CU / BPC per CU; LDS_F4 f4 results per block per chunk.
 // Chunk c covers f4 [c * G * LDS_F4, (c + 1) * G * LDS_F4); inside it, block g
 // takes 16-KiB tiles g, g + G, ... (U = 4 strides of 256 threads).
-template <int NB, int LDS_F4, int K, int BS = kBlock, int U = 4>
+template <int NB, int LDS_F4, int K, int BS = kBlock, int U = 4, int POL = 0>
 __global__ __launch_bounds__(BS) void bsum_phased(f4 *__restrict__ master, BucketPtrs b,
                                                   size_t n4, size_t chunk0) {
   constexpr int kTile = BS * U;                  // f4 per tile
@@ -50,7 +50,8 @@ __global__ __launch_bounds__(BS) void bsum_phased(f4 *__restrict__ master, Bucke
       f4 acc[U];
       f4 v[NB][U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] = master[base + u * BS];
+      for (int u = 0; u < U; ++u)
+        acc[u] = (POL & 1) ? __builtin_nontemporal_load(master + base + u * BS) : master[base + u * BS];
 #pragma unroll
       for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -69,20 +70,25 @@ __global__ __launch_bounds__(BS) void bsum_phased(f4 *__restrict__ master, Bucke
       const size_t base = lo + ((size_t)t * G + blockIdx.x) * kTile + threadIdx.x;
       if (base + (U - 1) * BS >= n4) break;
 #pragma unroll
-      for (int u = 0; u < U; ++u) master[base + u * BS] = res[t * kTile + u * BS + threadIdx.x];
+      for (int u = 0; u < U; ++u) {
+        if (POL & 2)
+          __builtin_nontemporal_store(res[t * kTile + u * BS + threadIdx.x], master + base + u * BS);
+        else
+          master[base + u * BS] = res[t * kTile + u * BS + threadIdx.x];
+      }
     }
     __syncthreads();
   }
 }
 
-template <int NB, int LDS_F4, int K, int BS = kBlock, int U = 4>
+template <int NB, int LDS_F4, int K, int BS = kBlock, int U = 4, int POL = 0>
 void launch_phased(float *m, const BucketPtrs &b, int bpc) {
   const size_t n4 = kN / 4;
   const size_t G = (size_t)num_cus() * bpc;
   const size_t chunk_f4 = G * LDS_F4;
   const size_t chunks = (n4 + chunk_f4 - 1) / chunk_f4;
   for (size_t c = 0; c < chunks; c += K)
-    hipLaunchKernelGGL((bsum_phased<NB, LDS_F4, K, BS, U>), dim3((unsigned)G), dim3(BS), 0, 0,
+    hipLaunchKernelGGL((bsum_phased<NB, LDS_F4, K, BS, U, POL>), dim3((unsigned)G), dim3(BS), 0, 0,
                        reinterpret_cast<f4 *>(m), b, n4, c);
 }
 
@@ -160,19 +166,14 @@ int main(int argc, char **argv) {
       vs.push_back(V{s.name + " NB" + std::to_string(nb) + " " + name, f, {}});
       vbytes.push_back((nb + 2.0) * kN * 4);
     };
-    for (int nb : {2, 4, 8}) {
+    for (int nb : {1, 2, 4, 8}) {
       add("prod", nb, [=]() { gp_bucket_sum_apply(m, bv.data(), nb, kN, nullptr); });
     }
-    add("ph64K k2 bpc2", 2, [=]() { launch_phased<2, 4096, 2>(m, bp, 2); });
-    add("ph64K k4 bpc2", 2, [=]() { launch_phased<2, 4096, 4>(m, bp, 2); });
-    add("ph64K k2 bpc2", 4, [=]() { launch_phased<4, 4096, 2>(m, bp, 2); });
-    add("ph64K k4 bpc2", 4, [=]() { launch_phased<4, 4096, 4>(m, bp, 2); });
-    add("ph64K k1 bpc2", 8, [=]() { launch_phased<8, 4096, 1>(m, bp, 2); });
-    add("ph64K k2 bpc2", 8, [=]() { launch_phased<8, 4096, 2>(m, bp, 2); });
-    add("ph64K k3 bpc2", 8, [=]() { launch_phased<8, 4096, 3>(m, bp, 2); });
-    add("ph64K k4 bpc2", 8, [=]() { launch_phased<8, 4096, 4>(m, bp, 2); });
-    add("ph64K bs512 k2 bpc2", 8, [=]() { launch_phased<8, 4096, 2, 512, 4>(m, bp, 2); });
-    add("ph64K U2 k2 bpc2", 8, [=]() { launch_phased<8, 4096, 2, 256, 2>(m, bp, 2); });
+    add("ph64K k4 ntM ntS", 8, [=]() { launch_phased<8, 4096, 4, 256, 4, 3>(m, bp, 2); });
+    add("ph64K k2 ntM ntS", 8, [=]() { launch_phased<8, 4096, 2, 256, 4, 3>(m, bp, 2); });
+    add("ph64K k4 ntM ntS", 4, [=]() { launch_phased<4, 4096, 4, 256, 4, 3>(m, bp, 2); });
+    add("ph64K k4 ntM ntS", 2, [=]() { launch_phased<2, 4096, 4, 256, 4, 3>(m, bp, 2); });
+    add("ph64K k4 ntM ntS", 1, [=]() { launch_phased<1, 4096, 4, 256, 4, 3>(m, bp, 2); });
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
