@@ -123,6 +123,70 @@ __global__ __launch_bounds__(kBlock) void rows_phased(float *__restrict__ y, con
   }
 }
 
+// Same, with the NEXT chunk's index entries loaded before this chunk's write
+// phase, so each chunk waits for one round trip (the rows), not two.
+template <bool ADD, int K>
+__global__ __launch_bounds__(kBlock) void rows_phased_pf(float *__restrict__ y, const float *__restrict__ x,
+                                                         const gp_double_index *__restrict__ idx,
+                                                         size_t n_rows, size_t chunk0) {
+  constexpr int kVW = 32, kRows = kLdsF4 / kVW;
+  constexpr int kGroups = kBlock / kVW, kRowsPerGroup = kRows / kGroups;
+  __shared__ f4 res[kLdsF4];
+  const int lane = threadIdx.x % kVW, grp = threadIdx.x / kVW;
+  f4 *yv = reinterpret_cast<f4 *>(y);
+  const f4 *xv = reinterpret_cast<const f4 *>(x);
+  const size_t G = gridDim.x;
+  uint64_t src[kRowsPerGroup], dst[kRowsPerGroup];
+  auto load_idx = [&](size_t c) {
+    const size_t lo = (c * G + blockIdx.x) * kRows;
+#pragma unroll
+    for (int i = 0; i < kRowsPerGroup; ++i) {
+      const size_t r = lo + (size_t)i * kGroups + grp;
+      src[i] = dst[i] = ~0ull;
+      if (r < n_rows) {
+        const gp_double_index ix = idx[r];
+        src[i] = ADD ? ix.id0 : ix.id1;
+        dst[i] = ADD ? ix.id1 : ix.id0;
+      }
+    }
+  };
+  if (chunk0 * G * kRows >= n_rows) return;
+  load_idx(chunk0);
+  for (int kc = 0; kc < K; ++kc) {
+    const size_t c = chunk0 + kc;
+    if (c * G * kRows >= n_rows) return;  // grid-uniform
+    f4 xs[kRowsPerGroup], ys[kRowsPerGroup];
+#pragma unroll
+    for (int i = 0; i < kRowsPerGroup; ++i)
+      if (src[i] != ~0ull) xs[i] = xv[src[i] * kVW + lane];
+    if (ADD) {
+#pragma unroll
+      for (int i = 0; i < kRowsPerGroup; ++i)
+        if (dst[i] != ~0ull) ys[i] = yv[dst[i] * kVW + lane];
+    }
+#pragma unroll
+    for (int i = 0; i < kRowsPerGroup; ++i)
+      if (src[i] != ~0ull) res[(i * kGroups + grp) * kVW + lane] = ADD ? ys[i] + xs[i] : xs[i];
+    uint64_t cur_dst[kRowsPerGroup];
+#pragma unroll
+    for (int i = 0; i < kRowsPerGroup; ++i) cur_dst[i] = dst[i];
+    if (kc + 1 < K) load_idx(c + 1);  // prefetch: in flight during the write phase
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kRowsPerGroup; ++i)
+      if (cur_dst[i] != ~0ull) yv[cur_dst[i] * kVW + lane] = res[(i * kGroups + grp) * kVW + lane];
+    __syncthreads();
+  }
+}
+
+template <bool ADD, int K>
+void launch_rows_phased_pf(float *y, const float *x, const gp_double_index *idx, size_t n, int bpc) {
+  const size_t G = (size_t)num_cus() * bpc, chunk = G * (kLdsF4 / 32);
+  const size_t chunks = (n + chunk - 1) / chunk;
+  for (size_t c = 0; c < chunks; c += K)
+    hipLaunchKernelGGL((rows_phased_pf<ADD, K>), dim3((unsigned)G), dim3(kBlock), 0, 0, y, x, idx, n, c);
+}
+
 template <int K>
 void launch_copy_phased(f4 *out, const f4 *in, size_t n4, int bpc) {
   const size_t G = (size_t)num_cus() * bpc, chunk = G * kLdsF4;
@@ -168,9 +232,9 @@ int main(int argc, char **argv) {
     CK(hipMemset(y, 0, bytes));
     CK(hipMemset(y2, 0, bytes));
     gp_gather_rows(y, x, idx, R, {0, 0}, 128, (size_t)-1, nullptr);
-    launch_rows_phased<false, 4>(y2, x, idx, R, 2);
+    launch_rows_phased_pf<false, 8>(y2, x, idx, R, 2);
     gp_scatter_add_rows(y, x, idx, R, {0, 0}, 128, (size_t)-1, nullptr);
-    launch_rows_phased<true, 4>(y2, x, idx, R, 2);
+    launch_rows_phased_pf<true, 8>(y2, x, idx, R, 2);
     CK(hipDeviceSynchronize());
     for (size_t off = 0; off < bytes / 4; off += bytes / 4 / 8) {
       CK(hipMemcpy(a.data(), y + off, a.size() * 4, hipMemcpyDeviceToHost));
@@ -196,9 +260,14 @@ int main(int argc, char **argv) {
   vs.push_back(V{"gather prod", gat_b, [=]() { gp_gather_rows(y, x, idx, R, {0, 0}, 128, (size_t)-1, nullptr); }, {}});
   vs.push_back(V{"gather phased k4 bpc2", gat_b, [=]() { launch_rows_phased<false, 4>(y, x, idx, R, 2); }, {}});
   vs.push_back(V{"gather phased k8 bpc2", gat_b, [=]() { launch_rows_phased<false, 8>(y, x, idx, R, 2); }, {}});
+  vs.push_back(V{"gather phased-pf k8 bpc2", gat_b, [=]() { launch_rows_phased_pf<false, 8>(y, x, idx, R, 2); }, {}});
+  vs.push_back(V{"gather phased-pf k16 bpc2", gat_b, [=]() { launch_rows_phased_pf<false, 16>(y, x, idx, R, 2); }, {}});
+  vs.push_back(V{"gather phased-pf k8 bpc4", gat_b, [=]() { launch_rows_phased_pf<false, 8>(y, x, idx, R, 4); }, {}});
   vs.push_back(V{"add prod", add_b, [=]() { gp_scatter_add_rows(y, x, idx, R, {0, 0}, 128, (size_t)-1, nullptr); }, {}});
   vs.push_back(V{"add phased k4 bpc2", add_b, [=]() { launch_rows_phased<true, 4>(y, x, idx, R, 2); }, {}});
   vs.push_back(V{"add phased k8 bpc2", add_b, [=]() { launch_rows_phased<true, 8>(y, x, idx, R, 2); }, {}});
+  vs.push_back(V{"add phased-pf k8 bpc2", add_b, [=]() { launch_rows_phased_pf<true, 8>(y, x, idx, R, 2); }, {}});
+  vs.push_back(V{"add phased-pf k16 bpc2", add_b, [=]() { launch_rows_phased_pf<true, 16>(y, x, idx, R, 2); }, {}});
 
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
