@@ -45,10 +45,10 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roofline"
 # Launch plan of gp_bucket_sum_apply (geeps_amd/csrc/gp_reduce.hip): shards of at
-# least 4 phase-separated chunks (chunk = 2 blocks/CU x 64 KiB of results) go to
-# bucket_sum_phased_kernel, 2 chunks per launch at 8 buckets and 4 below;
-# smaller ones to bucket_sum_vec_kernel in one launch.
-PHASE_LDS_F4, PHASE_BLOCKS_PER_CU, PHASE_MIN_CHUNKS, TILE_F4 = 4096, 2, 4, 1024
+# least 3 phase-separated chunks (chunk = 1 block/CU x 160 KiB of results) go to
+# bucket_sum_phased_kernel, 2 chunks per launch; smaller ones to
+# bucket_sum_vec_kernel in one launch.
+PHASE_LDS_F4, PHASE_BLOCKS_PER_CU, PHASE_MIN_CHUNKS, TILE_F4 = 10240, 1, 3, 1024
 
 
 def sum_launch_plan(num_vals: int, num_cus: int, num_buckets: int):
@@ -57,7 +57,7 @@ def sum_launch_plan(num_vals: int, num_cus: int, num_buckets: int):
     chunk_f4 = num_cus * PHASE_BLOCKS_PER_CU * PHASE_LDS_F4
     if n4_tiles >= chunk_f4 * PHASE_MIN_CHUNKS:
         chunks = -(-n4_tiles // chunk_f4)
-        per_launch = 2 if num_buckets >= 8 else 4
+        per_launch = 2
         return "bucket_sum_phased_kernel", -(-chunks // per_launch)
     return "bucket_sum_vec_kernel", 1
 

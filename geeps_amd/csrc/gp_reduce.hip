@@ -163,9 +163,13 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
 // chunk's reads are done cut the 8-way sum from 7.25-8.25 ms to 7.17-7.64 ms
 // over the same allocations, and 2- and 4-way sums by 8-10 %.
 //
-// No grid barrier: a launch covers K chunks, and its blocks stay roughly in
+// No grid barrier: a launch covers 2 chunks, and its blocks stay roughly in
 // phase because they do identical work and start together (a launch boundary
-// re-aligns them).  K = 2 for 8 buckets and 4 below measured best of 1-4.
+// re-aligns them).  Each block holds 160 KiB of results -- the CU's whole LDS
+// -- at one block per CU, so a chunk is 40 MiB on 256 CUs.  Against 64 KiB at
+// 2 blocks per CU that measured 6.66-6.73 vs 7.09 ms at 8 buckets and 3-4 %
+// faster at 1, 2 and 4 (profiles/r01b/phase_tune_lds160.txt): fewer, longer
+// phases switch HBM between reading and writing less often.
 // Every access is non-temporal here (master loads and stores too, unlike the
 // mixed form): +1.5-3 % at 1-8 buckets over plain master accesses, which
 // otherwise linger in the caches and drain to HBM during the next read phase.
@@ -173,12 +177,12 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
 // 16-KiB tiles g, g + G, ...  Only whole tiles: the caller passes
 // n4_tiles, a multiple of kBlock * 4, and sums any rest with the mixed form.
 // The order of the adds per element is the bucket order, as in every form.
-constexpr int kPhaseLdsF4 = 4096;  // 64 KiB of results per block, 2 blocks per CU
-constexpr int kPhaseBlocksPerCU = 2;
-constexpr int kPhaseMinChunks = 4;  // shards below 4 chunks (128 MiB on 256 CUs): mixed form
+constexpr int kPhaseLdsF4 = 10240;  // 160 KiB of results per block, 1 block per CU
+constexpr int kPhaseBlocksPerCU = 1;
+constexpr int kPhaseMinChunks = 3;  // shards below 3 chunks (120 MiB on 256 CUs): mixed form
 
 template <int NB>
-constexpr int phase_chunks_per_launch() { return NB >= 8 ? 2 : 4; }
+constexpr int phase_chunks_per_launch() { return 2; }
 
 template <int NB>
 __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(

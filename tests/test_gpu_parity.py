@@ -144,11 +144,11 @@ def test_bucket_sum_into_leaves_master(dev, N):
 
 @pytest.mark.parametrize("N,out_of_place", [(1, False), (3, False), (8, False), (8, True), (11, True)])
 def test_bucket_sum_phase_separated_path(dev, N, out_of_place):
-    """Shards of >= 128 MiB take the phase-separated kernel (reads summed into LDS
-    per chunk, then written) over their whole 16-KiB tiles; the rest goes to the
-    mixed and scalar forms.  This size gives 4 full chunks + a partial one (two
-    launches), 3 leftover tiles' worth of dwordx4 plus a 7-float scalar tail:
-    every element checked bit for bit."""
+    """Shards of >= 3 chunks (120 MiB on 256 CUs) take the phase-separated kernel
+    (reads summed into LDS per chunk, then written) over their whole 16-KiB
+    tiles; the rest goes to the mixed and scalar forms.  This size gives 3 full
+    40-MiB chunks + a partial one (two launches of 2 chunks), one dwordx4 for
+    the mixed form and a 3-float scalar tail: every element checked bit for bit."""
     from geeps_amd import rowops
     n = (32 << 20) + 1024 * 4 * 3 + 7
     ups = [oracle.synthetic_delta(300 + c, n) for c in range(N)]
