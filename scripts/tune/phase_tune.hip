@@ -169,15 +169,15 @@ int main(int argc, char **argv) {
     for (int nb : {1, 2, 4, 8}) {
       add("prod", nb, [=]() { gp_bucket_sum_apply(m, bv.data(), nb, kN, nullptr); });
     }
-    add("ph160K k1 U4 nt", 8, [=]() { launch_phased<8, 10240, 1, 256, 4, 3>(m, bp, 1); });
-    add("ph160K k2 U4 nt", 8, [=]() { launch_phased<8, 10240, 2, 256, 4, 3>(m, bp, 1); });
-    add("ph160K k3 U4 nt", 8, [=]() { launch_phased<8, 10240, 3, 256, 4, 3>(m, bp, 1); });
-    add("ph160K k4 U4 nt", 8, [=]() { launch_phased<8, 10240, 4, 256, 4, 3>(m, bp, 1); });
-    add("ph160K k2 B512 U2 nt", 8, [=]() { launch_phased<8, 10240, 2, 512, 2, 3>(m, bp, 1); });
-    add("ph160K k2 B512 U4 nt", 8, [=]() { launch_phased<8, 10240, 2, 512, 4, 3>(m, bp, 1); });
-    add("ph160K k4 U4 nt", 4, [=]() { launch_phased<4, 10240, 4, 256, 4, 3>(m, bp, 1); });
-    add("ph160K k4 U4 nt", 2, [=]() { launch_phased<2, 10240, 4, 256, 4, 3>(m, bp, 1); });
-    add("ph160K k4 U4 nt", 1, [=]() { launch_phased<1, 10240, 4, 256, 4, 3>(m, bp, 1); });
+    add("ph160K k1 B512 U2", 8, [=]() { launch_phased<8, 10240, 1, 512, 2, 3>(m, bp, 1); });
+    add("ph160K k2 B512 U2", 8, [=]() { launch_phased<8, 10240, 2, 512, 2, 3>(m, bp, 1); });
+    add("ph160K k2 B512 U1", 8, [=]() { launch_phased<8, 10240, 2, 512, 1, 3>(m, bp, 1); });
+    add("ph160K k2 B1024 U1", 8, [=]() { launch_phased<8, 10240, 2, 1024, 1, 3>(m, bp, 1); });
+    add("ph160K k2 B1024 U2", 8, [=]() { launch_phased<8, 10240, 2, 1024, 2, 3>(m, bp, 1); });
+    add("ph160K k2 B512 U2", 4, [=]() { launch_phased<4, 10240, 2, 512, 2, 3>(m, bp, 1); });
+    add("ph160K k2 B512 U2", 2, [=]() { launch_phased<2, 10240, 2, 512, 2, 3>(m, bp, 1); });
+    add("ph160K k2 B512 U2", 1, [=]() { launch_phased<1, 10240, 2, 512, 2, 3>(m, bp, 1); });
+    add("ph160K k2 B1024 U1", 2, [=]() { launch_phased<2, 10240, 2, 1024, 1, 3>(m, bp, 1); });
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
