@@ -11,8 +11,9 @@ hosted on rank c % N; its delta buffer is uniform in [-0.5, 0.5) (seed 1000+c).
 A *step* is one device-resident N-way reduction: each shard adds the 8 client
 buckets for its rows into its master copy in client order 0..7 with one
 gp_bucket_sum_apply call (the reference's TabletStorage::apply_updates x 8,
-src/server/tablet-server.cpp:119-134); for a 4 GiB shard that call issues 64
-launches of the phase-separated kernel, each summing 64 MiB of the shard.  At N > 1 the buckets were first moved
+src/server/tablet-server.cpp:119-134); for a 4 GiB shard that call issues 74
+launches of the phase-separated kernel, each summing a 56-MiB chunk of the
+shard (gp_bucket_sum_plan gives the count).  At N > 1 the buckets were first moved
 to their shard by RCCL all-to-all (untimed here; the exchange-inclusive step
 exchange + apply + all-gather refresh is timed separately and reported as
 `exchange_inclusive`).  Total work is fixed as N grows: scaling "strong".
@@ -44,22 +45,19 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roofline"
-# Launch plan of gp_bucket_sum_apply (geeps_amd/csrc/gp_reduce.hip): shards of at
-# least 3 phase-separated chunks (chunk = 1 block/CU x 160 KiB of results) go to
-# bucket_sum_phased_kernel, 2 chunks per launch; smaller ones to
-# bucket_sum_vec_kernel in one launch.
-PHASE_LDS_F4, PHASE_BLOCKS_PER_CU, PHASE_MIN_CHUNKS, TILE_F4 = 10240, 1, 3, 1024
-
-
-def sum_launch_plan(num_vals: int, num_cus: int, num_buckets: int):
-    """(dominant kernel name, its launches per step) for one N-way sum of num_vals floats."""
-    n4_tiles = num_vals // 4 // TILE_F4 * TILE_F4
-    chunk_f4 = num_cus * PHASE_BLOCKS_PER_CU * PHASE_LDS_F4
-    if n4_tiles >= chunk_f4 * PHASE_MIN_CHUNKS:
-        chunks = -(-n4_tiles // chunk_f4)
-        per_launch = 2
-        return "bucket_sum_phased_kernel", -(-chunks // per_launch)
-    return "bucket_sum_vec_kernel", 1
+def sum_launch_plan(num_vals: int, num_buckets: int):
+    """(dominant kernel name, its launches per step, register tiles) for one
+    N-way sum of num_vals floats, from the library's own launch plan
+    (gp_bucket_sum_plan): shards of at least 3 phase-separated chunks go to
+    bucket_sum_phased_kernel, smaller ones to bucket_sum_vec_kernel in one launch."""
+    import ctypes
+    from geeps_amd import native
+    launches, reg_tiles = ctypes.c_int(0), ctypes.c_int(0)
+    native.check(native.lib().gp_bucket_sum_plan(num_vals, num_buckets, ctypes.byref(launches),
+                                                 ctypes.byref(reg_tiles)), "gp_bucket_sum_plan")
+    if launches.value > 0:
+        return "bucket_sum_phased_kernel", launches.value, reg_tiles.value
+    return "bucket_sum_vec_kernel", 1, None
 
 
 def log(*a):
@@ -370,8 +368,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
     wall = max_over_ranks(wall, world, dev)
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     avg_kernel_ms_max = max_over_ranks(avg_kernel_ms, world, dev)
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
-    kernel_name, launches = sum_launch_plan(L.local_vals, cus, min(C, 8))
+    kernel_name, launches, reg_tiles = sum_launch_plan(L.local_vals, min(C, 8))
     step_s = wall / args.steps
     delta_bytes = C * R * W * 4
     value = delta_bytes / step_s / 1e9
@@ -452,6 +449,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
                          "traffic": traffic,
                          "kernel": kernel_name,
                          "launches_per_step": launches,
+                         "register_tiles": reg_tiles,
                          # HIP events around each step's launches on their stream
                          "avg_kernel_ms": round(avg_kernel_ms_max, 4),
                          # per launch, comparable with rocprofv3's average for the kernel

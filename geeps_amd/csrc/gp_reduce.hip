@@ -163,47 +163,62 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
 // chunk's reads are done cut the 8-way sum from 7.25-8.25 ms to 7.17-7.64 ms
 // over the same allocations, and 2- and 4-way sums by 8-10 %.
 //
-// No grid barrier: a launch covers 2 chunks, and its blocks stay roughly in
+// No grid barrier: a launch covers K chunks, and its blocks stay roughly in
 // phase because they do identical work and start together (a launch boundary
-// re-aligns them).  Each block holds 160 KiB of results -- the CU's whole LDS
-// -- at one block per CU, so a chunk is 40 MiB on 256 CUs.  Against 64 KiB at
-// 2 blocks per CU that measured 6.66-6.73 vs 7.09 ms at 8 buckets and 3-4 %
-// faster at 1, 2 and 4 (profiles/r01b/phase_tune_lds160.txt): fewer, longer
-// phases switch HBM between reading and writing less often.
+// re-aligns them).  Each block holds 160 KiB of results in LDS -- the CU's
+// whole LDS -- at one block per CU.  Against 64 KiB at 2 blocks per CU that
+// measured 6.66-6.73 vs 7.09 ms at 8 buckets and 3-4 % faster at 1, 2 and 4
+// (profiles/r01b/phase_tune_lds160.txt).  RT more 16-KiB tiles per block are
+// held in registers (VGPRs, spilling into AGPRs, never scratch: one wave per
+// SIMD has the register file to itself), which lengthens both phases.  That
+// pays with few buckets and not with many, whose read phase needs the
+// registers for its (NB + 1) * 4 loads in flight (profiles/r01b/
+// phase_tune_reg.txt): RT = 20 at 1-2 buckets (-2-3 %), 12 at 3-4 (-1-2 %),
+// 4 at 5-8 (-0.5 %).  K = 1 with register tiles, 2 without.
 // Every access is non-temporal here (master loads and stores too, unlike the
 // mixed form): +1.5-3 % at 1-8 buckets over plain master accesses, which
 // otherwise linger in the caches and drain to HBM during the next read phase.
-// Chunk c of a launch covers f4 [lo, lo + G * kPhaseLdsF4); block g takes its
-// 16-KiB tiles g, g + G, ...  Only whole tiles: the caller passes
-// n4_tiles, a multiple of kBlock * 4, and sums any rest with the mixed form.
-// The order of the adds per element is the bucket order, as in every form.
+// Chunk c covers tiles [c * G * kT, (c + 1) * G * kT) of kTile f4 each, kT =
+// kLdsTiles + RT; block g takes tiles g, g + G, ...  Only whole tiles: the
+// caller passes n4_tiles, a multiple of kTile, and sums any rest with the
+// mixed form.  The order of the adds per element is the bucket order, as in
+// every form.
 constexpr int kPhaseLdsF4 = 10240;  // 160 KiB of results per block, 1 block per CU
-constexpr int kPhaseBlocksPerCU = 1;
-constexpr int kPhaseMinChunks = 3;  // shards below 3 chunks (120 MiB on 256 CUs): mixed form
+constexpr int kPhaseU = 4;          // block-strides per tile
+constexpr int kPhaseTile = kBlock * kPhaseU;  // f4 per tile (16 KiB)
+constexpr int kPhaseLdsTiles = kPhaseLdsF4 / kPhaseTile;
+constexpr int kPhaseMinChunks = 3;  // shards below 3 chunks: a shorter chunk form, or mixed
 
 template <int NB>
-constexpr int phase_chunks_per_launch() { return 2; }
+constexpr int phase_reg_tiles() { return NB <= 2 ? 20 : NB <= 4 ? 12 : 4; }
 
-template <int NB>
+constexpr int phase_chunks_per_launch(int rt) { return rt > 0 ? 1 : 2; }
+
+inline size_t phase_chunk_f4(int rt) {
+  return (size_t)num_cus() * (size_t)(kPhaseLdsTiles + rt) * kPhaseTile;
+}
+
+template <int NB, int RT>
 __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
     size_t chunk0) {
-  constexpr int U = 4;
-  constexpr int kTile = kBlock * U;
-  constexpr int kTilesPerBlock = kPhaseLdsF4 / kTile;
+  constexpr int U = kPhaseU;
+  constexpr int kT = kPhaseLdsTiles + RT;
   __shared__ f4 res[kPhaseLdsF4];
+  f4 keep[RT > 0 ? RT : 1][U];
   const f4 *bp[NB];
 #pragma unroll
   for (int k = 0; k < NB; ++k) bp[k] = reinterpret_cast<const f4 *>(b.p[k]);
   const size_t G = gridDim.x;
-  const size_t chunk_f4 = G * kPhaseLdsF4;
-  for (int kc = 0; kc < phase_chunks_per_launch<NB>(); ++kc) {
+  const size_t chunk_f4 = G * (size_t)kT * kPhaseTile;
+  for (int kc = 0; kc < phase_chunks_per_launch(RT); ++kc) {
     const size_t lo = (chunk0 + kc) * chunk_f4;
     if (lo >= n4_tiles) return;  // grid-uniform: no block skips a barrier another waits at
-    // read phase: sum the chunk's tiles into LDS
-    for (int t = 0; t < kTilesPerBlock; ++t) {
-      const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kTile;
-      if (tile0 >= n4_tiles) break;  // block-uniform
+    // read phase: sum the chunk's tiles into LDS (t < kPhaseLdsTiles) and registers
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+      const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kPhaseTile;
+      if (tile0 >= n4_tiles) break;  // block-uniform; later tiles are further out
       const size_t base = tile0 + threadIdx.x;
       f4 acc[U];
       f4 v[NB][U];
@@ -217,21 +232,57 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
       for (int u = 0; u < U; ++u) {
 #pragma unroll
         for (int k = 0; k < NB; ++k) acc[u] += v[k][u];  // bucket order 0..NB-1
-        res[t * kTile + u * kBlock + threadIdx.x] = acc[u];
+        if (t < kPhaseLdsTiles)
+          res[t * kPhaseTile + u * kBlock + threadIdx.x] = acc[u];
+        else
+          keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u] = acc[u];
       }
     }
     __syncthreads();
     // write phase
-    for (int t = 0; t < kTilesPerBlock; ++t) {
-      const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kTile;
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+      const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kPhaseTile;
       if (tile0 >= n4_tiles) break;
       const size_t base = tile0 + threadIdx.x;
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        __builtin_nontemporal_store(res[t * kTile + u * kBlock + threadIdx.x], out + base + u * kBlock);
+        __builtin_nontemporal_store(t < kPhaseLdsTiles
+                                        ? res[t * kPhaseTile + u * kBlock + threadIdx.x]
+                                        : keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u],
+                                    out + base + u * kBlock);
     }
     __syncthreads();
   }
+}
+
+// Which phase-separated form sums a shard of n4_tiles whole tiles: the
+// register-extended one when the shard holds kPhaseMinChunks of its chunks,
+// else the LDS-only one on the same rule, else none (-1: the mixed form).
+template <int NB>
+int phase_form(size_t n4_tiles) {
+  if (n4_tiles >= phase_chunk_f4(phase_reg_tiles<NB>()) * kPhaseMinChunks)
+    return phase_reg_tiles<NB>();
+  if (n4_tiles >= phase_chunk_f4(0) * kPhaseMinChunks) return 0;
+  return -1;
+}
+
+inline size_t phase_launches(size_t n4_tiles, int rt) {
+  const size_t chunk_f4 = phase_chunk_f4(rt);
+  const size_t chunks = (n4_tiles + chunk_f4 - 1) / chunk_f4;
+  const size_t k = (size_t)phase_chunks_per_launch(rt);
+  return (chunks + k - 1) / k;
+}
+
+template <int NB, int RT>
+void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_tiles,
+                   hipStream_t s) {
+  const size_t G = (size_t)num_cus();
+  const size_t launches = phase_launches(n4_tiles, RT);
+  for (size_t l = 0; l < launches; ++l)
+    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT>), dim3((unsigned)G), dim3(kBlock), 0, s,
+                       reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
+                       n4_tiles, l * (size_t)phase_chunks_per_launch(RT));
 }
 
 // Buckets advanced by `off` floats.
@@ -252,16 +303,13 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
   size_t done = 0;  // floats summed so far
   if (vec) {
-    const size_t tile = (size_t)kBlock * 4;
-    const size_t n4_tiles = n / 4 / tile * tile;
-    const size_t G = (size_t)num_cus() * kPhaseBlocksPerCU;
-    const size_t chunk_f4 = G * kPhaseLdsF4;
-    if (n4_tiles >= chunk_f4 * kPhaseMinChunks) {
-      const size_t chunks = (n4_tiles + chunk_f4 - 1) / chunk_f4;
-      for (size_t c = 0; c < chunks; c += phase_chunks_per_launch<NB>())
-        hipLaunchKernelGGL((bucket_sum_phased_kernel<NB>), dim3((unsigned)G), dim3(kBlock), 0, s,
-                           reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
-                           n4_tiles, c);
+    const size_t n4_tiles = n / 4 / kPhaseTile * kPhaseTile;
+    const int rt = phase_form<NB>(n4_tiles);
+    if (rt > 0) {
+      launch_phased<NB, phase_reg_tiles<NB>()>(out, in, b, n4_tiles, s);
+      done = n4_tiles * 4;
+    } else if (rt == 0) {
+      launch_phased<NB, 0>(out, in, b, n4_tiles, s);
       done = n4_tiles * 4;
     }
   }
@@ -289,6 +337,16 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   }
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;
+}
+
+// Launch plan of one pass of nb buckets over n 16-B-aligned floats (bench.py
+// prices the phased kernel per launch with it).
+template <int NB>
+void bucket_sum_plan_nb(size_t n, int *launches, int *reg_tiles) {
+  const size_t n4_tiles = n / 4 / kPhaseTile * kPhaseTile;
+  const int rt = phase_form<NB>(n4_tiles);
+  *reg_tiles = rt;
+  *launches = rt < 0 ? 0 : (int)phase_launches(n4_tiles, rt);
 }
 
 int launch_bucket_sum(float *out, const float *in, const float *const *bk,
@@ -666,6 +724,23 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
                                   size_t num_vals_limit, gp_stream s) {
   return launch_row_op_seg<kAddFrom, kSegY>(const_cast<float *>(x), y_segments, index, num_rows,
                                             offset, row_size, num_vals_limit, (hipStream_t)s);
+}
+
+int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
+                       int *reg_tiles) {
+  if (!phased_launches || !reg_tiles) return set_error(GP_ERR_INVALID, "null pointer");
+  switch (num_buckets) {
+    case 1: bucket_sum_plan_nb<1>(num_vals, phased_launches, reg_tiles); break;
+    case 2: bucket_sum_plan_nb<2>(num_vals, phased_launches, reg_tiles); break;
+    case 3: bucket_sum_plan_nb<3>(num_vals, phased_launches, reg_tiles); break;
+    case 4: bucket_sum_plan_nb<4>(num_vals, phased_launches, reg_tiles); break;
+    case 5: bucket_sum_plan_nb<5>(num_vals, phased_launches, reg_tiles); break;
+    case 6: bucket_sum_plan_nb<6>(num_vals, phased_launches, reg_tiles); break;
+    case 7: bucket_sum_plan_nb<7>(num_vals, phased_launches, reg_tiles); break;
+    case 8: bucket_sum_plan_nb<8>(num_vals, phased_launches, reg_tiles); break;
+    default: return set_error(GP_ERR_INVALID, "bucket count out of range");
+  }
+  return GP_OK;
 }
 
 int gp_bucket_sum_apply(float *master, const float *const *buckets,

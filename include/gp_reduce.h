@@ -40,7 +40,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 3
+#define GP_ABI_VERSION 4
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -179,6 +179,16 @@ int gp_bucket_sum_apply(float *master, const float *const *buckets,
  * num_buckets == 0 copies `in` to `out`. */
 int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
                        int num_buckets, size_t num_vals, gp_stream s);
+
+/* Launch plan of ONE pass of gp_bucket_sum_apply / _into with num_buckets
+ * (1..8) over num_vals floats in 16-B-aligned buffers; launches nothing.
+ * *phased_launches = launches of the phase-separated kernel (0 when the shard
+ * is too small for it and the mixed form sums it in one launch);
+ * *reg_tiles = 16-KiB tiles per block held in registers by that form (0: LDS
+ * only; -1: not phased).  For measurement tools: bench.py prices the phased
+ * kernel per launch with it, as rocprofv3 reports it. */
+int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
+                       int *reg_tiles);
 
 /* y[i] = a[i] + b[i] — device form of cpu_add / vsAdd
  * (src/common/gpu-util/math_functions.hpp:60-61, mkl_alternate.hpp:59-74).

@@ -92,6 +92,72 @@ void launch_phased(float *m, const BucketPtrs &b, int bpc) {
                        reinterpret_cast<f4 *>(m), b, n4, c);
 }
 
+// Register-extended chunks: besides LDS_F4 f4 of results in LDS, each lane
+// keeps RT more tiles' results in VGPRs (1 wave per SIMD leaves ~300 VGPRs
+// for them), so a chunk per CU is (LDS_F4 / kTile + RT) tiles and the read and
+// write phases are that much longer.
+template <int NB, int LDS_F4, int RT, int K, int U = 4>
+__global__ __launch_bounds__(kBlock) void bsum_phased_reg(f4 *__restrict__ master, BucketPtrs b,
+                                                         size_t n4, size_t chunk0) {
+  constexpr int BS = kBlock;
+  constexpr int kTile = BS * U;
+  constexpr int kLT = LDS_F4 / kTile;
+  constexpr int kT = kLT + RT;  // tiles per block per chunk
+  __shared__ f4 res[LDS_F4];
+  const size_t G = gridDim.x;
+  const size_t chunk_f4 = G * (size_t)kT * kTile;
+  f4 keep[RT > 0 ? RT : 1][U];
+  for (int kc = 0; kc < K; ++kc) {
+    const size_t lo = (chunk0 + kc) * chunk_f4;
+    if (lo >= n4) return;  // grid-uniform
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+      const size_t base = lo + ((size_t)t * G + blockIdx.x) * kTile + threadIdx.x;
+      const bool live = base + (U - 1) * BS < n4;
+      f4 acc[U];
+      f4 v[NB][U];
+      if (live) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = __builtin_nontemporal_load(master + base + u * BS);
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            v[k][u] = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(b.p[k]) + base + u * BS);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int k = 0; k < NB; ++k) acc[u] += v[k][u];
+          if (t < kLT) res[t * kTile + u * BS + threadIdx.x] = acc[u];
+          else keep[t >= kLT ? t - kLT : 0][u] = acc[u];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+      const size_t base = lo + ((size_t)t * G + blockIdx.x) * kTile + threadIdx.x;
+      if (base + (U - 1) * BS >= n4) continue;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        __builtin_nontemporal_store(t < kLT ? res[t * kTile + u * BS + threadIdx.x] : keep[t >= kLT ? t - kLT : 0][u],
+                                    master + base + u * BS);
+    }
+    __syncthreads();
+  }
+}
+
+template <int NB, int LDS_F4, int RT, int K, int U = 4>
+void launch_phased_reg(float *m, const BucketPtrs &b) {
+  const size_t n4 = kN / 4;
+  const size_t G = (size_t)num_cus();
+  const size_t chunk_f4 = G * (size_t)(LDS_F4 / (kBlock * U) + RT) * kBlock * U;
+  const size_t chunks = (n4 + chunk_f4 - 1) / chunk_f4;
+  for (size_t c = 0; c < chunks; c += K)
+    hipLaunchKernelGGL((bsum_phased_reg<NB, LDS_F4, RT, K, U>), dim3((unsigned)G), dim3(kBlock), 0, 0,
+                       reinterpret_cast<f4 *>(m), b, n4, c);
+}
+
 __global__ void fill_k(float *p, size_t n, unsigned seed) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -148,6 +214,18 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(h2.data(), m2 + kN - h2.size(), h2.size() * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < h1.size(); ++i) bad += std::memcmp(&h1[i], &h2[i], 4) != 0;
     std::printf("phased vs production, sampled 9 Mi floats: %zu mismatches\n", bad);
+    // register-extended form: full compare against production on fresh copies
+    CK(hipMemcpy(m2, s.master, kN * 4, hipMemcpyDeviceToDevice));
+    gp_bucket_sum_apply(s.master, bv.data(), 8, kN, nullptr);
+    launch_phased_reg<8, 10240, 12, 1>(m2, s.b);
+    CK(hipDeviceSynchronize());
+    size_t bad2 = 0;
+    for (size_t off = 0; off < kN; off += h1.size()) {
+      CK(hipMemcpy(h1.data(), s.master + off, h1.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2.data(), m2 + off, h2.size() * 4, hipMemcpyDeviceToHost));
+      bad2 += std::memcmp(h1.data(), h2.data(), h1.size() * 4) != 0;
+    }
+    std::printf("register-extended phased vs production, all floats: %zu mismatching 4-MiB blocks\n", bad2);
     CK(hipFree(m2));
   }
 
@@ -169,15 +247,10 @@ int main(int argc, char **argv) {
     for (int nb : {1, 2, 4, 8}) {
       add("prod", nb, [=]() { gp_bucket_sum_apply(m, bv.data(), nb, kN, nullptr); });
     }
-    add("ph160K k1 B512 U2", 8, [=]() { launch_phased<8, 10240, 1, 512, 2, 3>(m, bp, 1); });
-    add("ph160K k2 B512 U2", 8, [=]() { launch_phased<8, 10240, 2, 512, 2, 3>(m, bp, 1); });
-    add("ph160K k2 B512 U1", 8, [=]() { launch_phased<8, 10240, 2, 512, 1, 3>(m, bp, 1); });
-    add("ph160K k2 B1024 U1", 8, [=]() { launch_phased<8, 10240, 2, 1024, 1, 3>(m, bp, 1); });
-    add("ph160K k2 B1024 U2", 8, [=]() { launch_phased<8, 10240, 2, 1024, 2, 3>(m, bp, 1); });
-    add("ph160K k2 B512 U2", 4, [=]() { launch_phased<4, 10240, 2, 512, 2, 3>(m, bp, 1); });
-    add("ph160K k2 B512 U2", 2, [=]() { launch_phased<2, 10240, 2, 512, 2, 3>(m, bp, 1); });
-    add("ph160K k2 B512 U2", 1, [=]() { launch_phased<1, 10240, 2, 512, 2, 3>(m, bp, 1); });
-    add("ph160K k2 B1024 U1", 2, [=]() { launch_phased<2, 10240, 2, 1024, 1, 3>(m, bp, 1); });
+    add("LDS-only k2 (previous prod)", 8, [=]() { launch_phased_reg<8, 10240, 0, 2>(m, bp); });
+    add("LDS-only k2 (previous prod)", 4, [=]() { launch_phased_reg<4, 10240, 0, 2>(m, bp); });
+    add("LDS-only k2 (previous prod)", 2, [=]() { launch_phased_reg<2, 10240, 0, 2>(m, bp); });
+    add("LDS-only k2 (previous prod)", 1, [=]() { launch_phased_reg<1, 10240, 0, 2>(m, bp); });
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));

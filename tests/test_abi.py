@@ -12,7 +12,7 @@ from geeps_amd import native
 def test_header_declares_expected_entry_points():
     syms = native.declared_symbols()
     for s in ("gp_scatter_add_rows", "gp_gather_rows", "gp_scatter_rows",
-              "gp_bucket_sum_apply", "gp_bucket_sum_into", "gp_add", "gp_zero",
+              "gp_bucket_sum_apply", "gp_bucket_sum_into", "gp_bucket_sum_plan", "gp_add", "gp_zero",
               "gp_last_error"):
         assert s in syms
     # every declared symbol has a ctypes signature and vice versa
@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 3
+    assert L.gp_abi_version() == native.ABI_VERSION == 4
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -111,3 +111,26 @@ def test_product_does_not_import_oracle():
             assert "oracle_" not in out
             deps = subprocess.run(["readelf", "-d", p], capture_output=True, text=True).stdout
             assert "liboracle" not in deps
+
+
+def test_bucket_sum_plan_without_device():
+    """gp_bucket_sum_plan launches nothing.  Without a device the library
+    assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 40 MiB
+    (LDS only), 56 / 88 / 120 MiB with 4 / 12 / 20 register tiles."""
+    L = native.lib()
+    launches, rt = ctypes.c_int(-5), ctypes.c_int(-5)
+
+    def plan(n, nb):
+        assert L.gp_bucket_sum_plan(n, nb, ctypes.byref(launches), ctypes.byref(rt)) == 0
+        return launches.value, rt.value
+
+    assert plan(1 << 30, 8) == (74, 4)      # the 4 GiB headline shard: 73.1 chunks, 1 per launch
+    assert plan(1 << 30, 2) == (35, 20)
+    assert plan(1 << 30, 4) == (47, 12)
+    assert plan(1 << 27, 8) == (10, 4)      # the 8-GPU shard (512 MiB)
+    assert plan(3 * 10 * 1024 * 1024, 8) == (2, 0)  # 120 MiB: 3 LDS-only chunks, 2 per launch
+    assert plan(3 * 10 * 1024 * 1024 - 4096, 8) == (0, -1)  # below: the mixed form
+    assert plan(0, 1) == (0, -1)
+    assert L.gp_bucket_sum_plan(16, 9, ctypes.byref(launches), ctypes.byref(rt)) == 1
+    assert L.gp_bucket_sum_plan(16, 0, ctypes.byref(launches), ctypes.byref(rt)) == 1
+    assert L.gp_bucket_sum_plan(16, 1, None, None) == 1

@@ -169,6 +169,47 @@ def test_bucket_sum_phase_separated_path(dev, N, out_of_place):
     assert np.array_equal(bits(out.cpu().numpy()), bits(e))
 
 
+@pytest.fixture(scope="module")
+def large_deltas():
+    """8 client buckets of 100 Mi + 20,483 floats (400 MiB each), made once."""
+    n = (100 << 20) + 1024 * 4 * 5 + 3
+    return n, [oracle.synthetic_delta(500 + c, n) for c in range(8)]
+
+
+@pytest.mark.parametrize("N,out_of_place", [(1, False), (2, True), (3, False), (4, False),
+                                            (5, True), (8, False)])
+def test_bucket_sum_register_tiles_path(dev, large_deltas, N, out_of_place):
+    """400-MiB shards take the register-extended phased form at every bucket
+    count (tiles held in registers beside the LDS ones: 20 at 1-2 buckets,
+    12 at 3-4, 4 at 5-8; chunks of 120 / 88 / 56 MiB, the last one partial),
+    then one dwordx4 for the mixed form and a 3-float scalar tail: every
+    element checked bit for bit, and the plan the library reports is that form."""
+    import ctypes
+    from geeps_amd import native, rowops
+    n, allups = large_deltas
+    launches, rt = ctypes.c_int(0), ctypes.c_int(0)
+    native.check(native.lib().gp_bucket_sum_plan(n, N, ctypes.byref(launches), ctypes.byref(rt)))
+    assert rt.value == (20 if N <= 2 else 12 if N <= 4 else 4) and launches.value >= 3
+    ups = allups[:N]
+    m0 = np.random.default_rng(N).standard_normal(n).astype(np.float32)
+    e = m0.copy()
+    oracle.apply_updates(e, ups)
+    m = T(m0, dev)
+    tb = [T(u, dev) for u in ups]
+    if out_of_place:
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+        rowops.bucket_sum_into(out, m, tb)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(m.cpu().numpy()), bits(m0))
+    else:
+        rowops.bucket_sum_apply(m, tb)
+        out = m
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()), bits(e))
+    del tb, m, out
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 255, 256, 257, 1023, 1024 * 256 + 3])
 def test_bucket_sum_sizes_and_alignment(dev, n):
     from geeps_amd import rowops
