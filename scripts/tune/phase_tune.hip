@@ -247,10 +247,13 @@ int main(int argc, char **argv) {
     for (int nb : {1, 2, 4, 8}) {
       add("prod", nb, [=]() { gp_bucket_sum_apply(m, bv.data(), nb, kN, nullptr); });
     }
-    add("LDS-only k2 (previous prod)", 8, [=]() { launch_phased_reg<8, 10240, 0, 2>(m, bp); });
-    add("LDS-only k2 (previous prod)", 4, [=]() { launch_phased_reg<4, 10240, 0, 2>(m, bp); });
-    add("LDS-only k2 (previous prod)", 2, [=]() { launch_phased_reg<2, 10240, 0, 2>(m, bp); });
-    add("LDS-only k2 (previous prod)", 1, [=]() { launch_phased_reg<1, 10240, 0, 2>(m, bp); });
+    add("reg R4 k2", 8, [=]() { launch_phased_reg<8, 10240, 4, 2>(m, bp); });
+    add("reg R4 k3", 8, [=]() { launch_phased_reg<8, 10240, 4, 3>(m, bp); });
+    add("reg R2 k1", 8, [=]() { launch_phased_reg<8, 10240, 2, 1>(m, bp); });
+    add("reg R6 k1", 8, [=]() { launch_phased_reg<8, 10240, 6, 1>(m, bp); });
+    add("reg R20 k2", 2, [=]() { launch_phased_reg<2, 10240, 20, 2>(m, bp); });
+    add("reg R28 k1", 2, [=]() { launch_phased_reg<2, 10240, 28, 1>(m, bp); });
+    add("reg R16 k1", 4, [=]() { launch_phased_reg<4, 10240, 16, 1>(m, bp); });
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
