@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
 // chunk's reads are done cut the 8-way sum from 7.25-8.25 ms to 7.17-7.64 ms
 // over the same allocations, and 2- and 4-way sums by 8-10 %.
 //
-// No grid barrier: a launch covers K chunks, and its blocks stay roughly in
+// No grid barrier: a launch covers one chunk, and its blocks stay roughly in
 // phase because they do identical work and start together (a launch boundary
 // re-aligns them).  Each block holds 160 KiB of results in LDS -- the CU's
 // whole LDS -- at one block per CU.  Against 64 KiB at 2 blocks per CU that
@@ -173,52 +173,85 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
 // SIMD has the register file to itself), which lengthens both phases.  That
 // pays with few buckets and not with many, whose read phase needs the
 // registers for its (NB + 1) * 4 loads in flight (profiles/r01b/
-// phase_tune_reg.txt): RT = 20 at 1-2 buckets (-2-3 %), 12 at 3-4 (-1-2 %),
-// 4 at 5-8 (-0.5 %).  K = 1 with register tiles, 2 without.
+// phase_tune_reg.txt): RT = 20 at 1-2 buckets (-2-5 %), 12 at 3-4 (-1-2 %),
+// 4 at 5-8 (-1-2 %), against LDS-only chunks 2 per launch.
+// Shards of fewer than 3 such chunks are split into C <= 3 balanced chunks
+// of T <= 10 + RT tiles per block (at least one), so no launch is a sliver:
+// 2-20 % faster than the mixed form or LDS-only chunks from 8 to 200 MiB at 1
+// and 8 buckets (profiles/r01b/balance_tune*.txt; libgeeps' AlexNet-sized
+// table puts 30 MiB shards on 8 servers).  Below one tile per block (4 MiB):
+// the mixed form.
 // Every access is non-temporal here (master loads and stores too, unlike the
 // mixed form): +1.5-3 % at 1-8 buckets over plain master accesses, which
 // otherwise linger in the caches and drain to HBM during the next read phase.
-// Chunk c covers tiles [c * G * kT, (c + 1) * G * kT) of kTile f4 each, kT =
-// kLdsTiles + RT; block g takes tiles g, g + G, ...  Only whole tiles: the
-// caller passes n4_tiles, a multiple of kTile, and sums any rest with the
-// mixed form.  The order of the adds per element is the bucket order, as in
-// every form.
+// Chunk c covers tiles [c * G * T, (c + 1) * G * T) of kTile f4 each; block g
+// takes tiles g, g + G, ...; the first 10 go to LDS, the rest to registers.
+// Only whole tiles: the caller passes n4_tiles, a multiple of kTile, and sums
+// any rest with the mixed form.  The order of the adds per element is the
+// bucket order, as in every form.
 constexpr int kPhaseLdsF4 = 10240;  // 160 KiB of results per block, 1 block per CU
 constexpr int kPhaseU = 4;          // block-strides per tile
 constexpr int kPhaseTile = kBlock * kPhaseU;  // f4 per tile (16 KiB)
 constexpr int kPhaseLdsTiles = kPhaseLdsF4 / kPhaseTile;
-constexpr int kPhaseMinChunks = 3;  // shards below 3 chunks: a shorter chunk form, or mixed
+constexpr int kPhaseMinChunks = 3;  // shards below 3 chunks: balanced chunks
 
 template <int NB>
 constexpr int phase_reg_tiles() { return NB <= 2 ? 20 : NB <= 4 ? 12 : 4; }
 
-constexpr int phase_chunks_per_launch(int rt) { return rt > 0 ? 1 : 2; }
+// How a shard of n4_tiles whole tiles is summed: rt < 0 = the mixed form;
+// else the phased kernel with rt register tiles, `tiles` tiles per block per
+// chunk, `per_launch` chunks per launch, `launches` launches.
+struct PhasePlan {
+  int rt;
+  int tiles;
+  int per_launch;
+  size_t launches;
+  bool balanced;
+};
 
-inline size_t phase_chunk_f4(int rt) {
-  return (size_t)num_cus() * (size_t)(kPhaseLdsTiles + rt) * kPhaseTile;
+template <int NB>
+PhasePlan phase_plan(size_t n4_tiles) {
+  const size_t G = (size_t)num_cus();
+  const size_t tiles = n4_tiles / kPhaseTile;
+  constexpr int rt = phase_reg_tiles<NB>();
+  const size_t reg_chunk = G * (kPhaseLdsTiles + rt);
+  if (tiles >= reg_chunk * kPhaseMinChunks)  // register-extended chunks, 1 per launch
+    return {rt, kPhaseLdsTiles + rt, 1, (tiles + reg_chunk - 1) / reg_chunk, false};
+  if (tiles >= G) {  // balanced: C <= 3 chunks of T <= 10 + rt tiles per block
+    const size_t chunks = (tiles + reg_chunk - 1) / reg_chunk;
+    return {rt, (int)((tiles + G * chunks - 1) / (G * chunks)), 1, chunks, true};
+  }
+  return {-1, 0, 0, 0, false};
 }
 
-template <int NB, int RT>
+// BAL: a balanced chunk of `bal_tiles` (<= kT) tiles per block, one chunk per
+// launch.  Otherwise chunks of kT tiles, 1 (register tiles) or 2 per launch,
+// all compile-time: the fixed forms measured 18 % slower with the tile count
+// and chunks per launch passed at run time: "prod" rows at 200 and 512 MiB
+// in profiles/r01b/balance_tune_runtime_tiles.txt.
+template <int NB, int RT, bool BAL>
 __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
-    size_t chunk0) {
+    size_t chunk0, int bal_tiles) {
   constexpr int U = kPhaseU;
   constexpr int kT = kPhaseLdsTiles + RT;
+  const int tiles = BAL ? bal_tiles : kT;
+  constexpr int per_launch = BAL ? 1 : (RT > 0 ? 1 : 2);
   __shared__ f4 res[kPhaseLdsF4];
   f4 keep[RT > 0 ? RT : 1][U];
   const f4 *bp[NB];
 #pragma unroll
   for (int k = 0; k < NB; ++k) bp[k] = reinterpret_cast<const f4 *>(b.p[k]);
   const size_t G = gridDim.x;
-  const size_t chunk_f4 = G * (size_t)kT * kPhaseTile;
-  for (int kc = 0; kc < phase_chunks_per_launch(RT); ++kc) {
+  const size_t chunk_f4 = G * (size_t)tiles * kPhaseTile;  // tiles <= kT
+  for (int kc = 0; kc < per_launch; ++kc) {
     const size_t lo = (chunk0 + kc) * chunk_f4;
     if (lo >= n4_tiles) return;  // grid-uniform: no block skips a barrier another waits at
     // read phase: sum the chunk's tiles into LDS (t < kPhaseLdsTiles) and registers
 #pragma unroll
     for (int t = 0; t < kT; ++t) {
       const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kPhaseTile;
-      if (tile0 >= n4_tiles) break;  // block-uniform; later tiles are further out
+      if (t >= tiles || tile0 >= n4_tiles) break;  // block-uniform; later tiles are further out
       const size_t base = tile0 + threadIdx.x;
       f4 acc[U];
       f4 v[NB][U];
@@ -243,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
 #pragma unroll
     for (int t = 0; t < kT; ++t) {
       const size_t tile0 = lo + ((size_t)t * G + blockIdx.x) * kPhaseTile;
-      if (tile0 >= n4_tiles) break;
+      if (t >= tiles || tile0 >= n4_tiles) break;
       const size_t base = tile0 + threadIdx.x;
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -256,33 +289,14 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
   }
 }
 
-// Which phase-separated form sums a shard of n4_tiles whole tiles: the
-// register-extended one when the shard holds kPhaseMinChunks of its chunks,
-// else the LDS-only one on the same rule, else none (-1: the mixed form).
-template <int NB>
-int phase_form(size_t n4_tiles) {
-  if (n4_tiles >= phase_chunk_f4(phase_reg_tiles<NB>()) * kPhaseMinChunks)
-    return phase_reg_tiles<NB>();
-  if (n4_tiles >= phase_chunk_f4(0) * kPhaseMinChunks) return 0;
-  return -1;
-}
-
-inline size_t phase_launches(size_t n4_tiles, int rt) {
-  const size_t chunk_f4 = phase_chunk_f4(rt);
-  const size_t chunks = (n4_tiles + chunk_f4 - 1) / chunk_f4;
-  const size_t k = (size_t)phase_chunks_per_launch(rt);
-  return (chunks + k - 1) / k;
-}
-
-template <int NB, int RT>
+template <int NB, int RT, bool BAL>
 void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_tiles,
-                   hipStream_t s) {
+                   const PhasePlan &p, hipStream_t s) {
   const size_t G = (size_t)num_cus();
-  const size_t launches = phase_launches(n4_tiles, RT);
-  for (size_t l = 0; l < launches; ++l)
-    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT>), dim3((unsigned)G), dim3(kBlock), 0, s,
-                       reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
-                       n4_tiles, l * (size_t)phase_chunks_per_launch(RT));
+  for (size_t l = 0; l < p.launches; ++l)
+    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT, BAL>), dim3((unsigned)G), dim3(kBlock), 0,
+                       s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
+                       n4_tiles, l * (size_t)p.per_launch, p.tiles);
 }
 
 // Buckets advanced by `off` floats.
@@ -304,12 +318,12 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   size_t done = 0;  // floats summed so far
   if (vec) {
     const size_t n4_tiles = n / 4 / kPhaseTile * kPhaseTile;
-    const int rt = phase_form<NB>(n4_tiles);
-    if (rt > 0) {
-      launch_phased<NB, phase_reg_tiles<NB>()>(out, in, b, n4_tiles, s);
-      done = n4_tiles * 4;
-    } else if (rt == 0) {
-      launch_phased<NB, 0>(out, in, b, n4_tiles, s);
+    const PhasePlan p = phase_plan<NB>(n4_tiles);
+    if (p.rt >= 0) {
+      if (p.balanced)
+        launch_phased<NB, phase_reg_tiles<NB>(), true>(out, in, b, n4_tiles, p, s);
+      else
+        launch_phased<NB, phase_reg_tiles<NB>(), false>(out, in, b, n4_tiles, p, s);
       done = n4_tiles * 4;
     }
   }
@@ -344,9 +358,9 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
 template <int NB>
 void bucket_sum_plan_nb(size_t n, int *launches, int *reg_tiles) {
   const size_t n4_tiles = n / 4 / kPhaseTile * kPhaseTile;
-  const int rt = phase_form<NB>(n4_tiles);
-  *reg_tiles = rt;
-  *launches = rt < 0 ? 0 : (int)phase_launches(n4_tiles, rt);
+  const PhasePlan p = phase_plan<NB>(n4_tiles);
+  *reg_tiles = p.rt;
+  *launches = (int)p.launches;
 }
 
 int launch_bucket_sum(float *out, const float *in, const float *const *bk,

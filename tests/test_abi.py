@@ -115,8 +115,9 @@ def test_product_does_not_import_oracle():
 
 def test_bucket_sum_plan_without_device():
     """gp_bucket_sum_plan launches nothing.  Without a device the library
-    assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 40 MiB
-    (LDS only), 56 / 88 / 120 MiB with 4 / 12 / 20 register tiles."""
+    assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 56 / 88 /
+    120 MiB with 4 / 12 / 20 register tiles beside 10 LDS tiles per block;
+    balanced chunks from 4 MiB (one 16-KiB tile per block) up."""
     L = native.lib()
     launches, rt = ctypes.c_int(-5), ctypes.c_int(-5)
 
@@ -128,8 +129,13 @@ def test_bucket_sum_plan_without_device():
     assert plan(1 << 30, 2) == (35, 20)
     assert plan(1 << 30, 4) == (47, 12)
     assert plan(1 << 27, 8) == (10, 4)      # the 8-GPU shard (512 MiB)
-    assert plan(3 * 10 * 1024 * 1024, 8) == (2, 0)  # 120 MiB: 3 LDS-only chunks, 2 per launch
-    assert plan(3 * 10 * 1024 * 1024 - 4096, 8) == (0, -1)  # below: the mixed form
+    # below 3 register-form chunks: <= 3 balanced chunks of the same form, one per launch
+    assert plan(3 * 10 * 1024 * 1024, 8) == (3, 4)   # 120 MiB: 7,680 tiles / 3,584 per chunk
+    assert plan(30 << 18, 5) == (1, 4)
+    assert plan(30 << 18, 4) == (1, 12)
+    assert plan(200 << 18, 1) == (2, 20)
+    assert plan(1 << 20, 8) == (1, 4)        # 4 MiB: one tile per block
+    assert plan((1 << 20) - 4, 8) == (0, -1)  # below: the mixed form
     assert plan(0, 1) == (0, -1)
     assert L.gp_bucket_sum_plan(16, 9, ctypes.byref(launches), ctypes.byref(rt)) == 1
     assert L.gp_bucket_sum_plan(16, 0, ctypes.byref(launches), ctypes.byref(rt)) == 1

@@ -144,11 +144,12 @@ def test_bucket_sum_into_leaves_master(dev, N):
 
 @pytest.mark.parametrize("N,out_of_place", [(1, False), (3, False), (8, False), (8, True), (11, True)])
 def test_bucket_sum_phase_separated_path(dev, N, out_of_place):
-    """Shards of >= 3 chunks (120 MiB on 256 CUs) take the phase-separated kernel
-    (reads summed into LDS per chunk, then written) over their whole 16-KiB
-    tiles; the rest goes to the mixed and scalar forms.  This size gives 3 full
-    40-MiB chunks + a partial one (two launches of 2 chunks), one dwordx4 for
-    the mixed form and a 3-float scalar tail: every element checked bit for bit."""
+    """128-MiB shards take the phase-separated kernel in balanced chunks (reads
+    summed into LDS and registers per chunk, then written) over their whole
+    16-KiB tiles: 2 chunks of 17 tiles per block at 1 and 3 buckets, 3 of 11
+    at 8 (11 buckets: a pass of 8, then one of 3).  The rest goes to the
+    mixed form (one dwordx4) and the scalar form (3 floats): every element
+    checked bit for bit."""
     from geeps_amd import rowops
     n = (32 << 20) + 1024 * 4 * 3 + 7
     ups = [oracle.synthetic_delta(300 + c, n) for c in range(N)]
@@ -208,6 +209,39 @@ def test_bucket_sum_register_tiles_path(dev, large_deltas, N, out_of_place):
     assert np.array_equal(bits(out.cpu().numpy()), bits(e))
     del tb, m, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("mib,N,out_of_place", [(4, 8, False), (30, 5, True), (30, 8, False),
+                                                 (100, 8, True), (100, 6, False), (30, 1, False),
+                                                 (100, 2, True), (64, 3, False)])
+def test_bucket_sum_balanced_small_shards(dev, large_deltas, mib, N, out_of_place):
+    """Shards of 4 MiB up to 3 register-form chunks take the phased kernel in
+    <= 3 balanced chunks (one launch each; 4 MiB: one tile per block), plus a
+    dwordx4 and a 3-float scalar tail: bit for bit."""
+    import ctypes
+    from geeps_amd import native, rowops
+    n = (mib << 18) + 4 + 3
+    launches, rt = ctypes.c_int(0), ctypes.c_int(0)
+    native.check(native.lib().gp_bucket_sum_plan(n, N, ctypes.byref(launches), ctypes.byref(rt)))
+    expect_rt = 20 if N <= 2 else 12 if N <= 4 else 4
+    tiles, per_chunk = mib * 64, 256 * (10 + expect_rt)
+    assert rt.value == expect_rt and launches.value == -(-tiles // per_chunk) <= 3
+    ups = [u[:n] for u in large_deltas[1][:N]]
+    m0 = np.random.default_rng(mib + N).standard_normal(n).astype(np.float32)
+    e = m0.copy()
+    oracle.apply_updates(e, ups)
+    m = T(m0, dev)
+    tb = [T(u, dev) for u in ups]
+    if out_of_place:
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+        rowops.bucket_sum_into(out, m, tb)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(m.cpu().numpy()), bits(m0))
+    else:
+        rowops.bucket_sum_apply(m, tb)
+        out = m
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()), bits(e))
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 255, 256, 257, 1023, 1024 * 256 + 3])
