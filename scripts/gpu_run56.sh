@@ -1,0 +1,16 @@
+#!/bin/bash
+# Evidence refresh for the current build: smoke, default bench, rocprof summary, FETCH/WRITE passes.
+cd "$GRAFT_REPO_ROOT"
+O=$GRAFT_REPO_ROOT/gpurun_out/r56; mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; rc=$?
+echo "smoke rc=$rc $(tail -n 1 $O/smoke.log)"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err; rc=$?
+echo "bench rc=$rc $(grep -o '"frac": [0-9.]*' $O/bench_default.json | head -1) $(grep -o '"avg_kernel_ms": [0-9.]*' $O/bench_default.json | head -1)"; [ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+ARGS="--no-cpu-baseline --no-host-inclusive --no-rowops --no-hbm-probe"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $O/prof_bench.json 2> $O/prof_bench.err; rc=$?
+echo "rocprof rc=$rc $(grep -o '"avg_launch_ms": [0-9.]*' $O/prof_bench.json)"; [ $rc -eq 0 ] || exit $rc
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS --steps 2 --warmup 1 > $O/pmc_fetch.log 2>&1; rc=$?
+echo "pmc fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS --steps 2 --warmup 1 > $O/pmc_write.log 2>&1; rc=$?
+echo "pmc write rc=$rc"; exit $rc
