@@ -429,6 +429,30 @@ __device__ __forceinline__ float *seg_row(const gp_row_segments &t, uint64_t row
   return t.base[s] + (row - t.first_row[s]) * row_size;
 }
 
+// Cache policy per stream, measured at 128-float rows, 8 M rows, random and
+// identity indexes on three boxes (profiles/r01b/rownt_tune*.txt):
+//  * scatter-add / fused init: the op buffer x is read once per call:
+//    non-temporal loads, 2-3 % faster.  The oplog side stays plain (nt on its
+//    loads or stores lost or tied; the server's sum reads it next and may find
+//    it in the Infinity Cache when the table is small).
+//  * gather (Read): non-temporal loads of the cache rows AND stores into the
+//    op buffer, 3-5 % faster; either one alone tied or lost.
+template <int OP, typename T>
+__device__ __forceinline__ T ld_src(const T *p) {
+  if constexpr (OP == kAddFrom || OP == kInitFrom || OP == kAssignTo)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+template <int OP, typename T>
+__device__ __forceinline__ void st_copy(T *p, T v) {
+  if constexpr (OP == kAssignTo)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 // T = f4 (VEC 4) or float (VEC 1).  A group of LPR consecutive lanes owns a
 // row; each group handles RPG rows per iteration, all their loads issued
 // before the first store.  `vw` = row_size / VEC (vectors per row).
@@ -469,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void row_op_kernel(
         T xs[RPG], ys[RPG];
 #pragma unroll
         for (int k = 0; k < RPG; ++k)
-          if (live[k]) xs[k] = xv[from[k] * vw + j];
+          if (live[k]) xs[k] = ld_src<OP>(xv + from[k] * vw + j);
         if (OP == kAddFrom) {
 #pragma unroll
           for (int k = 0; k < RPG; ++k)
@@ -483,7 +507,7 @@ __global__ __launch_bounds__(kBlock) void row_op_kernel(
             else if (OP == kInitFrom)
               yv[to[k] * vw + j] = T(0.0f) + xs[k];  // == zerofy then +=, -0 -> +0 included
             else
-              yv[to[k] * vw + j] = xs[k];
+              st_copy<OP>(yv + to[k] * vw + j, xs[k]);
           }
         }
       }
@@ -559,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void row_op_seg_kernel(
         T xs[RPG], ys[RPG];
 #pragma unroll
         for (int k = 0; k < RPG; ++k)
-          if (live[k]) xs[k] = reinterpret_cast<const T *>(xr[k])[j];
+          if (live[k]) xs[k] = ld_src<OP>(reinterpret_cast<const T *>(xr[k]) + j);
         if (OP == kAddFrom) {
 #pragma unroll
           for (int k = 0; k < RPG; ++k)
@@ -568,7 +592,7 @@ __global__ __launch_bounds__(kBlock) void row_op_seg_kernel(
 #pragma unroll
         for (int k = 0; k < RPG; ++k)
           if (live[k])
-            reinterpret_cast<T *>(yr[k])[j] = OP == kAddFrom ? ys[k] + xs[k] : xs[k];
+            st_copy<OP>(reinterpret_cast<T *>(yr[k]) + j, OP == kAddFrom ? ys[k] + xs[k] : xs[k]);
       }
     } else {
 #pragma unroll 1
