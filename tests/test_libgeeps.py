@@ -18,7 +18,9 @@ import pytest
 from conftest import REPO
 
 LIB = os.path.join(REPO, "geeps_amd", "lib", "libgeeps.so")
-SUM_APP = os.path.join(REPO, "build", "tests", "geeps_sum_app")
+# GEEPS_SUM_APP: another build of the same app, e.g. the host-UBSan one from
+# scripts/build_ubsan.sh.
+SUM_APP = os.environ.get("GEEPS_SUM_APP") or os.path.join(REPO, "build", "tests", "geeps_sum_app")
 HELLO = os.path.join(REPO, "build", "ref_apps", "helloworld")
 
 # Every member of class GeePs in the reference header (include/geeps.hpp:73-98).
