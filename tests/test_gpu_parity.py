@@ -314,7 +314,7 @@ def test_side_stream(dev):
     assert np.array_equal(bits(m.cpu().numpy()), bits(e))
 
 
-# ---- full BASELINE sizes: sampled-row exactness ---------------------------------
+# ---- full BASELINE sizes: every element vs torch, sampled rows vs the oracle -------
 
 def _sample_rows(rng, R, k=2048):
     # always include the first and last rows (grid-stride head and tail)
@@ -323,8 +323,9 @@ def _sample_rows(rng, R, k=2048):
 
 @pytest.mark.slow
 def test_full_size_8way_bucket_sum(dev):
-    """1M rows x 1024 fp32, 8 clients (36 GiB resident).  Per-element arithmetic is
-    independent across elements, so the oracle on sampled rows is an exact check."""
+    """1M rows x 1024 fp32, 8 clients (36 GiB resident).  Every element against a
+    plain torch fp32 reference in client order, and sampled rows against the C
+    oracle (per-element arithmetic is independent across elements)."""
     from geeps_amd import rowops
     R, W, N = 1 << 20, 1024, 8
     n = R * W
@@ -339,8 +340,15 @@ def test_full_size_8way_bucket_sum(dev):
     ridx = torch.from_numpy(rows).to(dev)
     m0 = master.view(R, W)[ridx].cpu().numpy().ravel()
     bs = [b.view(R, W)[ridx].cpu().numpy().ravel() for b in buckets]
+    # every element: a plain torch fp32 reference adding the buckets one at a
+    # time in client order (elementwise IEEE adds, the same order of operations)
+    expect = master.clone()
+    for b in buckets:
+        expect += b
     rowops.bucket_sum_apply(master, buckets)
     torch.cuda.synchronize()
+    assert torch.equal(master.view(torch.int32), expect.view(torch.int32))
+    del expect
     oracle.apply_updates(m0, bs)
     got = master.view(R, W)[ridx].cpu().numpy().ravel()
     assert np.array_equal(bits(got), bits(m0))
@@ -349,8 +357,9 @@ def test_full_size_8way_bucket_sum(dev):
 @pytest.mark.slow
 def test_full_size_scatter_add_permuted(dev):
     """8M RowData rows (the 1M x 1024 table through the 128-float API), random
-    permutation DoubleIndex; sampled rows exact vs oracle, and x added then
-    subtracted restores y bit-exactly on integer-valued data."""
+    permutation DoubleIndex; every row vs a torch reference and sampled rows vs
+    the oracle, and x added then subtracted restores y bit-exactly on
+    integer-valued data."""
     from geeps_amd import rowops
     R, W = 1 << 23, 128
     g = torch.Generator(device=dev)
@@ -369,6 +378,11 @@ def test_full_size_scatter_add_permuted(dev):
     got = y.view(R, W)[pidx].cpu().numpy()
     e = y0.view(R, W)[pidx].cpu().numpy() + x.view(R, W)[ridx].cpu().numpy()
     assert np.array_equal(bits(got), bits(e.astype(np.float32)))
+    # every row: the torch reference y0[perm[r]] + x[r] (integer-valued, exact)
+    full = y0.view(R, W).clone()
+    full[perm] = full[perm] + x.view(R, W)
+    assert torch.equal(y.view(R, W).view(torch.int32), full.view(torch.int32))
+    del full
     rowops.add_rows_from_double_index_gpu(y, -x, idx, R, (0, 0), W, R * W, validate=False)
     torch.cuda.synchronize()
     assert torch.equal(y, y0)
