@@ -158,6 +158,20 @@ void launch_phased_reg(float *m, const BucketPtrs &b) {
                        reinterpret_cast<f4 *>(m), b, n4, c);
 }
 
+// The production kernel's fixed-chunk launches alternated over two streams, so
+// chunk l + 1 can start on CUs that chunk l's tail has freed (no dependency:
+// chunks are disjoint).  Blocking streams: the null-stream events around a
+// call still bracket all of it.
+template <int NB>
+void launch_prod_two_streams(float *m, const BucketPtrs &b, hipStream_t s0, hipStream_t s1) {
+  const size_t n4_tiles = kN / 4 / kPhaseTile * kPhaseTile;
+  const PhasePlan p = phase_plan<NB>(n4_tiles);
+  for (size_t l = 0; l < p.launches; ++l)
+    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, phase_reg_tiles<NB>(), false>),
+                       dim3((unsigned)num_cus()), dim3(kBlock), 0, (l & 1) ? s1 : s0,
+                       reinterpret_cast<f4 *>(m), reinterpret_cast<const f4 *>(m), b, n4_tiles, l, 0);
+}
+
 __global__ void fill_k(float *p, size_t n, unsigned seed) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -236,6 +250,9 @@ int main(int argc, char **argv) {
   };
   std::vector<V> vs;
   std::vector<double> vbytes;
+  hipStream_t s0, s1;
+  CK(hipStreamCreate(&s0));
+  CK(hipStreamCreate(&s1));
   for (auto &s : sets) {
     std::vector<const float *> bv(s.b.p, s.b.p + 8);
     float *m = s.master;
@@ -247,13 +264,8 @@ int main(int argc, char **argv) {
     for (int nb : {1, 2, 4, 8}) {
       add("prod", nb, [=]() { gp_bucket_sum_apply(m, bv.data(), nb, kN, nullptr); });
     }
-    add("reg R4 k2", 8, [=]() { launch_phased_reg<8, 10240, 4, 2>(m, bp); });
-    add("reg R4 k3", 8, [=]() { launch_phased_reg<8, 10240, 4, 3>(m, bp); });
-    add("reg R2 k1", 8, [=]() { launch_phased_reg<8, 10240, 2, 1>(m, bp); });
-    add("reg R6 k1", 8, [=]() { launch_phased_reg<8, 10240, 6, 1>(m, bp); });
-    add("reg R20 k2", 2, [=]() { launch_phased_reg<2, 10240, 20, 2>(m, bp); });
-    add("reg R28 k1", 2, [=]() { launch_phased_reg<2, 10240, 28, 1>(m, bp); });
-    add("reg R16 k1", 4, [=]() { launch_phased_reg<4, 10240, 16, 1>(m, bp); });
+    add("prod 2 streams", 8, [=]() { launch_prod_two_streams<8>(m, bp, s0, s1); });
+    add("prod 2 streams", 2, [=]() { launch_prod_two_streams<2>(m, bp, s0, s1); });
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
