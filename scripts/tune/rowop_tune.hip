@@ -1,5 +1,5 @@
 // rowop_tune.hip — sweep of the product row-op kernel's template parameters
-// (lanes per row, rows per group iteration, grid size) for the client
+// (rows per group iteration, grid size) for the client
 // scatter-add / gather at 8M RowData rows with a random-permutation index.
 // Tuning harness, not product code: it #includes the product kernels.
 #include "../../geeps_amd/csrc/gp_reduce.hip"
@@ -65,30 +65,28 @@ int main(int argc, char **argv) {
   const double add_b = 3.0 * R * W * 4 + 16.0 * R, gat_b = 2.0 * R * W * 4 + 16.0 * R;
   std::vector<V> vs;
 #define ADD(NAME, B, ...) vs.push_back(V{NAME, B, [&]() { __VA_ARGS__; }, {}})
-  ADD("add separate (prod)", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 8)));
-  ADD("gather separate (prod)", gat_b, (launch<kAssignTo, 32, 8>(y, x, idx, R, W, 8)));
-  // one arena per variant: orders of {x, y} (index stays separate: 1 % of bytes)
-  const size_t fb = R * W * 4;
-  struct Lay { const char *add_name, *gat_name; float *x, *y; };
-  std::vector<Lay> lays;
-  {
-    char *a;
-    CK(hipMalloc(&a, 2 * fb));
-    lays.push_back({"add arena [x|y]", "gather arena [x|y]", (float *)a, (float *)(a + fb)});
-  }
-  {
-    char *a;
-    CK(hipMalloc(&a, 2 * fb));
-    lays.push_back({"add arena [y|x]", "gather arena [y|x]", (float *)(a + fb), (float *)a});
-  }
-  for (auto &L : lays) {
-    CK(hipMemset(L.x, 0, fb));
-    CK(hipMemset(L.y, 0, fb));
-    float *xx = L.x, *yy = L.y;
-    vs.push_back(V{L.add_name, add_b, [=]() { launch<kAddFrom, 32, 4>(yy, xx, idx, R, W, 8); }, {}});
-    // gather reads the cache (x role) and writes the op buffer (y role)
-    vs.push_back(V{L.gat_name, gat_b, [=]() { launch<kAssignTo, 32, 8>(yy, xx, idx, R, W, 8); }, {}});
-  }
+  // rows in flight per group (RPG) x blocks per CU, on the production kernel
+  // (with its per-stream cache policy); production: add RPG 4, others RPG 8, 8/CU
+  ADD("add   R2 x8", add_b, (launch<kAddFrom, 32, 2>(y, x, idx, R, W, 8)));
+  ADD("add   R4 x4", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 4)));
+  ADD("add   R4 x8 (prod)", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 8)));
+  ADD("add   R4 x16", add_b, (launch<kAddFrom, 32, 4>(y, x, idx, R, W, 16)));
+  ADD("add   R8 x4", add_b, (launch<kAddFrom, 32, 8>(y, x, idx, R, W, 4)));
+  ADD("add   R8 x8", add_b, (launch<kAddFrom, 32, 8>(y, x, idx, R, W, 8)));
+  ADD("gath  R4 x8", gat_b, (launch<kAssignTo, 32, 4>(y, x, idx, R, W, 8)));
+  ADD("gath  R8 x4", gat_b, (launch<kAssignTo, 32, 8>(y, x, idx, R, W, 4)));
+  ADD("gath  R8 x8 (prod)", gat_b, (launch<kAssignTo, 32, 8>(y, x, idx, R, W, 8)));
+  ADD("gath  R8 x16", gat_b, (launch<kAssignTo, 32, 8>(y, x, idx, R, W, 16)));
+  ADD("gath  R16 x4", gat_b, (launch<kAssignTo, 32, 16>(y, x, idx, R, W, 4)));
+  ADD("gath  R16 x8", gat_b, (launch<kAssignTo, 32, 16>(y, x, idx, R, W, 8)));
+  ADD("init  R4 x8", gat_b, (launch<kInitFrom, 32, 4>(y, x, idx, R, W, 8)));
+  ADD("init  R8 x8 (prod)", gat_b, (launch<kInitFrom, 32, 8>(y, x, idx, R, W, 8)));
+  ADD("init  R8 x16", gat_b, (launch<kInitFrom, 32, 8>(y, x, idx, R, W, 16)));
+  ADD("init  R16 x8", gat_b, (launch<kInitFrom, 32, 16>(y, x, idx, R, W, 8)));
+  ADD("add ident R4 x8 (prod)", add_b, (launch<kAddFrom, 32, 4>(y, x, ident, R, W, 8)));
+  ADD("add ident R8 x8", add_b, (launch<kAddFrom, 32, 8>(y, x, ident, R, W, 8)));
+  ADD("gath ident R8 x8 (prod)", gat_b, (launch<kAssignTo, 32, 8>(y, x, ident, R, W, 8)));
+  ADD("gath ident R16 x8", gat_b, (launch<kAssignTo, 32, 16>(y, x, ident, R, W, 8)));
 
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
