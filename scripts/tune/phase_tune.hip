@@ -193,15 +193,21 @@ int main(int argc, char **argv) {
   const int rounds = argc > 1 ? std::atoi(argv[1]) : 5;
   std::vector<Set> sets;
   const int n_arenas = argc > 2 ? std::atoi(argv[2]) : 3;
+  // PHASE_TUNE_PADS=1: arena i puts kPads[i % 5] bytes between consecutive
+  // buffers, so a CU's nine same-offset loads fall on different HBM channels.
+  const bool pads = std::getenv("PHASE_TUNE_PADS") != nullptr;
+  const size_t kPads[5] = {0, 4096, 16384, 69632, (1u << 20) + 4096};
   for (int i = 0; i < n_arenas; ++i) {
     char *a = nullptr;
-    CK(hipMalloc(&a, 9 * kN * 4));
-    Set s{"arena #" + std::to_string(i + 1), {}, nullptr};
+    const size_t pad = pads ? kPads[i % 5] : 0;
+    const size_t stride = kN * 4 + pad;
+    CK(hipMalloc(&a, 9 * stride));
+    Set s{"arena #" + std::to_string(i + 1) + (pads ? " pad " + std::to_string(pad) : ""), {}, nullptr};
     for (int k = 0; k < 8; ++k) {
-      s.b.p[k] = reinterpret_cast<const float *>(a + (size_t)k * kN * 4);
-      fill_k<<<4096, 256>>>(reinterpret_cast<float *>(a + (size_t)k * kN * 4), kN, 1000 + k);
+      s.b.p[k] = reinterpret_cast<const float *>(a + (size_t)k * stride);
+      fill_k<<<4096, 256>>>(reinterpret_cast<float *>(a + (size_t)k * stride), kN, 1000 + k);
     }
-    s.master = reinterpret_cast<float *>(a + (size_t)8 * kN * 4);
+    s.master = reinterpret_cast<float *>(a + (size_t)8 * stride);
     fill_k<<<4096, 256>>>(s.master, kN, 77);
     sets.push_back(s);
   }
@@ -261,11 +267,9 @@ int main(int argc, char **argv) {
       vs.push_back(V{s.name + " NB" + std::to_string(nb) + " " + name, f, {}});
       vbytes.push_back((nb + 2.0) * kN * 4);
     };
-    for (int nb : {1, 2, 4, 8}) {
+    for (int nb : {2, 8}) {
       add("prod", nb, [=]() { gp_bucket_sum_apply(m, bv.data(), nb, kN, nullptr); });
     }
-    add("prod 2 streams", 8, [=]() { launch_prod_two_streams<8>(m, bp, s0, s1); });
-    add("prod 2 streams", 2, [=]() { launch_prod_two_streams<2>(m, bp, s0, s1); });
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
