@@ -163,8 +163,10 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
  * cpu_add<float>, src/common/gpu-util/math_functions.cpp:132-136 -> vsAdd,
  * src/common/gpu-util/mkl_alternate.hpp:59-74).
  * `buckets` is a HOST array of `num_buckets` DEVICE pointers.
- * num_buckets == 0 or num_vals == 0 is a no-op.  One launch reads every
- * byte once: (N + 1) * num_vals * 4 B read, num_vals * 4 B written. */
+ * num_buckets == 0 or num_vals == 0 is a no-op.  Every byte moves once per
+ * pass of up to 8 buckets: (N + 1) * num_vals * 4 B read, num_vals * 4 B
+ * written, in one launch per phase-separated chunk (gp_bucket_sum_plan).
+ * More than 8 buckets: consecutive passes continue the bucket order. */
 int gp_bucket_sum_apply(float *master, const float *const *buckets,
                         int num_buckets, size_t num_vals, gp_stream s);
 
@@ -184,9 +186,10 @@ int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
  * (1..8) over num_vals floats in 16-B-aligned buffers; launches nothing.
  * *phased_launches = launches of the phase-separated kernel (0 when the shard
  * is too small for it and the mixed form sums it in one launch);
- * *reg_tiles = 16-KiB tiles per block held in registers by that form (0: LDS
- * only; -1: not phased).  For measurement tools: bench.py prices the phased
- * kernel per launch with it, as rocprofv3 reports it. */
+ * *reg_tiles = 16-KiB tiles per block held in registers beside the 10 in LDS
+ * (20 at 1-2 buckets, 12 at 3-4, 4 at 5-8; -1: not phased).  For measurement
+ * tools: bench.py prices the phased kernel per launch with it, as rocprofv3
+ * reports it.  Returns GP_ERR_INVALID for num_buckets outside 1..8. */
 int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
                        int *reg_tiles);
 
