@@ -10,9 +10,10 @@
 //    The reference makes N sequential passes over the shard (3 streams x 4 B
 //    per element per client); here one pass reads master + N buckets once and
 //    writes master once, summing in bucket order so every element is
-//    bit-identical to the sequential form.  Large shards use the
-//    phase-separated form (reads of a chunk summed into LDS, then written),
-//    smaller ones and leftovers the mixed dwordx4 form, then a scalar tail.
+//    bit-identical to the sequential form.  Shards of 4 MiB and up use the
+//    phase-separated form (reads of a chunk summed into LDS and registers,
+//    then written), smaller ones and leftovers the mixed dwordx4 form, then a
+//    scalar tail.
 //
 //  * row_op_kernel — the row-indexed scatter-add / gather / scatter-assign
 //    over a DoubleIndex (reference: src/common/row-op-util.cu:39-142).  The
