@@ -611,10 +611,127 @@ __global__ __launch_bounds__(kBlock) void row_op_seg_kernel(
   }
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const int lo = __shfl((int)(uint32_t)v, src, 64);
+  const int hi = __shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Wave-level index map, for the gather (Read) of 65-128-float rows (LPR = 32,
+// two rows per wave instruction).  Lane l of a wave loads entry t + l of the
+// wave's 64-row tile -- one coalesced 1-KiB read -- and resolves it to a
+// source pointer (flat cache, or the segmented cache's buffer), a destination
+// pointer and the row's num_vals_limit guard; the row groups take theirs by
+// __shfl.  The next tile's entries load while this tile's rows move, so no row
+// load waits on an index load.  Measured against the per-group index load of
+// row_op_kernel (scripts/tune/rowmap_tune.hip, profiles/r01b/rowmap_focus_*.txt):
+// 11-12 % faster for the gather at 128-float rows (1.39-1.44 ms for 8 M rows,
+// 76-78 % of 8 TB/s), while the same map was 3 % slower for the scatter-add
+// and 13 % slower at 1024-float rows, which keep row_op_kernel.
+template <typename T, int OP, int LPR, int RPG, int SEG>
+__global__ __launch_bounds__(kBlock) void row_wave_kernel(
+    float *__restrict__ y, const float *__restrict__ x,
+    const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
+    uint64_t off1, size_t row_size, size_t vw, size_t limit, const SegArg<SEG> seg) {
+  static_assert(OP == kAssignTo && (SEG == kFlat || SEG == kSegX), "gather only");
+  // Row pointers travel through __shfl as integers; accessed as global-address-
+  // space pointers so the loads and stores stay global_* (a generic pointer
+  // would make them flat_*, measured 2x slower here).  The gather's cache
+  // policy (ld_src / st_copy): non-temporal both ways.
+  typedef __attribute__((address_space(1))) T GT;
+  constexpr int kG = 64 / LPR;            // row groups per wave
+  constexpr int kRowsPerGroup = 64 / kG;  // rows of a 64-row tile per group
+  constexpr int kRPG = RPG < kRowsPerGroup ? RPG : kRowsPerGroup;
+  const int wl = threadIdx.x & 63, lane = wl % LPR, gw = wl / LPR;
+  const size_t wave = ((size_t)blockIdx.x * kBlock + threadIdx.x) / 64;
+  const size_t wstride = (size_t)gridDim.x * (kBlock / 64) * 64;
+  size_t t = wave * 64;
+  if (t >= num_rows) return;  // wave-uniform: every lane of a wave reaches each __shfl
+
+  // this lane's row of the current tile: source / destination row pointers,
+  // and whether the row is clear of num_vals_limit (guarded on the
+  // destination row, as in the reference's assign-to)
+  uint64_t msrc = 0, mdst = 0;
+  int mwhole = 0;
+  auto resolve = [&](const gp_double_index &ix, bool live) {
+    msrc = mdst = 0;
+    mwhole = 0;
+    if (!live) return;
+    uint64_t from, to;
+    row_endpoints<OP>(ix, off0, off1, from, to);
+    const float *src;
+    if constexpr (SEG == kSegX)
+      src = seg_row(seg.t, from, row_size);
+    else
+      src = x + from * row_size;
+    msrc = reinterpret_cast<uint64_t>(src);
+    mdst = reinterpret_cast<uint64_t>(y + to * row_size);
+    mwhole = (to + 1) * row_size <= limit;
+  };
+  {
+    const bool live = t + wl < num_rows;
+    gp_double_index ix = {0, 0};
+    if (live) ix = index[t + wl];
+    resolve(ix, live);
+  }
+  for (; t < num_rows; t += wstride) {
+    const size_t nr = t + wstride + wl;  // next tile's entry, in flight meanwhile
+    const bool nlive = nr < num_rows;
+    gp_double_index nix = {0, 0};
+    if (nlive) nix = index[nr];
+    const size_t rows_here = num_rows - t < 64 ? num_rows - t : 64;
+    for (int i0 = 0; i0 < kRowsPerGroup; i0 += kRPG) {
+      uint64_t sp[kRPG], dp[kRPG];
+      bool live[kRPG];
+      bool all_whole = true;
+#pragma unroll
+      for (int k = 0; k < kRPG; ++k) {
+        const int rt = gw + kG * (i0 + k);
+        live[k] = (size_t)rt < rows_here;
+        sp[k] = shfl64(msrc, rt);
+        dp[k] = shfl64(mdst, rt);
+        all_whole = all_whole && (!live[k] || __shfl(mwhole, rt, 64));
+      }
+      if (all_whole) {  // group-uniform
+        for (size_t j = lane; j < vw; j += LPR) {
+          T xs[kRPG];
+#pragma unroll
+          for (int k = 0; k < kRPG; ++k)
+            if (live[k]) xs[k] = __builtin_nontemporal_load(reinterpret_cast<const GT *>(sp[k]) + j);
+#pragma unroll
+          for (int k = 0; k < kRPG; ++k)
+            if (live[k]) __builtin_nontemporal_store(xs[k], reinterpret_cast<GT *>(dp[k]) + j);
+        }
+      } else {
+        // rows straddling num_vals_limit: element-wise guard, scalar accesses
+#pragma unroll 1
+        for (int k = 0; k < kRPG; ++k) {
+          if (!live[k]) continue;
+          const float *xr = reinterpret_cast<const float *>(sp[k]);
+          float *yr = reinterpret_cast<float *>(dp[k]);
+          const uint64_t to = (uint64_t)(yr - y) / row_size;  // the guarded row
+          for (size_t e = lane; e < row_size; e += LPR)
+            if (to * row_size + e < limit) yr[e] = xr[e];
+        }
+      }
+    }
+    resolve(nix, nlive);
+  }
+}
+
 template <typename T, int VEC, int OP, int SEG, int LPR>
 void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
                        size_t n, uint64_t off0, uint64_t off1, size_t row_size,
                        size_t limit, const SegArg<SEG> &seg, hipStream_t s) {
+  if constexpr (OP == kAssignTo && VEC == 4 && LPR == 32 && (SEG == kFlat || SEG == kSegX)) {
+    // the gather of 65-128-float rows: wave-level index map, 8 rows in flight
+    // per group (16 spilled past 256 VGPRs to 1 wave per SIMD: 9 % slower)
+    size_t grid = (n + kBlock - 1) / kBlock;  // one 64-row tile per wave
+    if (grid > grid_cap()) grid = grid_cap();
+    hipLaunchKernelGGL((row_wave_kernel<T, OP, LPR, 8, SEG>), dim3((unsigned)grid), dim3(kBlock),
+                       0, s, y, x, idx, n, off0, off1, row_size, row_size / VEC, limit, seg);
+    return;
+  }
   // Keep ~8 independent 16-B loads per lane in flight.
   constexpr int RPG = (OP == kAddFrom) ? 4 : 8;
   constexpr int kGroups = kBlock / LPR;

@@ -6,7 +6,8 @@
 //                            groups get theirs by __shfl from that lane
 // at several row widths, random-permutation DoubleIndex, plus sequential copy /
 // add ceilings of the same byte counts.  Interleaved rounds in one process,
-// median per variant.  Usage: rowmap_tune [rounds]
+// median per variant.  All forms use the product's per-stream cache policy
+// (ld_src / st_copy in gp_reduce.hip).  Usage: rowmap_tune [rounds]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
 #include <algorithm>
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void row_map_kernel(
           T xs[kRPG], ys[kRPG];
 #pragma unroll
           for (int k = 0; k < kRPG; ++k)
-            if (live[k]) xs[k] = xv[from[k] * vw + j];
+            if (live[k]) xs[k] = ld_src<OP>(xv + from[k] * vw + j);
           if (OP == kAddFrom) {
 #pragma unroll
             for (int k = 0; k < kRPG; ++k)
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void row_map_kernel(
               else if (OP == kInitFrom)
                 yv[to[k] * vw + j] = T(0.0f) + xs[k];  // == zerofy then +=, -0 -> +0 included
               else
-                yv[to[k] * vw + j] = xs[k];
+                st_copy<OP>(yv + to[k] * vw + j, xs[k]);
             }
           }
         }
@@ -143,11 +144,7 @@ __global__ __launch_bounds__(kBlock) void row_map_kernel(
   }
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-  const int lo = __shfl((int)(uint32_t)v, src, 64);
-  const int hi = __shfl((int)(uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
+// shfl64: the product's (gp_reduce.hip)
 
 // Wave-level map (whole rows only: the harness never sets a limit).
 template <int OP, int LPR, int RPG>
@@ -187,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void row_shfl_kernel(float *__restrict__ y,
         f4 xs[kRPG], ys[kRPG];
 #pragma unroll
         for (int k = 0; k < kRPG; ++k)
-          if (live[k]) xs[k] = xv[from[k] * vw + j];
+          if (live[k]) xs[k] = ld_src<OP>(xv + from[k] * vw + j);
         if (OP == kAddFrom) {
 #pragma unroll
           for (int k = 0; k < kRPG; ++k)
@@ -195,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void row_shfl_kernel(float *__restrict__ y,
         }
 #pragma unroll
         for (int k = 0; k < kRPG; ++k)
-          if (live[k]) yv[to[k] * vw + j] = OP == kAddFrom ? ys[k] + xs[k] : xs[k];
+          if (live[k]) st_copy<OP>(yv + to[k] * vw + j, OP == kAddFrom ? ys[k] + xs[k] : xs[k]);
       }
     }
     row_endpoints<OP>(nix, 0, 0, mf, mt);
@@ -238,6 +235,14 @@ __global__ void copy_k(f4 *__restrict__ out, const f4 *__restrict__ in, size_t n
   }
 }
 
+// the product's wave-map gather kernel at another RPG
+template <int RPG>
+void launch_wave(float *y, const float *x, const gp_double_index *idx, size_t n) {
+  size_t grid = std::min((n + kBlock - 1) / kBlock, grid_cap());
+  hipLaunchKernelGGL((row_wave_kernel<f4, kAssignTo, 32, RPG, kFlat>), dim3((unsigned)grid), dim3(kBlock), 0,
+                     0, y, x, idx, n, 0, 0, 128, 32, (size_t)-1, SegArg<kFlat>{});
+}
+
 gp_double_index *make_index(size_t R, uint64_t seed) {
   std::vector<uint64_t> perm(R);
   std::iota(perm.begin(), perm.end(), 0);
@@ -273,32 +278,50 @@ int main(int argc, char **argv) {
   auto add_b = [](size_t R, size_t W) { return 3.0 * R * W * 4 + 16.0 * R; };
   auto gat_b = [](size_t R, size_t W) { return 2.0 * R * W * 4 + 16.0 * R; };
 #define ADD(NAME, B, ...) vs.push_back(V{NAME, B, [=]() { __VA_ARGS__; }, {}})
-  ADD("W128 add prod L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kProd, y, x, i128, R128, 128, 8)));
-  ADD("W128 add map  L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kMap, y, x, i128, R128, 128, 8)));
-  ADD("W128 add map  L32R8", add_b(R128, 128), (launch<kAddFrom, 32, 8>(kMap, y, x, i128, R128, 128, 8)));
-  ADD("W128 add map  L32R4 pc4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kMap, y, x, i128, R128, 128, 4)));
-  ADD("W128 add shfl L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kShfl, y, x, i128, R128, 128, 8)));
-  ADD("W128 gat prod L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kProd, y, x, i128, R128, 128, 8)));
-  ADD("W128 gat map  L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kMap, y, x, i128, R128, 128, 8)));
-  ADD("W128 gat map  L32R4", gat_b(R128, 128), (launch<kAssignTo, 32, 4>(kMap, y, x, i128, R128, 128, 8)));
-  ADD("W128 gat shfl L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kShfl, y, x, i128, R128, 128, 8)));
-  ADD("W128 init prod L32R8", gat_b(R128, 128), (launch<kInitFrom, 32, 8>(kProd, y, x, i128, R128, 128, 8)));
-  ADD("W128 init map  L32R8", gat_b(R128, 128), (launch<kInitFrom, 32, 8>(kMap, y, x, i128, R128, 128, 8)));
-  ADD("W64 add prod L16R4", add_b(R64, 64), (launch<kAddFrom, 16, 4>(kProd, y, x, i64, R64, 64, 8)));
-  ADD("W64 add map  L16R4", add_b(R64, 64), (launch<kAddFrom, 16, 4>(kMap, y, x, i64, R64, 64, 8)));
-  ADD("W64 add shfl L16R4", add_b(R64, 64), (launch<kAddFrom, 16, 4>(kShfl, y, x, i64, R64, 64, 8)));
-  ADD("W64 gat prod L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kProd, y, x, i64, R64, 64, 8)));
-  ADD("W64 gat map  L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kMap, y, x, i64, R64, 64, 8)));
-  ADD("W16 add prod L4R4", add_b(R16, 16), (launch<kAddFrom, 4, 4>(kProd, y, x, i16, R16, 16, 8)));
-  ADD("W16 add map  L4R4", add_b(R16, 16), (launch<kAddFrom, 4, 4>(kMap, y, x, i16, R16, 16, 8)));
-  ADD("W16 add shfl L4R4", add_b(R16, 16), (launch<kAddFrom, 4, 4>(kShfl, y, x, i16, R16, 16, 8)));
-  ADD("W16 gat prod L4R8", gat_b(R16, 16), (launch<kAssignTo, 4, 8>(kProd, y, x, i16, R16, 16, 8)));
-  ADD("W16 gat map  L4R8", gat_b(R16, 16), (launch<kAssignTo, 4, 8>(kMap, y, x, i16, R16, 16, 8)));
-  ADD("W1024 add prod L64R4", add_b(R1024, 1024), (launch<kAddFrom, 64, 4>(kProd, y, x, i1024, R1024, 1024, 8)));
-  ADD("W1024 add map  L64R4", add_b(R1024, 1024), (launch<kAddFrom, 64, 4>(kMap, y, x, i1024, R1024, 1024, 8)));
-  ADD("W1024 gat prod L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kProd, y, x, i1024, R1024, 1024, 8)));
-  ADD("W1024 gat map  L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kMap, y, x, i1024, R1024, 1024, 8)));
+  if (std::getenv("ROWMAP_FOCUS")) {  // W = 128 gather / scatter-add: production vs shfl map
+    gp_double_index *id128 = make_index(R128, 0);  // seed 0: shuffled too
+    ADD("W128 gat prod L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kProd, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat shfl L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kShfl, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat C-ABI (wave R16)", gat_b(R128, 128), (gp_gather_rows(y, x, i128, R128, {0, 0}, 128, (size_t)-1, nullptr)));
+    ADD("W128 gat wave R8", gat_b(R128, 128), (launch_wave<8>(y, x, i128, R128)));
+    ADD("W128 gat shfl L32R4", gat_b(R128, 128), (launch<kAssignTo, 32, 4>(kShfl, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat shfl L32R16", gat_b(R128, 128), (launch<kAssignTo, 32, 16>(kShfl, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat shfl L32R8 x4", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kShfl, y, x, i128, R128, 128, 4)));
+    ADD("W128 gat prod idx2", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kProd, y, x, id128, R128, 128, 8)));
+    ADD("W128 gat shfl idx2", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kShfl, y, x, id128, R128, 128, 8)));
+    ADD("W128 add prod L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kProd, y, x, i128, R128, 128, 8)));
+    ADD("W128 add shfl L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kShfl, y, x, i128, R128, 128, 8)));
+    ADD("W128 add shfl L32R8", add_b(R128, 128), (launch<kAddFrom, 32, 8>(kShfl, y, x, i128, R128, 128, 8)));
+    ADD("W1024 gat prod L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kProd, y, x, i1024, R1024, 1024, 8)));
+    ADD("W1024 gat shfl L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kShfl, y, x, i1024, R1024, 1024, 8)));
+  } else {
+    ADD("W128 add prod L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kProd, y, x, i128, R128, 128, 8)));
+    ADD("W128 add map  L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kMap, y, x, i128, R128, 128, 8)));
+    ADD("W128 add map  L32R8", add_b(R128, 128), (launch<kAddFrom, 32, 8>(kMap, y, x, i128, R128, 128, 8)));
+    ADD("W128 add map  L32R4 pc4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kMap, y, x, i128, R128, 128, 4)));
+    ADD("W128 add shfl L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kShfl, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat prod L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kProd, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat map  L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kMap, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat map  L32R4", gat_b(R128, 128), (launch<kAssignTo, 32, 4>(kMap, y, x, i128, R128, 128, 8)));
+    ADD("W128 gat shfl L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kShfl, y, x, i128, R128, 128, 8)));
+    ADD("W128 init prod L32R8", gat_b(R128, 128), (launch<kInitFrom, 32, 8>(kProd, y, x, i128, R128, 128, 8)));
+    ADD("W128 init map  L32R8", gat_b(R128, 128), (launch<kInitFrom, 32, 8>(kMap, y, x, i128, R128, 128, 8)));
+    ADD("W64 add prod L16R4", add_b(R64, 64), (launch<kAddFrom, 16, 4>(kProd, y, x, i64, R64, 64, 8)));
+    ADD("W64 add map  L16R4", add_b(R64, 64), (launch<kAddFrom, 16, 4>(kMap, y, x, i64, R64, 64, 8)));
+    ADD("W64 add shfl L16R4", add_b(R64, 64), (launch<kAddFrom, 16, 4>(kShfl, y, x, i64, R64, 64, 8)));
+    ADD("W64 gat prod L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kProd, y, x, i64, R64, 64, 8)));
+    ADD("W64 gat map  L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kMap, y, x, i64, R64, 64, 8)));
+    ADD("W16 add prod L4R4", add_b(R16, 16), (launch<kAddFrom, 4, 4>(kProd, y, x, i16, R16, 16, 8)));
+    ADD("W16 add map  L4R4", add_b(R16, 16), (launch<kAddFrom, 4, 4>(kMap, y, x, i16, R16, 16, 8)));
+    ADD("W16 add shfl L4R4", add_b(R16, 16), (launch<kAddFrom, 4, 4>(kShfl, y, x, i16, R16, 16, 8)));
+    ADD("W16 gat prod L4R8", gat_b(R16, 16), (launch<kAssignTo, 4, 8>(kProd, y, x, i16, R16, 16, 8)));
+    ADD("W16 gat map  L4R8", gat_b(R16, 16), (launch<kAssignTo, 4, 8>(kMap, y, x, i16, R16, 16, 8)));
+    ADD("W1024 add prod L64R4", add_b(R1024, 1024), (launch<kAddFrom, 64, 4>(kProd, y, x, i1024, R1024, 1024, 8)));
+    ADD("W1024 add map  L64R4", add_b(R1024, 1024), (launch<kAddFrom, 64, 4>(kMap, y, x, i1024, R1024, 1024, 8)));
+    ADD("W1024 gat prod L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kProd, y, x, i1024, R1024, 1024, 8)));
+    ADD("W1024 gat map  L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kMap, y, x, i1024, R1024, 1024, 8)));
   // ceilings: sequential streams of the same bytes
+  }
   ADD("ceil copy 1R1W (kernel)", 2.0 * bytes,
       (copy_k<<<num_cus() * 8, kBlock>>>(reinterpret_cast<f4 *>(y), reinterpret_cast<const f4 *>(x), bytes / 16)));
   ADD("ceil add 2R1W (gp_add)", 3.0 * bytes, (gp_add(bytes / 4, y, x, y, nullptr)));

@@ -425,7 +425,7 @@ def _split(rng, n_cache, k):
     return [0] + [int(c) for c in cuts] + [n_cache]
 
 
-@pytest.mark.parametrize("W", [1, 3, 4, 64, 128, 1000])
+@pytest.mark.parametrize("W", [1, 3, 4, 64, 100, 128, 1000])
 @pytest.mark.parametrize("nseg", [1, 2, 8, 64])
 def test_segmented_gather_and_add(dev, W, nseg):
     """Gather from / scatter-add into a cache split over separate buffers equals
