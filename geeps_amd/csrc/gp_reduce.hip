@@ -617,8 +617,8 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-// Wave-level index map, for the gather (Read) of 65-128-float rows (LPR = 32,
-// two rows per wave instruction).  Lane l of a wave loads entry t + l of the
+// Wave-level index map, for the gather (Read) of rows of up to 128 floats
+// (LPR <= 32 lanes per row, 2 or more rows per wave instruction).  Lane l of a wave loads entry t + l of the
 // wave's 64-row tile -- one coalesced 1-KiB read -- and resolves it to a
 // source pointer (flat cache, or the segmented cache's buffer), a destination
 // pointer and the row's num_vals_limit guard; the row groups take theirs by
@@ -626,8 +626,10 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // load waits on an index load.  Measured against the per-group index load of
 // row_op_kernel (scripts/tune/rowmap_tune.hip, profiles/r01b/rowmap_focus_*.txt):
 // 11-12 % faster for the gather at 128-float rows (1.39-1.44 ms for 8 M rows,
-// 76-78 % of 8 TB/s), while the same map was 3 % slower for the scatter-add
-// and 13 % slower at 1024-float rows, which keep row_op_kernel.
+// 76-78 % of 8 TB/s), 8-10 % at 64-float rows and 6-7 % at 16-float rows
+// (profiles/r01b/rowmap_short_{a,b}.txt), while the same map was 3 % slower
+// for the scatter-add and 13 % slower at 1024-float rows (one row per wave
+// instruction), which keep row_op_kernel.
 template <typename T, int OP, int LPR, int RPG, int SEG>
 __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
@@ -723,12 +725,15 @@ template <typename T, int VEC, int OP, int SEG, int LPR>
 void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
                        size_t n, uint64_t off0, uint64_t off1, size_t row_size,
                        size_t limit, const SegArg<SEG> &seg, hipStream_t s) {
-  if constexpr (OP == kAssignTo && VEC == 4 && LPR == 32 && (SEG == kFlat || SEG == kSegX)) {
-    // the gather of 65-128-float rows: wave-level index map, 8 rows in flight
-    // per group (16 spilled past 256 VGPRs to 1 wave per SIMD: 9 % slower)
+  if constexpr (OP == kAssignTo && VEC == 4 && LPR <= 32 && (SEG == kFlat || SEG == kSegX)) {
+    // the gather of rows up to 128 floats: wave-level index map.  Rows in
+    // flight per group: 8 at 32 lanes per row (16 spilled past 256 VGPRs to 1
+    // wave per SIMD: 9 % slower), 16 at 16 lanes; shorter rows have fewer rows
+    // per group than that (kRowsPerGroup = LPR).
+    constexpr int RPG = LPR == 32 ? 8 : 16;
     size_t grid = (n + kBlock - 1) / kBlock;  // one 64-row tile per wave
     if (grid > grid_cap()) grid = grid_cap();
-    hipLaunchKernelGGL((row_wave_kernel<T, OP, LPR, 8, SEG>), dim3((unsigned)grid), dim3(kBlock),
+    hipLaunchKernelGGL((row_wave_kernel<T, OP, LPR, RPG, SEG>), dim3((unsigned)grid), dim3(kBlock),
                        0, s, y, x, idx, n, off0, off1, row_size, row_size / VEC, limit, seg);
     return;
   }

@@ -235,12 +235,12 @@ __global__ void copy_k(f4 *__restrict__ out, const f4 *__restrict__ in, size_t n
   }
 }
 
-// the product's wave-map gather kernel at another RPG
-template <int RPG>
-void launch_wave(float *y, const float *x, const gp_double_index *idx, size_t n) {
+// the product's wave-map gather kernel at any lanes-per-row / rows in flight
+template <int RPG, int LPR = 32>
+void launch_wave(float *y, const float *x, const gp_double_index *idx, size_t n, size_t W = 128) {
   size_t grid = std::min((n + kBlock - 1) / kBlock, grid_cap());
-  hipLaunchKernelGGL((row_wave_kernel<f4, kAssignTo, 32, RPG, kFlat>), dim3((unsigned)grid), dim3(kBlock), 0,
-                     0, y, x, idx, n, 0, 0, 128, 32, (size_t)-1, SegArg<kFlat>{});
+  hipLaunchKernelGGL((row_wave_kernel<f4, kAssignTo, LPR, RPG, kFlat>), dim3((unsigned)grid), dim3(kBlock),
+                     0, 0, y, x, idx, n, 0, 0, W, W / 4, (size_t)-1, SegArg<kFlat>{});
 }
 
 gp_double_index *make_index(size_t R, uint64_t seed) {
@@ -294,6 +294,16 @@ int main(int argc, char **argv) {
     ADD("W128 add shfl L32R8", add_b(R128, 128), (launch<kAddFrom, 32, 8>(kShfl, y, x, i128, R128, 128, 8)));
     ADD("W1024 gat prod L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kProd, y, x, i1024, R1024, 1024, 8)));
     ADD("W1024 gat shfl L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kShfl, y, x, i1024, R1024, 1024, 8)));
+  } else if (std::getenv("ROWMAP_SHORT")) {  // gather of short rows: production vs maps
+    ADD("W64 gat prod L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kProd, y, x, i64, R64, 64, 8)));
+    ADD("W64 gat map  L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kMap, y, x, i64, R64, 64, 8)));
+    ADD("W64 gat wave L16R8", gat_b(R64, 64), (launch_wave<8, 16>(y, x, i64, R64, 64)));
+    ADD("W64 gat wave L16R16", gat_b(R64, 64), (launch_wave<16, 16>(y, x, i64, R64, 64)));
+    ADD("W16 gat prod L4R8", gat_b(R16, 16), (launch<kAssignTo, 4, 8>(kProd, y, x, i16, R16, 16, 8)));
+    ADD("W16 gat map  L4R8", gat_b(R16, 16), (launch<kAssignTo, 4, 8>(kMap, y, x, i16, R16, 16, 8)));
+    ADD("W16 gat wave L4R4", gat_b(R16, 16), (launch_wave<4, 4>(y, x, i16, R16, 16)));
+    ADD("W128 gat wave L32R8", gat_b(R128, 128), (launch_wave<8, 32>(y, x, i128, R128, 128)));
+    ADD("W128 gat prod L32R8", gat_b(R128, 128), (launch<kAssignTo, 32, 8>(kProd, y, x, i128, R128, 128, 8)));
   } else {
     ADD("W128 add prod L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kProd, y, x, i128, R128, 128, 8)));
     ADD("W128 add map  L32R4", add_b(R128, 128), (launch<kAddFrom, 32, 4>(kMap, y, x, i128, R128, 128, 8)));
