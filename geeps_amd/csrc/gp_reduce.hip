@@ -627,15 +627,19 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // row_op_kernel (scripts/tune/rowmap_tune.hip, profiles/r01b/rowmap_focus_*.txt):
 // 11-12 % faster for the gather at 128-float rows (1.39-1.44 ms for 8 M rows,
 // 76-78 % of 8 TB/s), 8-10 % at 64-float rows and 6-7 % at 16-float rows
-// (profiles/r01b/rowmap_short_{a,b}.txt), while the same map was 3 % slower
-// for the scatter-add and 13 % slower at 1024-float rows (one row per wave
-// instruction), which keep row_op_kernel.
+// (profiles/r01b/rowmap_short_{a,b}.txt).  The scatter ops keep row_op_kernel:
+// through this kernel (the add / init forms below exist for that A/B only;
+// the product instantiates the gather) the scatter-add was 3-8 % slower and
+// the fused init 13-18 % slower (profiles/r01b/rowmap_scatter_{a,b}.txt), and
+// so were 1024-float rows (13 %, one row per wave instruction).
 template <typename T, int OP, int LPR, int RPG, int SEG>
 __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
     const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
     uint64_t off1, size_t row_size, size_t vw, size_t limit, const SegArg<SEG> seg) {
-  static_assert(OP == kAssignTo && (SEG == kFlat || SEG == kSegX), "gather only");
+  static_assert((OP == kAssignTo && (SEG == kFlat || SEG == kSegX)) ||
+                    ((OP == kAddFrom || OP == kInitFrom) && SEG == kFlat),
+                "gather (flat / segmented source) or flat scatter-add / init");
   // Row pointers travel through __shfl as integers; accessed as global-address-
   // space pointers so the loads and stores stay global_* (a generic pointer
   // would make them flat_*, measured 2x slower here).  The gather's cache
@@ -652,7 +656,8 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
 
   // this lane's row of the current tile: source / destination row pointers,
   // and whether the row is clear of num_vals_limit (guarded on the
-  // destination row, as in the reference's assign-to)
+  // destination row for the gather, as in the reference's assign-to, and on
+  // the source row for the scatter ops)
   uint64_t msrc = 0, mdst = 0;
   int mwhole = 0;
   auto resolve = [&](const gp_double_index &ix, bool live) {
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
       src = x + from * row_size;
     msrc = reinterpret_cast<uint64_t>(src);
     mdst = reinterpret_cast<uint64_t>(y + to * row_size);
-    mwhole = (to + 1) * row_size <= limit;
+    mwhole = ((OP == kAssignTo ? to : from) + 1) * row_size <= limit;
   };
   {
     const bool live = t + wl < num_rows;
@@ -696,13 +701,26 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
       }
       if (all_whole) {  // group-uniform
         for (size_t j = lane; j < vw; j += LPR) {
-          T xs[kRPG];
+          T xs[kRPG], ys[kRPG];
 #pragma unroll
           for (int k = 0; k < kRPG; ++k)
             if (live[k]) xs[k] = __builtin_nontemporal_load(reinterpret_cast<const GT *>(sp[k]) + j);
+          if (OP == kAddFrom) {
 #pragma unroll
-          for (int k = 0; k < kRPG; ++k)
-            if (live[k]) __builtin_nontemporal_store(xs[k], reinterpret_cast<GT *>(dp[k]) + j);
+            for (int k = 0; k < kRPG; ++k)
+              if (live[k]) ys[k] = reinterpret_cast<const GT *>(dp[k])[j];
+          }
+#pragma unroll
+          for (int k = 0; k < kRPG; ++k) {
+            if (!live[k]) continue;
+            GT *d = reinterpret_cast<GT *>(dp[k]) + j;
+            if (OP == kAddFrom)
+              *d = ys[k] + xs[k];
+            else if (OP == kInitFrom)
+              *d = T(0.0f) + xs[k];  // == zerofy then +=, -0 -> +0 included
+            else
+              __builtin_nontemporal_store(xs[k], d);
+          }
         }
       } else {
         // rows straddling num_vals_limit: element-wise guard, scalar accesses
@@ -711,9 +729,21 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
           if (!live[k]) continue;
           const float *xr = reinterpret_cast<const float *>(sp[k]);
           float *yr = reinterpret_cast<float *>(dp[k]);
-          const uint64_t to = (uint64_t)(yr - y) / row_size;  // the guarded row
-          for (size_t e = lane; e < row_size; e += LPR)
-            if (to * row_size + e < limit) yr[e] = xr[e];
+          // the guarded row: destination of a gather, (flat) source otherwise
+          const uint64_t g = OP == kAssignTo ? (uint64_t)(yr - y) / row_size
+                                             : (uint64_t)(xr - x) / row_size;
+          for (size_t e = lane; e < row_size; e += LPR) {
+            if (g * row_size + e < limit) {
+              if (OP == kAddFrom)
+                yr[e] += xr[e];
+              else if (OP == kInitFrom)
+                yr[e] = 0.0f + xr[e];
+              else
+                yr[e] = xr[e];
+            } else if (OP == kInitFrom) {
+              yr[e] = 0.0f;  // the zerofied value the add never touched
+            }
+          }
         }
       }
     }

@@ -235,11 +235,11 @@ __global__ void copy_k(f4 *__restrict__ out, const f4 *__restrict__ in, size_t n
   }
 }
 
-// the product's wave-map gather kernel at any lanes-per-row / rows in flight
-template <int RPG, int LPR = 32>
+// the product's wave-map kernel at any op / lanes-per-row / rows in flight
+template <int RPG, int LPR = 32, int OP = kAssignTo>
 void launch_wave(float *y, const float *x, const gp_double_index *idx, size_t n, size_t W = 128) {
   size_t grid = std::min((n + kBlock - 1) / kBlock, grid_cap());
-  hipLaunchKernelGGL((row_wave_kernel<f4, kAssignTo, LPR, RPG, kFlat>), dim3((unsigned)grid), dim3(kBlock),
+  hipLaunchKernelGGL((row_wave_kernel<f4, OP, LPR, RPG, kFlat>), dim3((unsigned)grid), dim3(kBlock),
                      0, 0, y, x, idx, n, 0, 0, W, W / 4, (size_t)-1, SegArg<kFlat>{});
 }
 
@@ -294,6 +294,19 @@ int main(int argc, char **argv) {
     ADD("W128 add shfl L32R8", add_b(R128, 128), (launch<kAddFrom, 32, 8>(kShfl, y, x, i128, R128, 128, 8)));
     ADD("W1024 gat prod L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kProd, y, x, i1024, R1024, 1024, 8)));
     ADD("W1024 gat shfl L64R8", gat_b(R1024, 1024), (launch<kAssignTo, 64, 8>(kShfl, y, x, i1024, R1024, 1024, 8)));
+  } else if (std::getenv("ROWMAP_SCATTER")) {  // scatter-add / fused init: production vs wave map
+    for (int rep = 0; rep < 2; ++rep) {
+      ADD("W128 add C-ABI", add_b(R128, 128), (gp_scatter_add_rows(y, x, i128, R128, {0, 0}, 128, (size_t)-1, nullptr)));
+      ADD("W128 add wave R4", add_b(R128, 128), (launch_wave<4, 32, kAddFrom>(y, x, i128, R128)));
+      ADD("W128 add wave R8", add_b(R128, 128), (launch_wave<8, 32, kAddFrom>(y, x, i128, R128)));
+      ADD("W128 init C-ABI", gat_b(R128, 128), (gp_scatter_init_rows(y, x, i128, R128, {0, 0}, 128, (size_t)-1, nullptr)));
+      ADD("W128 init wave R8", gat_b(R128, 128), (launch_wave<8, 32, kInitFrom>(y, x, i128, R128)));
+      ADD("W128 init wave R16", gat_b(R128, 128), (launch_wave<16, 32, kInitFrom>(y, x, i128, R128)));
+      ADD("W64 add C-ABI", add_b(R64, 64), (gp_scatter_add_rows(y, x, i64, R64, {0, 0}, 64, (size_t)-1, nullptr)));
+      ADD("W64 add wave R8", add_b(R64, 64), (launch_wave<8, 16, kAddFrom>(y, x, i64, R64, 64)));
+      ADD("W64 init C-ABI", gat_b(R64, 64), (gp_scatter_init_rows(y, x, i64, R64, {0, 0}, 64, (size_t)-1, nullptr)));
+      ADD("W64 init wave R16", gat_b(R64, 64), (launch_wave<16, 16, kInitFrom>(y, x, i64, R64, 64)));
+    }
   } else if (std::getenv("ROWMAP_SHORT")) {  // gather of short rows: production vs maps
     ADD("W64 gat prod L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kProd, y, x, i64, R64, 64, 8)));
     ADD("W64 gat map  L16R8", gat_b(R64, 64), (launch<kAssignTo, 16, 8>(kMap, y, x, i64, R64, 64, 8)));
