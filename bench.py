@@ -11,9 +11,9 @@ hosted on rank c % N; its delta buffer is uniform in [-0.5, 0.5) (seed 1000+c).
 A *step* is one device-resident N-way reduction: each shard adds the 8 client
 buckets for its rows into its master copy in client order 0..7 with one
 gp_bucket_sum_apply call (the reference's TabletStorage::apply_updates x 8,
-src/server/tablet-server.cpp:119-134); for a 4 GiB shard that call issues 74
-launches of the phase-separated kernel, each summing a 56-MiB chunk of the
-shard (gp_bucket_sum_plan gives the count).  At N > 1 the buckets were first moved
+src/server/tablet-server.cpp:119-134); for a 4 GiB shard that call issues 64
+launches of the phase-separated sweep kernel, each summing a 64-MiB chunk of
+the shard (gp_bucket_sum_sweep_plan gives the count).  At N > 1 the buckets were first moved
 to their shard by RCCL all-to-all (untimed here; the exchange-inclusive step
 exchange + apply + all-gather refresh is timed separately and reported as
 `exchange_inclusive`).  Total work is fixed as N grows: scaling "strong".
@@ -46,15 +46,21 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roofline"
 def sum_launch_plan(num_vals: int, num_buckets: int):
-    """(dominant kernel name, its launches per step, register tiles) for one
-    N-way sum of num_vals floats, from the library's own launch plan
-    (gp_bucket_sum_plan): shards of at least 3 phase-separated chunks go to
-    bucket_sum_phased_kernel, smaller ones to bucket_sum_vec_kernel in one launch."""
+    """(dominant kernel name, launches per step, register tiles) for one N-way
+    sum of num_vals floats, from the library's own launch plan
+    (gp_bucket_sum_sweep_plan): at 3-8 buckets, shards of at least 3 whole
+    64-MiB chunks go to bucket_sum_sweep_kernel (the 4 GiB headline shard and
+    its 1/2, 1/4, 1/8 slices are whole chunks, so every launch is one), the
+    rest to bucket_sum_phased_kernel; shards under 4 MiB to bucket_sum_vec_kernel
+    in one launch."""
     import ctypes
     from geeps_amd import native
-    launches, reg_tiles = ctypes.c_int(0), ctypes.c_int(0)
-    native.check(native.lib().gp_bucket_sum_plan(num_vals, num_buckets, ctypes.byref(launches),
-                                                 ctypes.byref(reg_tiles)), "gp_bucket_sum_plan")
+    launches, reg_tiles, sweeps = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    native.check(native.lib().gp_bucket_sum_sweep_plan(
+        num_vals, num_buckets, ctypes.byref(launches), ctypes.byref(reg_tiles),
+        ctypes.byref(sweeps)), "gp_bucket_sum_sweep_plan")
+    if sweeps.value > 0:
+        return "bucket_sum_sweep_kernel", launches.value, reg_tiles.value
     if launches.value > 0:
         return "bucket_sum_phased_kernel", launches.value, reg_tiles.value
     return "bucket_sum_vec_kernel", 1, None
@@ -328,13 +334,18 @@ def cpu_baseline(rows, W, clients, seconds):
     return res
 
 
-def load_traffic(workload_key):
+def load_traffic(workload_key, kernel=None):
+    """PMC HBM bytes per launch for this workload from profiles/pmc_traffic.json;
+    None when absent or measured on another kernel than the one this run's
+    plan launches (a stale entry would not be this kernel's traffic)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             data = json.load(f)
         entry = data.get(workload_key)
-        return None if entry is None else float(entry["hbm_bytes_per_launch"])
+        if entry is None or (kernel is not None and kernel not in entry.get("kernel", "")):
+            return None
+        return float(entry["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         return None
 
@@ -422,7 +433,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
             cpu = cpu_baseline(min(args.cpu_rows, R), W, C, args.cpu_seconds)
 
     if rank == 0:
-        traffic = load_traffic(workload_key)
+        traffic = load_traffic(workload_key, kernel_name)
         line = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -300,6 +300,101 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
                        n4_tiles, l * (size_t)p.per_launch, p.tiles);
 }
 
+// Stream-by-stream ("sweep") form of the phased sum, for 3-8 buckets.  Same
+// chunk scheme (LDS + register tiles, then a write phase), but the read phase
+// sweeps the block's tiles once per stream, in bucket order: pass 0 parks the
+// master's (or `in`'s) tiles, pass k adds bucket k-1's tiles into them.  So at
+// any moment the chip reads one contiguous region of one stream instead of
+// NB + 1 regions at once, and each pass keeps TG tiles' loads in flight with
+// the same registers at any NB.  The per-element order is unchanged, ((in +
+// b0) + b1) + ..., so the bits are those of every other form.  Measured
+// (scripts/tune/bmaj_tune.hip, profiles/r01b/bmaj_tune_*.txt, 3 arenas): 8
+// buckets 6.42-6.57 ms against 6.62-7.03 ms for the tile-major form, 4
+// buckets 3.92-3.97 against 4.11-4.21 ms, and a far smaller spread between
+// allocations; at 1-2 buckets it ties or loses, so they keep the tile-major
+// form.  16 tiles per block (10 LDS + 6 register) make a 64-MiB chunk on 256
+// CUs, which divides the 4 GiB headline shard and its 1/2, 1/4, 1/8 slices.
+// Whole chunks only (no guards: the waitcnt counts stay exact); the caller
+// hands the rest of the shard to the tile-major plan.
+constexpr int kSweepRT = 6;
+constexpr int kSweepTG = 4;  // tiles per burst of loads
+constexpr int kSweepT = kPhaseLdsTiles + kSweepRT;
+constexpr int kSweepMinBuckets = 3;
+
+// RT register tiles, bursts of TG tiles (template arguments so the tuning
+// harness can instantiate other shapes; production uses kSweepRT, kSweepTG).
+template <int NB, int RT = kSweepRT, int TG = kSweepTG>
+__global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
+    f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
+    size_t chunk) {
+  constexpr int U = kPhaseU;
+  constexpr int kT = kPhaseLdsTiles + RT;
+  static_assert(kT % TG == 0, "whole bursts");
+  __shared__ f4 res[kPhaseLdsF4];
+  f4 keep[RT][U];
+  const f4 *src[NB + 1];
+  src[0] = in;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) src[k + 1] = reinterpret_cast<const f4 *>(b.p[k]);
+  const size_t G = gridDim.x;
+  const size_t lo = chunk * G * (size_t)kT * kPhaseTile;
+  // Never taken (the host launches whole chunks only), but keep it: with this
+  // exit the compiler schedules each burst's loads together at 6-8 buckets;
+  // without it, short of registers, it regrouped the register tiles' adds
+  // into load -> vmcnt(0) -> add chains (117-224 full drains per chunk, 8.3
+  // instead of 6.5 ms at 8 buckets; profiles/r01b/sweep_ab.txt).
+  if (lo >= n4_tiles) return;
+#pragma unroll
+  for (int k = 0; k <= NB; ++k) {
+#pragma unroll
+    for (int t0 = 0; t0 < kT; t0 += TG) {
+      f4 v[TG][U];
+#pragma unroll
+      for (int j = 0; j < TG; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[j][u] = ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kPhaseTile +
+                              threadIdx.x + u * kBlock);
+#pragma unroll
+      for (int j = 0; j < TG; ++j) {
+        const int t = t0 + j;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          // each lane owns its slots: no barrier between passes; bucket order 0..NB-1
+          if (t < kPhaseLdsTiles) {
+            f4 &r = res[t * kPhaseTile + u * kBlock + threadIdx.x];
+            r = k == 0 ? v[j][u] : r + v[j][u];
+          } else {
+            f4 &r = keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u];
+            r = k == 0 ? v[j][u] : r + v[j][u];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kT; ++t) {
+    const size_t base = lo + ((size_t)t * G + blockIdx.x) * kPhaseTile + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      __builtin_nontemporal_store(t < kPhaseLdsTiles
+                                      ? res[t * kPhaseTile + u * kBlock + threadIdx.x]
+                                      : keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u],
+                                  out + base + u * kBlock);
+  }
+}
+
+// Whole sweep chunks in a shard of n4_tiles f4: used when NB >= 3 and there
+// are at least kPhaseMinChunks of them, else 0.
+template <int NB>
+size_t sweep_chunks(size_t n4_tiles) {
+  if (NB < kSweepMinBuckets) return 0;
+  const size_t chunk_f4 = (size_t)num_cus() * kSweepT * kPhaseTile;
+  const size_t c = n4_tiles / chunk_f4;
+  return c >= (size_t)kPhaseMinChunks ? c : 0;
+}
+
 // Buckets advanced by `off` floats.
 template <int NB>
 BucketPtrs offset_buckets(const BucketPtrs &b, size_t off) {
@@ -318,14 +413,24 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
   size_t done = 0;  // floats summed so far
   if (vec) {
-    const size_t n4_tiles = n / 4 / kPhaseTile * kPhaseTile;
+    // 3-8 buckets: whole sweep chunks first, one launch each
+    const size_t sweeps = sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
+    if constexpr (NB >= kSweepMinBuckets)
+      for (size_t c = 0; c < sweeps; ++c)
+        hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB>), dim3((unsigned)num_cus()), dim3(kBlock),
+                           0, s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
+                           n / 4, c);
+    done = sweeps * (size_t)num_cus() * kSweepT * kPhaseTile * 4;
+    // the rest (all of it below 3 sweep chunks): the tile-major phased form
+    const size_t n4_tiles = (n - done) / 4 / kPhaseTile * kPhaseTile;
     const PhasePlan p = phase_plan<NB>(n4_tiles);
     if (p.rt >= 0) {
+      const BucketPtrs bo = offset_buckets<NB>(b, done);
       if (p.balanced)
-        launch_phased<NB, phase_reg_tiles<NB>(), true>(out, in, b, n4_tiles, p, s);
+        launch_phased<NB, phase_reg_tiles<NB>(), true>(out + done, in + done, bo, n4_tiles, p, s);
       else
-        launch_phased<NB, phase_reg_tiles<NB>(), false>(out, in, b, n4_tiles, p, s);
-      done = n4_tiles * 4;
+        launch_phased<NB, phase_reg_tiles<NB>(), false>(out + done, in + done, bo, n4_tiles, p, s);
+      done += n4_tiles * 4;
     }
   }
   if (vec && n - done >= 4) {
@@ -357,11 +462,14 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
 // Launch plan of one pass of nb buckets over n 16-B-aligned floats (bench.py
 // prices the phased kernel per launch with it).
 template <int NB>
-void bucket_sum_plan_nb(size_t n, int *launches, int *reg_tiles) {
-  const size_t n4_tiles = n / 4 / kPhaseTile * kPhaseTile;
+void bucket_sum_plan_nb(size_t n, int *launches, int *reg_tiles, int *sweep_launches) {
+  const size_t sweeps = sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
+  const size_t done = sweeps * (size_t)num_cus() * kSweepT * kPhaseTile * 4;
+  const size_t n4_tiles = (n - done) / 4 / kPhaseTile * kPhaseTile;
   const PhasePlan p = phase_plan<NB>(n4_tiles);
-  *reg_tiles = p.rt;
-  *launches = (int)p.launches;
+  *sweep_launches = (int)sweeps;
+  *reg_tiles = sweeps ? kSweepRT : p.rt;
+  *launches = (int)(sweeps + (p.rt >= 0 ? p.launches : 0));
 }
 
 int launch_bucket_sum(float *out, const float *in, const float *const *bk,
@@ -917,21 +1025,29 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
                                             offset, row_size, num_vals_limit, (hipStream_t)s);
 }
 
-int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
-                       int *reg_tiles) {
-  if (!phased_launches || !reg_tiles) return set_error(GP_ERR_INVALID, "null pointer");
+int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launches,
+                             int *reg_tiles, int *sweep_launches) {
+  if (!phased_launches || !reg_tiles || !sweep_launches)
+    return set_error(GP_ERR_INVALID, "null pointer");
+  int *l = phased_launches, *r = reg_tiles, *w = sweep_launches;
   switch (num_buckets) {
-    case 1: bucket_sum_plan_nb<1>(num_vals, phased_launches, reg_tiles); break;
-    case 2: bucket_sum_plan_nb<2>(num_vals, phased_launches, reg_tiles); break;
-    case 3: bucket_sum_plan_nb<3>(num_vals, phased_launches, reg_tiles); break;
-    case 4: bucket_sum_plan_nb<4>(num_vals, phased_launches, reg_tiles); break;
-    case 5: bucket_sum_plan_nb<5>(num_vals, phased_launches, reg_tiles); break;
-    case 6: bucket_sum_plan_nb<6>(num_vals, phased_launches, reg_tiles); break;
-    case 7: bucket_sum_plan_nb<7>(num_vals, phased_launches, reg_tiles); break;
-    case 8: bucket_sum_plan_nb<8>(num_vals, phased_launches, reg_tiles); break;
+    case 1: bucket_sum_plan_nb<1>(num_vals, l, r, w); break;
+    case 2: bucket_sum_plan_nb<2>(num_vals, l, r, w); break;
+    case 3: bucket_sum_plan_nb<3>(num_vals, l, r, w); break;
+    case 4: bucket_sum_plan_nb<4>(num_vals, l, r, w); break;
+    case 5: bucket_sum_plan_nb<5>(num_vals, l, r, w); break;
+    case 6: bucket_sum_plan_nb<6>(num_vals, l, r, w); break;
+    case 7: bucket_sum_plan_nb<7>(num_vals, l, r, w); break;
+    case 8: bucket_sum_plan_nb<8>(num_vals, l, r, w); break;
     default: return set_error(GP_ERR_INVALID, "bucket count out of range");
   }
   return GP_OK;
+}
+
+int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
+                       int *reg_tiles) {
+  int sweeps = 0;
+  return gp_bucket_sum_sweep_plan(num_vals, num_buckets, phased_launches, reg_tiles, &sweeps);
 }
 
 int gp_bucket_sum_apply(float *master, const float *const *buckets,

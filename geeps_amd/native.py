@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 4  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 5  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -63,6 +63,7 @@ _SIGNATURES = {
     "gp_bucket_sum_apply": (_i, [_vp, _c.POINTER(_vp), _i, _sz, _vp]),
     "gp_bucket_sum_into": (_i, [_vp, _vp, _c.POINTER(_vp), _i, _sz, _vp]),
     "gp_bucket_sum_plan": (_i, [_sz, _i, _c.POINTER(_i), _c.POINTER(_i)]),
+    "gp_bucket_sum_sweep_plan": (_i, [_sz, _i, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
     "gp_add": (_i, [_sz, _vp, _vp, _vp, _vp]),
     "gp_zero": (_i, [_vp, _sz, _vp]),
     "gp_device_count": (_i, [_c.POINTER(_i)]),

@@ -40,7 +40,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 4
+#define GP_ABI_VERSION 5
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -184,14 +184,22 @@ int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
 
 /* Launch plan of ONE pass of gp_bucket_sum_apply / _into with num_buckets
  * (1..8) over num_vals floats in 16-B-aligned buffers; launches nothing.
- * *phased_launches = launches of the phase-separated kernel (0 when the shard
- * is too small for it and the mixed form sums it in one launch);
+ * *phased_launches = launches of the phase-separated kernels, sweep and
+ * tile-major together (0 when the shard is too small for them and the mixed
+ * form sums it in one launch);
  * *reg_tiles = 16-KiB tiles per block held in registers beside the 10 in LDS
- * (20 at 1-2 buckets, 12 at 3-4, 4 at 5-8; -1: not phased).  For measurement
- * tools: bench.py prices the phased kernel per launch with it, as rocprofv3
- * reports it.  Returns GP_ERR_INVALID for num_buckets outside 1..8. */
+ * by the dominant form (sweep: 6; tile-major: 20 at 1-2 buckets, 12 at 3-4,
+ * 4 at 5-8; -1: not phased).  For measurement tools: bench.py prices the
+ * dominant kernel per launch with it, as rocprofv3 reports it.
+ * Returns GP_ERR_INVALID for num_buckets outside 1..8. */
 int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
                        int *reg_tiles);
+
+/* The same plan, plus *sweep_launches = how many of the phased launches are
+ * the stream-by-stream sweep kernel (64-MiB chunks on 256 CUs; 3-8 buckets,
+ * shards of at least 3 chunks; the tile-major form takes the rest). */
+int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launches,
+                             int *reg_tiles, int *sweep_launches);
 
 /* y[i] = a[i] + b[i] — device form of cpu_add / vsAdd
  * (src/common/gpu-util/math_functions.hpp:60-61, mkl_alternate.hpp:59-74).

@@ -12,7 +12,7 @@ from geeps_amd import native
 def test_header_declares_expected_entry_points():
     syms = native.declared_symbols()
     for s in ("gp_scatter_add_rows", "gp_gather_rows", "gp_scatter_rows",
-              "gp_bucket_sum_apply", "gp_bucket_sum_into", "gp_bucket_sum_plan", "gp_add", "gp_zero",
+              "gp_bucket_sum_apply", "gp_bucket_sum_into", "gp_bucket_sum_plan", "gp_bucket_sum_sweep_plan", "gp_add", "gp_zero",
               "gp_last_error"):
         assert s in syms
     # every declared symbol has a ctypes signature and vice versa
@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 4
+    assert L.gp_abi_version() == native.ABI_VERSION == 5
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -115,9 +115,11 @@ def test_product_does_not_import_oracle():
 
 def test_bucket_sum_plan_without_device():
     """gp_bucket_sum_plan launches nothing.  Without a device the library
-    assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 56 / 88 /
-    120 MiB with 4 / 12 / 20 register tiles beside 10 LDS tiles per block;
-    balanced chunks from 4 MiB (one 16-KiB tile per block) up."""
+    assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 64 MiB
+    for the sweep form (3-8 buckets, 6 register tiles beside 10 LDS tiles per
+    block, shards of at least 3 such chunks); tile-major 56 / 88 / 120 MiB
+    with 4 / 12 / 20 register tiles for the rest; balanced chunks from 4 MiB
+    (one 16-KiB tile per block) up."""
     L = native.lib()
     launches, rt = ctypes.c_int(-5), ctypes.c_int(-5)
 
@@ -125,10 +127,22 @@ def test_bucket_sum_plan_without_device():
         assert L.gp_bucket_sum_plan(n, nb, ctypes.byref(launches), ctypes.byref(rt)) == 0
         return launches.value, rt.value
 
-    assert plan(1 << 30, 8) == (74, 4)      # the 4 GiB headline shard: 73.1 chunks, 1 per launch
-    assert plan(1 << 30, 2) == (35, 20)
-    assert plan(1 << 30, 4) == (47, 12)
-    assert plan(1 << 27, 8) == (10, 4)      # the 8-GPU shard (512 MiB)
+    sweeps = ctypes.c_int(-5)
+
+    def sweep_plan(n, nb):
+        assert L.gp_bucket_sum_sweep_plan(n, nb, ctypes.byref(launches), ctypes.byref(rt),
+                                          ctypes.byref(sweeps)) == 0
+        return launches.value, rt.value, sweeps.value
+
+    assert sweep_plan(1 << 30, 8) == (64, 6, 64)  # the 4 GiB headline shard: 64 sweep chunks
+    assert plan(1 << 30, 8) == (64, 6)
+    assert sweep_plan(1 << 30, 2) == (35, 20, 0)  # 1-2 buckets: tile-major only
+    assert sweep_plan(1 << 30, 4) == (64, 6, 64)
+    assert sweep_plan(1 << 27, 8) == (8, 6, 8)    # the 8-GPU shard (512 MiB)
+    assert sweep_plan(1 << 28, 3) == (16, 6, 16)  # the 4-GPU shard (1 GiB)
+    # 200 MiB: 3 sweep chunks (192 MiB), then the 8-MiB rest in 1 balanced tile-major chunk
+    assert sweep_plan(200 << 18, 8) == (4, 6, 3)
+    assert sweep_plan(120 << 18, 8) == (3, 4, 0)  # under 3 sweep chunks: tile-major only
     # below 3 register-form chunks: <= 3 balanced chunks of the same form, one per launch
     assert plan(3 * 10 * 1024 * 1024, 8) == (3, 4)   # 120 MiB: 7,680 tiles / 3,584 per chunk
     assert plan(30 << 18, 5) == (1, 4)

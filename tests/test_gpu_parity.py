@@ -178,19 +178,24 @@ def large_deltas():
 
 
 @pytest.mark.parametrize("N,out_of_place", [(1, False), (2, True), (3, False), (4, False),
-                                            (5, True), (8, False)])
+                                            (5, True), (6, True), (8, False), (8, True)])
 def test_bucket_sum_register_tiles_path(dev, large_deltas, N, out_of_place):
-    """400-MiB shards take the register-extended phased form at every bucket
-    count (tiles held in registers beside the LDS ones: 20 at 1-2 buckets,
-    12 at 3-4, 4 at 5-8; chunks of 120 / 88 / 56 MiB, the last one partial),
-    then one dwordx4 for the mixed form and a 3-float scalar tail: every
-    element checked bit for bit, and the plan the library reports is that form."""
+    """400-MiB shards: at 1-2 buckets the register-extended tile-major form
+    (20 register tiles beside the 10 LDS ones, 120-MiB chunks, the last one
+    partial); at 3-8 buckets 6 whole 64-MiB sweep chunks, then the 16-MiB rest
+    in one balanced tile-major chunk; then one dwordx4 for the mixed form and a
+    3-float scalar tail: every element checked bit for bit, and the plan the
+    library reports is that form."""
     import ctypes
     from geeps_amd import native, rowops
     n, allups = large_deltas
     launches, rt = ctypes.c_int(0), ctypes.c_int(0)
     native.check(native.lib().gp_bucket_sum_plan(n, N, ctypes.byref(launches), ctypes.byref(rt)))
-    assert rt.value == (20 if N <= 2 else 12 if N <= 4 else 4) and launches.value >= 3
+    assert rt.value == (20 if N <= 2 else 6) and launches.value >= 3
+    sw = ctypes.c_int(-1)
+    native.check(native.lib().gp_bucket_sum_sweep_plan(n, N, ctypes.byref(launches),
+                                                        ctypes.byref(rt), ctypes.byref(sw)))
+    assert (sw.value, launches.value) == ((0, 4) if N <= 2 else (6, 7))
     ups = allups[:N]
     m0 = np.random.default_rng(N).standard_normal(n).astype(np.float32)
     e = m0.copy()
