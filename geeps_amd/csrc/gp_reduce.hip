@@ -26,10 +26,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "gp_reduce.h"
 
@@ -59,22 +62,25 @@ int set_error(int code, const std::string &msg) {
     }                                                                       \
   } while (0)
 
-int g_num_cus = 0;
+// CU count per device, cached on first use and never reset: a device's CU
+// count is fixed, and libgeeps' server, reader and app threads plan launches
+// concurrently (the sweep kernel's grid must equal the plan's G), so nothing
+// may zero a slot another thread reads.  Devices past kMaxDevices (or a failed
+// query, e.g. no GPU in a CPU-only test) read 256, the MI355X count.
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_num_cus[kMaxDevices];  // zero-initialised (static storage)
 
 int num_cus() {
-  // Cached per process (the device's CU count never changes); a race here is
-  // benign (both writers store the same value).
-  if (g_num_cus == 0) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
-                              dev) != hipSuccess ||
-        cus <= 0) {
-      cus = 256;
-    }
-    g_num_cus = cus;
-  }
-  return g_num_cus;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+  const int cached = g_num_cus[dev].load(std::memory_order_relaxed);
+  if (cached > 0) return cached;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  g_num_cus[dev].store(cus, std::memory_order_relaxed);
+  return cus;
 }
 
 size_t grid_cap() { return (size_t)num_cus() * kBlocksPerCU; }
@@ -98,8 +104,11 @@ __device__ __forceinline__ f4 ld_stream(const f4 *p) {
 }
 
 // UNROLL consecutive block-strides per thread: (NB + 1) * UNROLL independent
-// 16-B loads are in flight per lane before the first add.
-template <int NB, int UNROLL>
+// 16-B loads are in flight per lane before the first add.  ZIN (every form
+// below has it): `in` is not read and the sum starts from +0.0f, so
+// out = 0.0f + b0 -- the fused zerofy + scatter-add of a dense row run
+// (gp_scatter_init_rows_planned; 0.0f + -0.0f = +0.0f as after a memset).
+template <int NB, int UNROLL, bool ZIN = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4) {
   const size_t tile = (size_t)kBlock * UNROLL;
@@ -114,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
     f4 acc[UNROLL];
     f4 v[NB][UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) acc[u] = in[base + u * kBlock];
+    for (int u = 0; u < UNROLL; ++u) acc[u] = ZIN ? f4(0.0f) : in[base + u * kBlock];
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -131,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
   for (int u = 0; u < UNROLL; ++u) {
     const size_t i = base + u * kBlock;
     if (i < n4) {
-      f4 acc = in[i];
+      f4 acc = ZIN ? f4(0.0f) : in[i];
 #pragma unroll
       for (int k = 0; k < NB; ++k) acc += ld_stream(bp[k] + i);
       out[i] = acc;
@@ -140,13 +149,13 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
 }
 
 // Scalar form: unaligned pointers and the < 4-float tail.
-template <int NB>
+template <int NB, bool ZIN = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
     float *__restrict__ out, const float *__restrict__ in, BucketPtrs b,
     size_t n) {
   const size_t stride = (size_t)gridDim.x * kBlock;
   for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    float acc = in[i];
+    float acc = ZIN ? 0.0f : in[i];
 #pragma unroll
     for (int k = 0; k < NB; ++k) acc += b.p[k][i];
     out[i] = acc;
@@ -230,7 +239,7 @@ PhasePlan phase_plan(size_t n4_tiles) {
 // all compile-time: the fixed forms measured 18 % slower with the tile count
 // and chunks per launch passed at run time: "prod" rows at 200 and 512 MiB
 // in profiles/r01b/balance_tune_runtime_tiles.txt.
-template <int NB, int RT, bool BAL>
+template <int NB, int RT, bool BAL, bool ZIN = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
     size_t chunk0, int bal_tiles) {
@@ -257,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
       f4 acc[U];
       f4 v[NB][U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] = ld_stream(in + base + u * kBlock);
+      for (int u = 0; u < U; ++u) acc[u] = ZIN ? f4(0.0f) : ld_stream(in + base + u * kBlock);
 #pragma unroll
       for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -290,12 +299,12 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
   }
 }
 
-template <int NB, int RT, bool BAL>
+template <int NB, int RT, bool BAL, bool ZIN = false>
 void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_tiles,
                    const PhasePlan &p, hipStream_t s) {
   const size_t G = (size_t)num_cus();
   for (size_t l = 0; l < p.launches; ++l)
-    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT, BAL>), dim3((unsigned)G), dim3(kBlock), 0,
+    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT, BAL, ZIN>), dim3((unsigned)G), dim3(kBlock), 0,
                        s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
                        n4_tiles, l * (size_t)p.per_launch, p.tiles);
 }
@@ -405,34 +414,40 @@ BucketPtrs offset_buckets(const BucketPtrs &b, size_t off) {
 
 // out[i] = in[i] + b0[i] + ... over i < n: the phase-separated form over the
 // whole 16-KiB tiles of a large shard, the mixed dwordx4 form over what is
-// left of the 16-B-aligned part, the scalar form over the rest.
-template <int NB>
+// left of the 16-B-aligned part, the scalar form over the rest.  ZIN: in is
+// ignored (may be null) and out[i] = 0.0f + b0[i] + ...  The CU count is read
+// once, so the plan and every grid of the call agree.
+template <int NB, bool ZIN = false>
 int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
                          size_t n, hipStream_t s) {
-  bool vec = aligned16(out) && aligned16(in);
+  const size_t G = (size_t)num_cus();
+  bool vec = aligned16(out) && (ZIN || aligned16(in));
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
   size_t done = 0;  // floats summed so far
+  const float *in_at = in;  // `in` advanced by `done` (null stays null under ZIN)
   if (vec) {
     // 3-8 buckets: whole sweep chunks first, one launch each
-    const size_t sweeps = sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
-    if constexpr (NB >= kSweepMinBuckets)
+    const size_t sweeps = ZIN ? 0 : sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
+    if constexpr (NB >= kSweepMinBuckets && !ZIN)
       for (size_t c = 0; c < sweeps; ++c)
-        hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB>), dim3((unsigned)num_cus()), dim3(kBlock),
+        hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB>), dim3((unsigned)G), dim3(kBlock),
                            0, s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
                            n / 4, c);
-    done = sweeps * (size_t)num_cus() * kSweepT * kPhaseTile * 4;
+    done = sweeps * G * kSweepT * kPhaseTile * 4;
     // the rest (all of it below 3 sweep chunks): the tile-major phased form
     const size_t n4_tiles = (n - done) / 4 / kPhaseTile * kPhaseTile;
     const PhasePlan p = phase_plan<NB>(n4_tiles);
     if (p.rt >= 0) {
       const BucketPtrs bo = offset_buckets<NB>(b, done);
+      const float *ip = ZIN ? nullptr : in + done;
       if (p.balanced)
-        launch_phased<NB, phase_reg_tiles<NB>(), true>(out + done, in + done, bo, n4_tiles, p, s);
+        launch_phased<NB, phase_reg_tiles<NB>(), true, ZIN>(out + done, ip, bo, n4_tiles, p, s);
       else
-        launch_phased<NB, phase_reg_tiles<NB>(), false>(out + done, in + done, bo, n4_tiles, p, s);
+        launch_phased<NB, phase_reg_tiles<NB>(), false, ZIN>(out + done, ip, bo, n4_tiles, p, s);
       done += n4_tiles * 4;
     }
   }
+  if (!ZIN) in_at = in + done;
   if (vec && n - done >= 4) {
     // 4 block-strides per thread at 2 blocks per CU: (NB + 1) * 4 dwordx4 loads
     // in flight per lane.  Measured on MI355X at 8 x 4 GiB buckets: +2-3 % over
@@ -441,19 +456,20 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     constexpr int kPerCU = NB <= 2 ? 4 : 2;
     const size_t n4 = (n - done) / 4;
     const size_t tiles = (n4 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    const size_t cap = (size_t)num_cus() * kPerCU;
+    const size_t cap = G * kPerCU;
     const size_t grid = tiles < cap ? tiles : cap;
-    hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U, ZIN>), dim3((unsigned)grid),
                        dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out + done),
-                       reinterpret_cast<const f4 *>(in + done), offset_buckets<NB>(b, done), n4);
+                       reinterpret_cast<const f4 *>(in_at), offset_buckets<NB>(b, done), n4);
     done += n4 * 4;
+    if (!ZIN) in_at = in + done;
   }
   if (done < n) {
     const size_t rem = n - done;
     size_t grid = (rem + kBlock - 1) / kBlock;
-    if (grid > grid_cap()) grid = grid_cap();
-    hipLaunchKernelGGL((bucket_sum_scalar_kernel<NB>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, s, out + done, in + done, offset_buckets<NB>(b, done), rem);
+    if (grid > G * kBlocksPerCU) grid = G * kBlocksPerCU;
+    hipLaunchKernelGGL((bucket_sum_scalar_kernel<NB, ZIN>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, out + done, in_at, offset_buckets<NB>(b, done), rem);
   }
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;
@@ -970,6 +986,108 @@ int launch_row_op_seg(float *flat_ptr, const gp_row_segments *t,
   return GP_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Row plans: a scatter DoubleIndex compiled once (libgeeps' indexes are fixed
+// at FinishVirtualIteration, clientlib-viter.cpp:817-883).
+//
+// The rows are ordered by destination (id1), which is bit-neutral because
+// destinations are distinct: every destination row receives exactly the same
+// adds whatever order the rows are visited in.  Maximal runs in which both
+// id0 and id1 step by one and every row is clear of num_vals_limit are then
+// plain dense ranges -- y[y0 .. y0 + L*W) (+)= x[x0 .. x0 + L*W) -- and runs
+// of at least kDenseRunBytes go to the dense sum kernels (the server's
+// phase-separated form with one bucket: 2 reads + 1 write at its HBM rate, no
+// index traffic).  libgeeps assigns cache rows in first-access order, so an
+// op's rows are typically one run per channel.  Every other row stays in a
+// residual index, sorted by id1, run through the row kernels: its read-
+// modify-write side walks y in order, like the gather's write side.
+// ---------------------------------------------------------------------------
+// A dense run launches 1-3 kernels; below 4 MiB (the phased form's smallest
+// shard) the row kernel moves it at about the same rate without the launches.
+constexpr size_t kDenseRunBytes = 4u << 20;
+
+struct RowRun {
+  uint64_t x_row, y_row, rows;  // offsets applied
+};
+
+}  // namespace
+
+struct gp_row_plan_s {
+  size_t num_rows = 0, row_size = 0, limit = 0;
+  std::vector<RowRun> dense;
+  size_t dense_rows = 0;
+  gp_double_index *residual = nullptr;  // device, offsets applied, ascending id1
+  size_t residual_rows = 0;
+  int device = 0;
+};
+
+namespace {
+
+int build_row_plan(gp_row_plan_s *p, const gp_double_index *host_index, size_t n,
+                   gp_double_index off, size_t row_size, size_t limit) {
+  std::vector<gp_double_index> rows(n);
+  for (size_t r = 0; r < n; ++r)
+    rows[r] = gp_double_index{host_index[r].id0 + off.id0, host_index[r].id1 + off.id1};
+  std::sort(rows.begin(), rows.end(), [](const gp_double_index &a, const gp_double_index &b) {
+    return a.id1 < b.id1;
+  });
+  for (size_t r = 1; r < n; ++r)
+    if (rows[r].id1 == rows[r - 1].id1)
+      return set_error(GP_ERR_INVALID, "row plan: destination row " + std::to_string(rows[r].id1) +
+                                           " repeats (scatter destinations must be distinct)");
+  auto whole = [&](const gp_double_index &d) { return (d.id0 + 1) * row_size <= limit; };
+  const size_t min_rows = std::max<size_t>(1, kDenseRunBytes / (row_size * sizeof(float)));
+  std::vector<gp_double_index> rest;
+  for (size_t a = 0; a < n;) {
+    size_t b = a + 1;
+    if (whole(rows[a]))
+      while (b < n && whole(rows[b]) && rows[b].id0 == rows[b - 1].id0 + 1 &&
+             rows[b].id1 == rows[b - 1].id1 + 1)
+        ++b;
+    if (whole(rows[a]) && b - a >= min_rows) {
+      p->dense.push_back(RowRun{rows[a].id0, rows[a].id1, b - a});
+      p->dense_rows += b - a;
+    } else {
+      rest.insert(rest.end(), rows.begin() + a, rows.begin() + b);
+    }
+    a = b;
+  }
+  p->residual_rows = rest.size();
+  if (!rest.empty()) {
+    GP_HIP_TRY(hipMalloc(&p->residual, rest.size() * sizeof(gp_double_index)));
+    GP_HIP_TRY(hipMemcpy(p->residual, rest.data(), rest.size() * sizeof(gp_double_index),
+                         hipMemcpyHostToDevice));
+  }
+  return GP_OK;
+}
+
+// OP kAddFrom: y += x over the plan's rows; kInitFrom: y = 0.0f + x (0.0f past
+// the limit), as gp_scatter_add_rows / gp_scatter_init_rows with the plan's
+// index, offset and limit.
+template <int OP>
+int launch_planned(float *y, const float *x, const gp_row_plan_s *p, hipStream_t s) {
+  if (!p) return set_error(GP_ERR_INVALID, "null row plan");
+  if (p->num_rows == 0) return GP_OK;
+  if (!y || !x) return set_error(GP_ERR_INVALID, "null pointer");
+  int dev = -1;
+  GP_HIP_TRY(hipGetDevice(&dev));
+  if (dev != p->device && p->residual_rows)
+    return set_error(GP_ERR_INVALID, "row plan used on another device than it was built on");
+  const size_t W = p->row_size;
+  for (const RowRun &r : p->dense) {
+    BucketPtrs b = {};
+    b.p[0] = x + r.x_row * W;
+    float *yr = y + r.y_row * W;
+    const int rc = OP == kAddFrom ? launch_bucket_sum_nb<1>(yr, yr, b, r.rows * W, s)
+                                  : launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s);
+    if (rc != GP_OK) return rc;
+  }
+  if (p->residual_rows)
+    return launch_row_op<OP>(y, x, p->residual, p->residual_rows, gp_double_index{0, 0}, W,
+                             p->limit, s);
+  return GP_OK;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1023,6 +1141,52 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
                                   size_t num_vals_limit, gp_stream s) {
   return launch_row_op_seg<kAddFrom, kSegY>(const_cast<float *>(x), y_segments, index, num_rows,
                                             offset, row_size, num_vals_limit, (hipStream_t)s);
+}
+
+int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
+                       gp_double_index offset, size_t row_size, size_t num_vals_limit) {
+  if (!plan) return set_error(GP_ERR_INVALID, "null pointer");
+  *plan = nullptr;
+  if (num_rows && !host_index) return set_error(GP_ERR_INVALID, "null index");
+  if (row_size == 0) return set_error(GP_ERR_INVALID, "row_size == 0");
+  auto *p = new gp_row_plan_s;
+  p->num_rows = num_rows;
+  p->row_size = row_size;
+  p->limit = num_vals_limit;
+  if (hipGetDevice(&p->device) != hipSuccess) p->device = 0;
+  const int rc = build_row_plan(p, host_index, num_rows, offset, row_size, num_vals_limit);
+  if (rc != GP_OK) {
+    gp_row_plan_destroy(p);
+    return rc;
+  }
+  *plan = p;
+  return GP_OK;
+}
+
+int gp_row_plan_destroy(gp_row_plan plan) {
+  if (!plan) return GP_OK;
+  const hipError_t e = plan->residual ? hipFree(plan->residual) : hipSuccess;
+  delete plan;
+  GP_HIP_TRY(e);
+  return GP_OK;
+}
+
+int gp_row_plan_info(gp_row_plan plan, size_t *dense_runs, size_t *dense_rows,
+                     size_t *residual_rows) {
+  if (!plan || !dense_runs || !dense_rows || !residual_rows)
+    return set_error(GP_ERR_INVALID, "null pointer");
+  *dense_runs = plan->dense.size();
+  *dense_rows = plan->dense_rows;
+  *residual_rows = plan->residual_rows;
+  return GP_OK;
+}
+
+int gp_scatter_add_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s) {
+  return launch_planned<kAddFrom>(y, x, plan, (hipStream_t)s);
+}
+
+int gp_scatter_init_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s) {
+  return launch_planned<kInitFrom>(y, x, plan, (hipStream_t)s);
 }
 
 int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launches,
@@ -1122,7 +1286,6 @@ int gp_device_count(int *count) {
 
 int gp_set_device(int device) {
   GP_HIP_TRY(hipSetDevice(device));
-  g_num_cus = 0;
   return GP_OK;
 }
 

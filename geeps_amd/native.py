@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 5  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 6  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -56,6 +56,11 @@ _SIGNATURES = {
     "gp_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_init_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
+    "gp_row_plan_create": (_i, [_c.POINTER(_vp), _vp, _sz, DoubleIndex, _sz, _sz]),
+    "gp_row_plan_destroy": (_i, [_vp]),
+    "gp_row_plan_info": (_i, [_vp, _c.POINTER(_sz), _c.POINTER(_sz), _c.POINTER(_sz)]),
+    "gp_scatter_add_rows_planned": (_i, [_vp, _vp, _vp, _vp]),
+    "gp_scatter_init_rows_planned": (_i, [_vp, _vp, _vp, _vp]),
     "gp_gather_rows_segmented": (_i, [_vp, _c.POINTER(RowSegments), _vp, _sz, DoubleIndex, _sz,
                                       _sz, _vp]),
     "gp_scatter_add_rows_segmented": (_i, [_c.POINTER(RowSegments), _vp, _vp, _sz, DoubleIndex,

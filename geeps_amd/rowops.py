@@ -166,6 +166,81 @@ def assign_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, inde
             num_vals_limit, stream, validate)
 
 
+class RowPlan:
+    """A scatter DoubleIndex compiled once (gp_row_plan_create): the rows in
+    destination order, dense id0/id1 runs of >= 4 MiB moved by the dense sum
+    kernels, the rest by the row kernels over an id1-sorted device index.
+
+    ``index``: (n, 2) int64 array or tensor (copied to the host once), as for
+    add_rows_from_double_index_gpu; ``index_offset`` and ``num_vals_limit``
+    are baked in.  ``add(y, x)`` / ``init(y, x)`` are bit-identical to
+    add_rows_from_double_index_gpu / init_rows_from_double_index_gpu over the
+    same index.  Destinations must be distinct (ValueError otherwise)."""
+
+    def __init__(self, index, num_rows=None, index_offset=None, row_size=ROW_DATA_SIZE,
+                 num_vals_limit=None):
+        import numpy as np
+        if isinstance(index, torch.Tensor):
+            index = index.detach().cpu().numpy()
+        idx = np.ascontiguousarray(index, dtype=np.int64)
+        if idx.ndim != 2 or idx.shape[1] != 2:
+            raise ValueError("index must have shape (n, 2)")
+        n = idx.shape[0] if num_rows is None else int(num_rows)
+        if n > idx.shape[0]:
+            raise ValueError("num_rows exceeds index length")
+        if n and int(idx[:n].min()) < 0:
+            raise ValueError("negative row id in DoubleIndex")
+        if row_size <= 0:
+            raise ValueError("row_size must be positive")
+        idx = np.ascontiguousarray(idx[:n])
+        self.num_rows, self.row_size = n, int(row_size)
+        self.offset = _as_offset(index_offset)
+        self.limit = (1 << 64) - 1 if num_vals_limit is None else int(num_vals_limit)
+        r0 = idx[:, 0] + self.offset.id0 if n else idx[:, 0]
+        r1 = idx[:, 1] + self.offset.id1 if n else idx[:, 1]
+        active = r0 * self.row_size < self.limit if self.limit < (1 << 62) else np.ones(n, bool)
+        # bounds the row kernels need: source rows below the limit, every destination
+        self.x_need = min((int(r0[active].max()) + 1) * self.row_size, self.limit) if active.any() else 0
+        self.y_need = (int(r1.max()) + 1) * self.row_size if n else 0
+        self._h = ctypes.c_void_p()
+        check(native.lib().gp_row_plan_create(ctypes.byref(self._h), idx.ctypes.data, n, self.offset,
+                                              self.row_size, self.limit), "gp_row_plan_create")
+
+    def info(self) -> dict:
+        a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        check(native.lib().gp_row_plan_info(self._h, ctypes.byref(a), ctypes.byref(b),
+                                            ctypes.byref(c)), "gp_row_plan_info")
+        return {"dense_runs": a.value, "dense_rows": b.value, "residual_rows": c.value}
+
+    def _run(self, fn, y, x, stream, what):
+        _dev_f32(y, "rows_y")
+        _dev_f32(x, "rows_x")
+        if self.x_need > x.numel():
+            raise ValueError("source row out of range for rows_x")
+        if self.y_need > y.numel():
+            raise ValueError("destination row out of range for rows_y")
+        check(fn(y.data_ptr(), x.data_ptr(), self._h, _stream_ptr(stream)), what)
+
+    def add(self, rows_y, rows_x, stream=None) -> None:
+        self._run(native.lib().gp_scatter_add_rows_planned, rows_y, rows_x, stream,
+                  "gp_scatter_add_rows_planned")
+
+    def init(self, rows_y, rows_x, stream=None) -> None:
+        self._run(native.lib().gp_scatter_init_rows_planned, rows_y, rows_x, stream,
+                  "gp_scatter_init_rows_planned")
+
+    def close(self) -> None:
+        if self._h:
+            native.lib().gp_row_plan_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _segments(segments, row_size):
     """[(first_row, tensor), ...] -> (RowSegments, row ranges) with checks."""
     if not 1 <= len(segments) <= native.GP_MAX_SEGMENTS:

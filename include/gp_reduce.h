@@ -40,7 +40,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 5
+#define GP_ABI_VERSION 6
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -114,6 +114,38 @@ int gp_gather_rows(float *y, const float *x, const gp_double_index *index,
 int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
                     size_t num_rows, gp_double_index offset, size_t row_size,
                     size_t num_vals_limit, gp_stream s);
+
+/* ---------------------------------------------------------------------------
+ * Row plans: a scatter DoubleIndex compiled once, for ops whose index is fixed
+ * (libgeeps builds one per op and channel at FinishVirtualIteration, where the
+ * reference builds the op's device DoubleIndex: vi_create_double_index,
+ * src/client/clientlib-viter.cpp:817-883).  The plan visits the rows in
+ * destination (id1) order -- bit-neutral, since destinations are distinct --
+ * and moves runs where id0 and id1 both step by one (whole rows, at least
+ * 4 MiB) as dense ranges through the bucket-sum kernels; the other rows keep a
+ * device index, sorted by id1, for the row kernels.  Results are bit-identical
+ * to gp_scatter_add_rows / gp_scatter_init_rows over the same index, offset
+ * and num_vals_limit.
+ * ------------------------------------------------------------------------- */
+typedef struct gp_row_plan_s *gp_row_plan;
+
+/* Build a plan from a HOST copy of `num_rows` DoubleIndex entries; `offset`
+ * and `num_vals_limit` are baked in (same meaning as gp_scatter_add_rows).
+ * The plan's device index lives on the current device.  GP_ERR_INVALID if a
+ * destination row (id1 + offset.id1) repeats. */
+int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
+                       gp_double_index offset, size_t row_size, size_t num_vals_limit);
+int gp_row_plan_destroy(gp_row_plan plan);
+/* How the plan splits its rows: dense runs, rows in them, rows left to the
+ * row kernels (for tests and measurement). */
+int gp_row_plan_info(gp_row_plan plan, size_t *dense_runs, size_t *dense_rows,
+                     size_t *residual_rows);
+/* gp_scatter_add_rows(y, x, index, ...) through the plan (a3:
+ * add_rows_from_double_index_gpu, src/common/row-op-util.cu:109-142). */
+int gp_scatter_add_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s);
+/* gp_scatter_init_rows(y, x, index, ...) through the plan (a7 + a3: the fused
+ * zerofy_data_gpu + add, common-util.hpp:445-456). */
+int gp_scatter_init_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s);
 
 /* ---------------------------------------------------------------------------
  * Segmented param cache.  The cache rows of one table are split into up to

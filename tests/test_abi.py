@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 5
+    assert L.gp_abi_version() == native.ABI_VERSION == 6
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -154,3 +154,62 @@ def test_bucket_sum_plan_without_device():
     assert L.gp_bucket_sum_plan(16, 9, ctypes.byref(launches), ctypes.byref(rt)) == 1
     assert L.gp_bucket_sum_plan(16, 0, ctypes.byref(launches), ctypes.byref(rt)) == 1
     assert L.gp_bucket_sum_plan(16, 1, None, None) == 1
+
+
+def _plan(idx, offset=(0, 0), row_size=128, limit=None):
+    import numpy as np
+    L = native.lib()
+    h = ctypes.c_void_p()
+    a = np.ascontiguousarray(idx, dtype=np.int64)
+    rc = L.gp_row_plan_create(ctypes.byref(h), a.ctypes.data, a.shape[0], native.DoubleIndex(*offset),
+                              row_size, (1 << 64) - 1 if limit is None else limit)
+    return rc, h
+
+
+def _info(h):
+    a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    assert native.lib().gp_row_plan_info(h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == 0
+    return a.value, b.value, c.value
+
+
+def test_row_plan_classifies_dense_runs_without_device():
+    """Plans whose rows are all in dense runs need no device memory, so the
+    host-side classifier runs here: runs of >= 4 MiB where id0 and id1 both
+    step by one, found after sorting by id1 (any op row order), offsets
+    applied, rows past num_vals_limit kept out of the runs."""
+    import numpy as np
+    L = native.lib()
+    W, R = 128, 8192  # one 4-MiB run at 128 floats
+    ident = np.stack([np.arange(R), np.arange(R)], 1)
+    rc, h = _plan(ident)
+    assert rc == 0 and _info(h) == (1, R, 0)
+    L.gp_row_plan_destroy(h)
+    # two runs listed in reverse op order, destinations of the second below the first's
+    two = np.concatenate([np.stack([np.arange(R), 5 * R + np.arange(R)], 1),
+                          np.stack([R + np.arange(R), np.arange(R)], 1)])[::-1]
+    rc, h = _plan(two, offset=(3, 7))
+    assert rc == 0 and _info(h) == (2, 2 * R, 0)
+    L.gp_row_plan_destroy(h)
+    # 64-float rows: a run needs 16384 rows
+    rc, h = _plan(np.stack([np.arange(2 * R), np.arange(2 * R)], 1), row_size=64)
+    assert rc == 0 and _info(h) == (1, 2 * R, 0)
+    L.gp_row_plan_destroy(h)
+    # empty plan
+    rc, h = _plan(np.zeros((0, 2)))
+    assert rc == 0 and _info(h) == (0, 0, 0)
+    assert L.gp_row_plan_destroy(h) == 0
+    assert L.gp_row_plan_destroy(None) == 0
+
+
+def test_row_plan_rejects_repeated_destinations():
+    import numpy as np
+    idx = np.stack([np.arange(4), np.array([5, 9, 5, 2])], 1)
+    rc, h = _plan(idx)
+    assert rc == native.GP_ERR_INVALID and b"repeats" in native.lib().gp_last_error()
+    assert not h.value
+    # distinct before the offset, distinct after: fine; null args rejected
+    L = native.lib()
+    assert L.gp_row_plan_create(None, None, 0, native.DoubleIndex(0, 0), 128, 0) == 1
+    h = ctypes.c_void_p()
+    assert L.gp_row_plan_create(ctypes.byref(h), None, 4, native.DoubleIndex(0, 0), 128, 0) == 1
+    assert L.gp_scatter_add_rows_planned(None, None, None, None) == 1

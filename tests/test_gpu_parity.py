@@ -501,3 +501,106 @@ def test_segmented_rejects_bad_tables(dev):
     rc = native.lib().gp_scatter_add_rows_segmented(t, y.data_ptr(), idx.data_ptr(), 1,
                                                     native.DoubleIndex(0, 0), 128, 1 << 40, None)
     assert rc == native.GP_ERR_INVALID
+
+
+# ---- row plans (compiled DoubleIndex: dense runs + id1-sorted residual) ----------
+
+def _plan_index(rng, kind, n_cache, W):
+    """(index, n_op): identity; a random permutation; or a mix of 3 dense runs
+    (listed out of order), short runs and scattered rows."""
+    if kind == "identity":
+        n = n_cache
+        return np.stack([np.arange(n), np.arange(n)], 1).astype(np.int64), n
+    if kind == "permuted":
+        n = n_cache
+        return np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64), n
+    run = max(1, (4 << 20) // (W * 4))
+    dst = rng.permutation(n_cache)
+    parts, j0, d0 = [], 0, 0
+    for L in (run, 5, run + 3, 1, 2 * run, 17):
+        parts.append(np.stack([j0 + np.arange(L), d0 + np.arange(L)], 1))
+        j0, d0 = j0 + L, d0 + L + 2  # a 2-row gap between destination runs
+    used = np.concatenate([p[:, 1] for p in parts])
+    free = np.setdiff1d(np.arange(n_cache), used)
+    k = min(len(free), 3000)
+    parts.append(np.stack([j0 + np.arange(k), rng.choice(free, k, replace=False)], 1))
+    idx = np.concatenate(parts)
+    return idx[rng.permutation(idx.shape[0])].astype(np.int64), idx.shape[0]
+
+
+@pytest.mark.parametrize("kind", ["identity", "permuted", "mixed"])
+@pytest.mark.parametrize("W,limit_frac,off", [(128, None, (0, 0)), (64, None, (5, 3)),
+                                               (128, 0.83, (0, 0)), (1024, None, (0, 2)),
+                                               (130, None, (0, 0)), (4, 0.5, (1, 1))])
+def test_row_plan_matches_oracle(dev, kind, W, limit_frac, off):
+    """gp_scatter_add_rows_planned / gp_scatter_init_rows_planned equal the
+    oracle's add_rows_from_double_index (init: on zeroed listed rows) bit for
+    bit, with the plan's dense runs, residual rows, offsets and num_vals_limit
+    tails; rows not listed are untouched."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(W * 7 + len(kind) + int((limit_frac or 0) * 10))
+    n_cache = 5 * ((4 << 20) // (W * 4)) + 8000
+    idx, n_op = _plan_index(rng, kind, n_cache - off[1], W)
+    limit = None if limit_frac is None else int((n_op + off[0]) * W * limit_frac) + 3
+    x = rng.standard_normal((n_op + off[0]) * W).astype(np.float32)
+    x[rng.choice(x.size, 300, replace=False)] = np.float32(-0.0)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    plan = rowops.RowPlan(idx, n_op, off, W, limit)
+    info = plan.info()
+    assert info["dense_rows"] + info["residual_rows"] == n_op
+    if kind == "identity" and limit is None:
+        assert info == {"dense_runs": 1, "dense_rows": n_op, "residual_rows": 0}
+    if kind == "mixed" and limit is None:
+        assert info["dense_runs"] == 3
+    # add
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    ty = T(y, dev)
+    plan.add(ty, T(x, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", kind, W)
+    # init: listed destination rows zeroed, then the add
+    e = y.copy()
+    listed = np.zeros(n_cache, bool)
+    listed[idx[:, 1] + off[1]] = True
+    e.reshape(n_cache, W)[listed] = 0.0
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    ty = T(y, dev)
+    plan.init(ty, T(x, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", kind, W)
+    plan.close()
+
+
+def test_row_plan_unaligned_and_side_stream(dev):
+    """Bases 4 B off 16-B alignment (dense runs take the scalar sum form) on a
+    side stream: still bit-exact."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(9)
+    W, n = 128, 20000
+    idx = np.stack([np.arange(n), np.arange(n)], 1).astype(np.int64)
+    idx[12000:] = idx[12000:][rng.permutation(n - 12000)]
+    idx[12000:, 0] = np.arange(12000, n)
+    x = rng.standard_normal(n * W + 1).astype(np.float32)
+    y = rng.standard_normal(n * W + 1).astype(np.float32)
+    e = y[1:].copy()
+    oracle.add_rows_from_double_index(e, x[1:].copy(), idx, (0, 0), W)
+    plan = rowops.RowPlan(idx, row_size=W)
+    assert plan.info()["dense_runs"] == 1
+    ty, tx = T(y, dev), T(x, dev)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        plan.add(ty[1:], tx[1:])
+    s.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()[1:]), bits(e))
+    assert ty[0].item() == y[0]
+
+
+def test_row_plan_rejects_small_buffers(dev):
+    from geeps_amd import rowops
+    idx = np.stack([np.arange(10), np.arange(10) + 5], 1)
+    plan = rowops.RowPlan(idx, row_size=128)
+    with pytest.raises(ValueError):
+        plan.add(torch.zeros(14 * 128, device=dev), torch.zeros(10 * 128, device=dev))
+    with pytest.raises(ValueError):
+        plan.add(torch.zeros(15 * 128, device=dev), torch.zeros(9 * 128, device=dev))
