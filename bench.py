@@ -3,9 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
-Workload (BASELINE.json north-star target / configs[2]): a 1M-row x 1024 fp32
-parameter table, 8 synthetic clients, the table row-range sharded over the N
-GPUs as N server shards (src/client/clientlib-viter.cpp:674-682).  Client c is
+Workload (BASELINE.json north-star target: the 8-way sum at 1M x 1024; at N = 8
+it is configs[2]'s shape): a 1M-row x 1024 fp32 parameter table, 8 synthetic
+clients, the table row-range sharded over the N GPUs as N server shards
+(src/client/clientlib-viter.cpp:674-682).  Client c is
 hosted on rank c % N; its delta buffer is uniform in [-0.5, 0.5) (seed 1000+c).
 
 A *step* is one device-resident N-way reduction: each shard adds the 8 client
@@ -26,8 +27,13 @@ roofline.achieved = algorithmic HBM bytes of one step ((clients + 2) * shard
         stream; per launch, the same ratio (avg_launch_ms is what rocprofv3
         reports for the kernel).
 cpu_baseline = the oracle's restatement of the reference server arithmetic
-        (sequential vsAdd per client, gcc -O3) on rank 0's host cores, on a
-        bounded 128K-row sample.
+        (sequential vsAdd per client, gcc -O3) on rank 0's host cores, on the
+        full 1M x 1024 table with the same 8 clients: 1 thread, plus the
+        process's CPU share (OMP_NUM_THREADS) as "all_cores".
+Other legs at N = 1 (rank 0): config2 (BASELINE configs[1], 2 clients),
+client_rowops (scatter-add / fused init / gather of the table's 8M RowData
+rows, random and identity DoubleIndex, unplanned and through a row plan),
+host_inclusive (pinned H2D + sum + D2H, serialized and pipelined, full table).
 """
 from __future__ import annotations
 
@@ -45,14 +51,16 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roofline"
-def sum_launch_plan(num_vals: int, num_buckets: int):
-    """(dominant kernel name, launches per step, register tiles) for one N-way
-    sum of num_vals floats, from the library's own launch plan
+def sum_launch_plan(num_vals: int, num_buckets: int) -> dict:
+    """The dominant kernel of one N-way sum of num_vals floats and how many
+    launches of it one sum issues, from the library's own launch plan
     (gp_bucket_sum_sweep_plan): at 3-8 buckets, shards of at least 3 whole
     64-MiB chunks go to bucket_sum_sweep_kernel (the 4 GiB headline shard and
-    its 1/2, 1/4, 1/8 slices are whole chunks, so every launch is one), the
-    rest to bucket_sum_phased_kernel; shards under 4 MiB to bucket_sum_vec_kernel
-    in one launch."""
+    its 1/2, 1/4, 1/8 slices are whole chunks), any rest to
+    bucket_sum_phased_kernel (`other_launches`); at 1-2 buckets the phased
+    kernel takes shards of >= 4 MiB; smaller ones bucket_sum_vec_kernel in one
+    launch.  `launches` counts the dominant kernel only, so a per-launch time
+    or byte figure divides by the launches rocprofv3 averages over."""
     import ctypes
     from geeps_amd import native
     launches, reg_tiles, sweeps = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
@@ -60,10 +68,12 @@ def sum_launch_plan(num_vals: int, num_buckets: int):
         num_vals, num_buckets, ctypes.byref(launches), ctypes.byref(reg_tiles),
         ctypes.byref(sweeps)), "gp_bucket_sum_sweep_plan")
     if sweeps.value > 0:
-        return "bucket_sum_sweep_kernel", launches.value, reg_tiles.value
+        return {"kernel": "bucket_sum_sweep_kernel", "launches": sweeps.value,
+                "other_launches": launches.value - sweeps.value, "reg_tiles": reg_tiles.value}
     if launches.value > 0:
-        return "bucket_sum_phased_kernel", launches.value, reg_tiles.value
-    return "bucket_sum_vec_kernel", 1, None
+        return {"kernel": "bucket_sum_phased_kernel", "launches": launches.value,
+                "other_launches": 0, "reg_tiles": reg_tiles.value}
+    return {"kernel": "bucket_sum_vec_kernel", "launches": 1, "other_launches": 0, "reg_tiles": None}
 
 
 def log(*a):
@@ -82,9 +92,12 @@ def parse(argv=None):
     p.add_argument("--exchange-steps", type=int, default=5)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
-    p.add_argument("--cpu-rows", type=int, default=1 << 17)
+    p.add_argument("--cpu-rows", type=int, default=1 << 20)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-rowops", action="store_true")
+    p.add_argument("--rowops-only", nargs="*", default=None, choices=list(ROWOP_LEGS),
+                   help="run only these client row-op legs (PMC passes)")
+    p.add_argument("--no-config2", action="store_true")
     p.add_argument("--no-hbm-probe", action="store_true")
     p.add_argument("--layout", choices=["arena", "separate"], default="arena",
                    help="HBM layout of buckets + master: one arena (master last) or one "
@@ -218,136 +231,304 @@ def timed_exchange(red, deltas, steps, warmup, world, dev):
     return time.perf_counter() - t0
 
 
-def host_inclusive(rows, W, clients, dev, steps=3):
-    """The path starts and ends in host memory: H2D of the arriving client
-    buckets (pinned), the N-way sum, D2H of the refreshed shard.  Measured on a
-    1/8-size table (128K rows) so the pinned staging stays small."""
+def host_inclusive(rows, W, clients, dev, chunk_rows=16384, steps=2):
+    """The path starts and ends in host memory: the client buckets arrive in
+    pinned host buffers (as from the socket, clientlib-data.cpp:473-476), the
+    refreshed shard leaves to one (recv_row_batch_gpu's H2D is its mirror,
+    :128-130).  Full table (rows x W fp32, `clients` buckets), master resident
+    in HBM.  Three schedules, each timed over `steps` steps after a warm-up:
+      serialized  all H2D, then the N-way sum, then the D2H of the shard;
+      pipelined   rows cut into chunks: H2D of chunk i (copy stream), the sum
+                  of chunk i-1 (compute stream), the D2H of chunk i-2 (a third
+                  stream), 3 device slots of `clients` chunk buffers;
+      copy_bound  the pipelined schedule without the sum: what pinned PCIe
+                  moves in this run, both directions at once."""
     from geeps_amd import rowops
     n = rows * W
-    host = [torch.empty(n, dtype=torch.float32).pin_memory() for _ in range(clients)]
-    for c, h in enumerate(host):
-        h.uniform_(-0.5, 0.5)
-    out = torch.empty(n, dtype=torch.float32).pin_memory()
-    dbuf = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(clients)]
+    cn = chunk_rows * W
+    nchunks = (rows + chunk_rows - 1) // chunk_rows
+    host = [torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(clients)]
+    g = torch.Generator(device=dev)
+    for c, h in enumerate(host):  # synthetic deltas made on the device, copied out once
+        g.manual_seed(1000 + c)
+        h.copy_(torch.rand(n, generator=g, device=dev).sub_(0.5))
+    out = torch.empty(n, dtype=torch.float32, pin_memory=True)
     master = torch.zeros(n, dtype=torch.float32, device=dev)
-    copy = torch.cuda.Stream()
     comp = torch.cuda.current_stream()
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    res = {"rows": rows, "width": W, "clients": clients, "chunk_rows": chunk_rows,
+           "bytes_h2d": clients * n * 4, "bytes_d2h": n * 4}
 
-    def one():
-        # H2D on a copy stream, bucket k's arrival overlapped with nothing else
-        # to keep it simple and honest: all copies, then the sum, then D2H.
-        with torch.cuda.stream(copy):
+    def timed(step):
+        step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    # serialized: every bucket resident first
+    dbuf = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(clients)]
+
+    def serialized():
+        with torch.cuda.stream(s_in):
             for h, d in zip(host, dbuf):
                 d.copy_(h, non_blocking=True)
-        comp.wait_stream(copy)
+        comp.wait_stream(s_in)
         rowops.bucket_sum_apply(master, dbuf)
-        out.copy_(master, non_blocking=True)
-        torch.cuda.synchronize()
+        s_out.wait_stream(comp)
+        with torch.cuda.stream(s_out):
+            out.copy_(master, non_blocking=True)
+        comp.wait_stream(s_out)
 
-    one()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        one()
-    dt = (time.perf_counter() - t0) / steps
-    return {"rows": rows, "width": W, "clients": clients,
-            "ms_per_step": dt * 1e3,
-            "delta_GBps": clients * n * 4 / dt / 1e9,
-            "note": "pinned H2D of all client buckets + one N-way sum + D2H of the shard"}
+    t_ser = timed(serialized)
+    del dbuf
+    torch.cuda.empty_cache()
+    slots = [[torch.empty(cn, dtype=torch.float32, device=dev) for _ in range(clients)]
+             for _ in range(3)]
+    free = [torch.cuda.Event() for _ in range(3)]    # slot k no longer read by a sum
+    landed = [torch.cuda.Event() for _ in range(3)]  # slot k's H2D done
+    summed = [torch.cuda.Event() for _ in range(3)]  # chunk j's sum done (j % 3)
+    for e in free:
+        e.record(comp)
+
+    def pipelined(with_sum=True):
+        for i in range(nchunks + 2):
+            if i < nchunks:  # H2D of chunk i into slot i % 3
+                a, b = i * cn, min(n, (i + 1) * cn)
+                s_in.wait_event(free[i % 3])
+                with torch.cuda.stream(s_in):
+                    for h, d in zip(host, slots[i % 3]):
+                        d[:b - a].copy_(h[a:b], non_blocking=True)
+                landed[i % 3].record(s_in)
+            if 1 <= i <= nchunks:  # sum of chunk i - 1
+                j = i - 1
+                a, b = j * cn, min(n, (j + 1) * cn)
+                comp.wait_event(landed[j % 3])
+                if with_sum:
+                    rowops.bucket_sum_apply(master[a:b], [d[:b - a] for d in slots[j % 3]])
+                free[j % 3].record(comp)
+                summed[j % 3].record(comp)
+            if i >= 2:  # D2H of chunk i - 2
+                j = i - 2
+                a, b = j * cn, min(n, (j + 1) * cn)
+                s_out.wait_event(summed[j % 3])
+                with torch.cuda.stream(s_out):
+                    out[a:b].copy_(master[a:b], non_blocking=True)
+        comp.wait_stream(s_out)
+
+    t_pipe = timed(pipelined)
+    t_copy = timed(lambda: pipelined(False))
+    delta = clients * n * 4
+    for name, t in (("serialized", t_ser), ("pipelined", t_pipe), ("copy_bound", t_copy)):
+        res[name] = {"ms_per_step": round(t * 1e3, 2), "delta_GBps": round(delta / t / 1e9, 2),
+                     "pcie_GBps": round((clients + 1) * n * 4 / t / 1e9, 2)}
+    res["pipelined_vs_copy_bound"] = round(t_copy / t_pipe, 4)
+    res["note"] = ("pinned H2D of every client bucket + device N-way sum + D2H of the shard; "
+                   "delta_GBps = client delta bytes / step time")
+    del host, out, master, slots
+    torch.cuda.empty_cache()
+    return res
 
 
-def rowops_leg(rows, W, dev, reps=5):
+ROWOP_LEGS = ("scatter_add", "scatter_add_planned", "scatter_init", "scatter_init_planned",
+              "gather")
+
+
+def _time_calls(fn, reps, stream):
+    fn()  # warm-up
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fn()
+        b.record(stream)
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    return sum(ms) / len(ms)
+
+
+def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None):
     """The client half of the path at the same table size: the 1M x 1024 table
-    through the 128-float API is 8M RowData rows; one Update of all of them is a
-    row-indexed scatter-add into the oplog over a random-permutation DoubleIndex
-    (reference add_rows_from_double_index_gpu, row-op-util.cu:109-142), and one
-    Read is the gather back (assign_rows_to_double_index_gpu, :39-72).
-    Algorithmic bytes per launch: scatter-add 3*n*512 + 16*n, gather 2*n*512 + 16*n."""
+    through the 128-float API is R = 8M RowData rows.  Per DoubleIndex
+    (random permutation of the destinations, and identity -- libgeeps' cache
+    rows are in first-access order, so its real indexes are long runs):
+      scatter_add          gp_scatter_add_rows: index read on device every call
+                           (reference add_rows_from_double_index_gpu, row-op-util.cu:109-142)
+      scatter_add_planned  the same through a gp_row_plan (what libgeeps runs)
+      scatter_init         gp_scatter_init_rows: fused zerofy + add (common-util.hpp:445-456 + a3)
+      scatter_init_planned the same through the plan
+      gather               gp_gather_rows (assign_rows_to_double_index_gpu, :39-72)
+    Algorithmic bytes per call: add 3*R*512 + 16*R, init / gather
+    2*R*512 + 16*R (rows + the 16-B DoubleIndex entries)."""
     from geeps_amd import rowops
     R = rows * W // 128
+    stream = torch.cuda.current_stream()
     g = torch.Generator(device=dev)
     g.manual_seed(5)
-    perm = torch.randperm(R, generator=g, device=dev)
-    idx = torch.stack([torch.arange(R, device=dev), perm], 1).contiguous()
     x = torch.rand(R * 128, generator=g, device=dev)
     y = torch.zeros(R * 128, device=dev)
-    stream = torch.cuda.current_stream()
     out = {}
-    for name, fn, nbytes in (
-            ("scatter_add", rowops.add_rows_from_double_index_gpu, 3 * R * 512 + 16 * R),
-            ("gather", rowops.assign_rows_to_double_index_gpu, 2 * R * 512 + 16 * R)):
-        fn(y, x, idx, R, (0, 0), 128, R * 128, validate=False)  # warm-up
-        ms = []
-        for _ in range(reps):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            fn(y, x, idx, R, (0, 0), 128, R * 128, validate=False)
-            b.record(stream)
-            b.synchronize()
-            ms.append(a.elapsed_time(b))
-        avg = sum(ms) / len(ms)
-        gbps = nbytes / (avg / 1e3) / 1e9
-        out[name] = {"rows": R, "row_size": 128, "index": "random permutation",
-                     "avg_kernel_ms": round(avg, 4), "GBps": round(gbps, 1),
-                     "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_launch": nbytes,
-                     "traffic": load_traffic(f"rowops_{name}_r{R}_w128")}
+    for kind in indexes:
+        if kind == "random":
+            dst = torch.randperm(R, generator=g, device=dev)
+        else:
+            dst = torch.arange(R, device=dev)
+        idx = torch.stack([torch.arange(R, device=dev), dst], 1).contiguous()
+        plan = rowops.RowPlan(idx, R, (0, 0), 128, R * 128)
+        info = plan.info()
+        legs = {}
+        for name in ROWOP_LEGS:
+            if only and name not in only:
+                continue
+            planned = name.endswith("_planned")
+            nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * R
+            if name == "scatter_add":
+                fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
+                                                                   validate=False)
+                kernel = "row_op_kernel"
+            elif name == "scatter_init":
+                fn = lambda: rowops.init_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
+                                                                    validate=False)
+                kernel = "row_wave_kernel"
+            elif name == "gather":
+                fn = lambda: rowops.assign_rows_to_double_index_gpu(x, y, idx, R, (0, 0), 128, R * 128,
+                                                                    validate=False)
+                kernel = "row_wave_kernel"
+            else:
+                fn = (lambda: plan.add(y, x)) if name == "scatter_add_planned" else (lambda: plan.init(y, x))
+                kernel = "row_wave_kernel"
+            launches = 1
+            avg = _time_calls(fn, reps, stream)
+            gbps = nbytes / (avg / 1e3) / 1e9
+            leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),
+                   "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes": nbytes, "kernel": kernel,
+                   "launches": launches, "avg_launch_ms": round(avg / launches, 5)}
+            if planned:
+                leg["plan"] = info
+            traffic = load_traffic(f"rowops_{name}_{kind}_r{R}_w128", kernel)
+            if traffic:
+                leg["traffic"] = traffic["bytes_per_launch"] * launches
+                leg["traffic_source"] = traffic
+            legs[name] = leg
+        out[kind] = dict(rows=R, row_size=128, index=f"{kind} permutation of destinations"
+                         if kind == "random" else "identity", **legs)
+        plan.close()
+        del idx, dst
     return out
 
 
+def cpu_threads() -> tuple[int, str]:
+    """Threads for the all-cores CPU figure: the CPU share this process may
+    use (OMP_NUM_THREADS, set to the box's per-GPU share; else the affinity
+    mask), and how it was chosen."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        t = min(int(env), aff)
+        return t, f"OMP_NUM_THREADS={env} (this process's CPU share; nproc={nproc}, affinity={aff})"
+    return aff, f"affinity mask (nproc={nproc})"
+
+
 def cpu_baseline(rows, W, clients, seconds):
-    """The oracle's restatement of the reference server arithmetic, timed on the
-    host (bounded sample).  1 thread = the reference's one server thread per
-    channel (src/client/clientlib.cpp:102-105)."""
+    """The oracle's restatement of the reference server arithmetic (sequential
+    vsAdd per client message, gcc -O3, oracle/oracle.c) timed on the host, on
+    the FULL table: `clients` synthetic client buffers of rows x W fp32 and a
+    master of the same size.  1 thread = the reference's one tablet-server
+    thread per channel (src/client/clientlib.cpp:102-105); the all-cores
+    figure splits rows over threads as num_comm_channels server threads do
+    (clientlib.cpp:216-224)."""
     import numpy as np
     from oracle import oracle
     n = rows * W
-    ups = [oracle.synthetic_delta(c, n) for c in range(clients)]
+    threads, how = cpu_threads()
+    t0 = time.perf_counter()
+    ups = [oracle.fill_uniform(np.empty(n, np.float32), 1000 + c, threads) for c in range(clients)]
     master = np.zeros(n, np.float32)
-    oracle.apply_updates(master, ups)  # warm the pages
+    oracle.apply_updates(master, ups, threads=threads)  # fault the pages in
+    setup = time.perf_counter() - t0
     rounds, t0 = 0, time.perf_counter()
     while True:
         oracle.apply_updates(master, ups)
         rounds += 1
         dt = time.perf_counter() - t0
-        if dt >= seconds:
+        if dt >= seconds or rounds >= 50:
             break
     per = dt / rounds
     res = {"value": clients * n * 4 / per / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
-           "sample": f"{rows} rows x {W} fp32, {clients} clients applied sequentially "
-                     f"(oracle_apply_updates, gcc -O3), {rounds} rounds in {dt:.1f} s"}
-    threads = min(16, os.cpu_count() or 1)
+           "sample": f"full table: {rows} rows x {W} fp32, {clients} clients applied sequentially "
+                     f"per message (oracle_apply_updates, gcc -O3), {rounds} rounds in {dt:.1f} s",
+           "ms_per_round": round(per * 1e3, 1)}
     if threads > 1:
         t0, r2 = time.perf_counter(), 0
-        while time.perf_counter() - t0 < seconds / 3:
+        while True:
             oracle.apply_updates(master, ups, threads=threads)
             r2 += 1
-        per2 = (time.perf_counter() - t0) / r2
-        res["all_cores"] = {"value": clients * n * 4 / per2 / 1e9, "cores": threads,
+            dt2 = time.perf_counter() - t0
+            if dt2 >= seconds / 2 or r2 >= 100:
+                break
+        per2 = dt2 / r2
+        res["all_cores"] = {"value": clients * n * 4 / per2 / 1e9, "unit": "GB/s", "cores": threads,
+                            "threads_from": how, "ms_per_round": round(per2 * 1e3, 1),
                             "note": "row range split over threads = num_comm_channels "
                                     "server threads (clientlib.cpp:216-224)"}
+    res["setup_s"] = round(setup, 1)
     try:
         with open("/proc/cpuinfo") as f:
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
         res["cpu_model"] = model
-        res["nproc"] = os.cpu_count()
     except OSError:
         pass
+    res["nproc"] = os.cpu_count()
+    del ups, master
     return res
 
 
-def load_traffic(workload_key, kernel=None):
-    """PMC HBM bytes per launch for this workload from profiles/pmc_traffic.json;
-    None when absent or measured on another kernel than the one this run's
-    plan launches (a stale entry would not be this kernel's traffic)."""
+def load_traffic(workload_key, kernel):
+    """PMC HBM bytes per launch of `kernel` for this workload, from
+    profiles/pmc_traffic.json (written by scripts/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench), with where
+    it came from: {"bytes_per_launch", "kernel" (the name the counters were
+    filtered on), "source", "emulated" (true: an N-GPU rank's work measured on
+    one GPU), "round"}.  None when absent or measured on another kernel than
+    the one this run launches."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            data = json.load(f)
-        entry = data.get(workload_key)
-        if entry is None or (kernel is not None and kernel not in entry.get("kernel", "")):
+            entry = json.load(f).get(workload_key)
+        if entry is None or kernel not in entry.get("kernel", ""):
             return None
-        return float(entry["hbm_bytes_per_launch"])
+        return {"bytes_per_launch": float(entry["hbm_bytes_per_launch"]),
+                "kernel": entry["kernel"], "source": f"profiles/pmc_traffic.json[{workload_key}]",
+                "emulated": bool(entry.get("emulated", False)),
+                "round": entry.get("round")}
     except (OSError, ValueError, KeyError):
         return None
+
+
+def config2_leg(deltas, master, dev, reps=5):
+    """BASELINE configs[1]: the same 1M x 1024 shard, 2 client buckets (the
+    first two resident deltas, client order 0, 1) summed into the master by one
+    gp_bucket_sum_apply.  Algorithmic bytes (2 + 2) * shard bytes."""
+    from geeps_amd import rowops
+    n = master.numel()
+    plan = sum_launch_plan(n, 2)
+    stream = torch.cuda.current_stream()
+    avg = _time_calls(lambda: rowops.bucket_sum_apply(master, deltas[:2]), reps, stream)
+    nbytes = 4 * n * 4
+    gbps = nbytes / (avg / 1e3) / 1e9
+    rows = n // 1024
+    return {"workload": f"configs[1]: 2 clients, {rows} rows x 1024 fp32, 1 shard, device-resident",
+            "ms": round(avg, 4), "GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "delta_GBps": round(2 * n * 4 / (avg / 1e3) / 1e9, 1), "bytes": nbytes,
+            "kernel": plan["kernel"], "launches": plan["launches"],
+            "avg_launch_ms": round(avg / plan["launches"], 5),
+            "traffic_source": load_traffic(f"r{rows}_w1024_c2_g1", plan["kernel"])}
 
 
 def main(argv=None, backend="nccl", apply_fn=None):
@@ -379,12 +560,13 @@ def main(argv=None, backend="nccl", apply_fn=None):
     wall = max_over_ranks(wall, world, dev)
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     avg_kernel_ms_max = max_over_ranks(avg_kernel_ms, world, dev)
-    kernel_name, launches, reg_tiles = sum_launch_plan(L.local_vals, min(C, 8))
+    plan = sum_launch_plan(L.local_vals, min(C, 8))
+    kernel_name, launches = plan["kernel"], plan["launches"]
     step_s = wall / args.steps
     delta_bytes = C * R * W * 4
     value = delta_bytes / step_s / 1e9
     shard_bytes = L.local_vals * 4
-    algo_bytes = (C + 2) * shard_bytes           # per launch on this rank
+    algo_bytes = (C + 2) * shard_bytes           # per step on this rank
     achieved = algo_bytes / (avg_kernel_ms / 1e3) / 1e9
     achieved_min = max_over_ranks(-achieved, world, dev) * -1  # slowest rank
 
@@ -412,22 +594,27 @@ def main(argv=None, backend="nccl", apply_fn=None):
     cpu = None
     rowops_res = None
     probe = None
+    config2 = None
     if rank == 0 and world == 1 and dev.type == "cuda":
         if not args.no_hbm_probe:
             log("[rank 0] HBM copy probe")
             scratch = torch.empty_like(deltas[0])
             probe = hbm_copy_probe(deltas[0], scratch)
             del scratch
+        if not args.no_config2 and C >= 2 and master is not None:
+            log("[rank 0] configs[1] leg (2 clients)")
+            config2 = config2_leg(deltas, master, dev)
         del deltas
         red = None
+        master = None
         torch.cuda.empty_cache()
         if not args.no_rowops:
             log("[rank 0] client row-op leg")
-            rowops_res = rowops_leg(R, W, dev)
+            rowops_res = rowops_leg(R, W, dev, only=args.rowops_only)
             torch.cuda.empty_cache()
         if not args.no_host_inclusive:
             log("[rank 0] host-inclusive leg")
-            host_inc = host_inclusive(R // 8, W, C, dev)
+            host_inc = host_inclusive(R, W, C, dev)
         if not args.no_cpu_baseline:
             log("[rank 0] cpu baseline leg")
             cpu = cpu_baseline(min(args.cpu_rows, R), W, C, args.cpu_seconds)
@@ -449,7 +636,9 @@ def main(argv=None, backend="nccl", apply_fn=None):
             "data": "synthetic (uniform [-0.5,0.5) deltas, seed 1000+client)",
             "config": {"workload": f"{C}-way fp32 row reduction into the master table, "
                                    f"{R} rows x {W} fp32, {world} server shard(s), "
-                                   f"device-resident (BASELINE.json north-star / configs[2])",
+                                   f"device-resident (BASELINE.json north-star target: "
+                                   f"8-way at 1M x 1024"
+                                   + ("; configs[2] shape at 8 shards)" if world > 1 else ")"),
                        "rows": R, "row_width": W, "clients": C, "shards": world,
                        "exchange": args.exchange if world > 1 else "none (resident)",
                        "hbm_layout": args.layout,
@@ -457,10 +646,12 @@ def main(argv=None, backend="nccl", apply_fn=None):
             "roofline": {"bound": "hbm", "achieved": round(achieved_min, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_min / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic,
                          "kernel": kernel_name,
                          "launches_per_step": launches,
-                         "register_tiles": reg_tiles,
+                         "other_launches_per_step": plan["other_launches"],
+                         "register_tiles": plan["reg_tiles"],
                          # HIP events around each step's launches on their stream
                          "avg_kernel_ms": round(avg_kernel_ms_max, 4),
                          # per launch, comparable with rocprofv3's average for the kernel
@@ -476,6 +667,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
         if probe:
             line["roofline"]["same_box_copy_GBps"] = probe["copy_GBps"]
             line["hbm_probe"] = probe
+        if config2:
+            line["config2"] = config2
         if host_inc:
             line["host_inclusive"] = host_inc
         if rowops_res:

@@ -168,8 +168,7 @@ def assign_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, inde
 
 class RowPlan:
     """A scatter DoubleIndex compiled once (gp_row_plan_create): the rows in
-    destination order, dense id0/id1 runs of >= 4 MiB moved by the dense sum
-    kernels, the rest by the row kernels over an id1-sorted device index.
+    destination (id1) order on the device, run by the wave-map row kernel.
 
     ``index``: (n, 2) int64 array or tensor (copied to the host once), as for
     add_rows_from_double_index_gpu; ``index_offset`` and ``num_vals_limit``
@@ -207,10 +206,10 @@ class RowPlan:
                                               self.row_size, self.limit), "gp_row_plan_create")
 
     def info(self) -> dict:
-        a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
-        check(native.lib().gp_row_plan_info(self._h, ctypes.byref(a), ctypes.byref(b),
-                                            ctypes.byref(c)), "gp_row_plan_info")
-        return {"dense_runs": a.value, "dense_rows": b.value, "residual_rows": c.value}
+        a, b = ctypes.c_size_t(), ctypes.c_size_t()
+        check(native.lib().gp_row_plan_info(self._h, ctypes.byref(a), ctypes.byref(b)),
+              "gp_row_plan_info")
+        return {"rows": a.value, "runs": b.value}
 
     def _run(self, fn, y, x, stream, what):
         _dev_f32(y, "rows_y")

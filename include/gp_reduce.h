@@ -20,8 +20,9 @@
  *     (src/common/gpu-util/device_alternate.hpp:16-28).  The C++ layer above
  *     turns a non-zero status into an abort with that message.
  *
- * All functions are re-entrant and keep no global state besides the
- * thread-local error string.
+ * All functions are re-entrant.  Global state: the thread-local error string,
+ * and per-device / per-kernel launch facts cached on first use (CU count,
+ * resident blocks per CU), which never change once read.
  */
 #ifndef GP_REDUCE_H_
 #define GP_REDUCE_H_
@@ -119,27 +120,24 @@ int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
  * Row plans: a scatter DoubleIndex compiled once, for ops whose index is fixed
  * (libgeeps builds one per op and channel at FinishVirtualIteration, where the
  * reference builds the op's device DoubleIndex: vi_create_double_index,
- * src/client/clientlib-viter.cpp:817-883).  The plan visits the rows in
- * destination (id1) order -- bit-neutral, since destinations are distinct --
- * and moves runs where id0 and id1 both step by one (whole rows, at least
- * 4 MiB) as dense ranges through the bucket-sum kernels; the other rows keep a
- * device index, sorted by id1, for the row kernels.  Results are bit-identical
- * to gp_scatter_add_rows / gp_scatter_init_rows over the same index, offset
- * and num_vals_limit.
+ * src/client/clientlib-viter.cpp:817-883).  The plan keeps the rows in
+ * destination (id1) order with the offsets applied -- bit-neutral, since
+ * destinations are distinct -- so the scatter's read-modify-write side walks
+ * y front to back.  Results are bit-identical to gp_scatter_add_rows /
+ * gp_scatter_init_rows over the same index, offset and num_vals_limit.
  * ------------------------------------------------------------------------- */
 typedef struct gp_row_plan_s *gp_row_plan;
 
 /* Build a plan from a HOST copy of `num_rows` DoubleIndex entries; `offset`
  * and `num_vals_limit` are baked in (same meaning as gp_scatter_add_rows).
- * The plan's device index lives on the current device.  GP_ERR_INVALID if a
- * destination row (id1 + offset.id1) repeats. */
+ * The plan's device index lives on the current device, and the plan runs only
+ * there.  GP_ERR_INVALID if a destination row (id1 + offset.id1) repeats. */
 int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
                        gp_double_index offset, size_t row_size, size_t num_vals_limit);
 int gp_row_plan_destroy(gp_row_plan plan);
-/* How the plan splits its rows: dense runs, rows in them, rows left to the
- * row kernels (for tests and measurement). */
-int gp_row_plan_info(gp_row_plan plan, size_t *dense_runs, size_t *dense_rows,
-                     size_t *residual_rows);
+/* The plan's rows, and how many maximal runs they form in destination order
+ * where id0 and id1 both step by one (1 for an identity-like index). */
+int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *runs);
 /* gp_scatter_add_rows(y, x, index, ...) through the plan (a3:
  * add_rows_from_double_index_gpu, src/common/row-op-util.cu:109-142). */
 int gp_scatter_add_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s);

@@ -155,3 +155,47 @@ int oracle_apply_updates_mt(float *master, const float *const *updates,
   for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
   return 0;
 }
+
+/* Synthetic deltas for the CPU baseline at full table size (bench.py): fp32
+ * uniform in [-0.5, 0.5) from a per-(seed, block) splitmix64 stream, filled
+ * by `threads` threads.  Not the reference's arithmetic (it has no data
+ * generator); only the timed oracle_apply_updates* above is. */
+typedef struct {
+  float *p;
+  int64_t begin, end;
+  uint64_t seed;
+} oracle_fill_job;
+
+static uint64_t oracle_splitmix(uint64_t *s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static void *oracle_fill_run(void *arg) {
+  oracle_fill_job *j = (oracle_fill_job *)arg;
+  uint64_t s = j->seed ^ ((uint64_t)j->begin * 0xD1B54A32D192ED03ull);
+  for (int64_t i = j->begin; i < j->end; ++i)
+    j->p[i] = (float)(oracle_splitmix(&s) >> 40) * (1.0f / 16777216.0f) - 0.5f;
+  return NULL;
+}
+
+int oracle_fill_uniform(float *p, int64_t n, uint64_t seed, int threads) {
+  enum { kMaxThreads = 256 };
+  if (threads < 1) threads = 1;
+  if (threads > kMaxThreads) threads = kMaxThreads;
+  pthread_t tid[kMaxThreads];
+  oracle_fill_job job[kMaxThreads];
+  const int64_t div = n / threads, res = n % threads;
+  for (int t = 0; t < threads; ++t) {
+    const int64_t b = div * t + (res > t ? t : res);
+    job[t].p = p;
+    job[t].begin = b;
+    job[t].end = b + div + (res > t ? 1 : 0);
+    job[t].seed = seed;
+    if (pthread_create(&tid[t], NULL, oracle_fill_run, &job[t]) != 0) return -2;
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  return 0;
+}

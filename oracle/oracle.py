@@ -46,6 +46,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_apply_updates_mt.restype = ctypes.c_int
         L.oracle_server_partition.argtypes = [ctypes.c_size_t, ctypes.c_size_t, _u64p, _u64p]
         L.oracle_server_partition.restype = None
+        L.oracle_fill_uniform.argtypes = [_fp, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int]
+        L.oracle_fill_uniform.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -120,3 +122,12 @@ def synthetic_delta(client_id: int, num_vals: int) -> np.ndarray:
     """fp32 deltas uniform in [-0.5, 0.5), seed 1000 + client_id."""
     rng = np.random.default_rng(1000 + client_id)
     return (rng.random(num_vals, dtype=np.float32) - np.float32(0.5)).astype(np.float32)
+
+
+def fill_uniform(out: np.ndarray, seed: int, threads: int = 1) -> np.ndarray:
+    """Fill a float32 array with uniform [-0.5, 0.5) values, multi-threaded
+    (synthetic deltas for the full-size CPU baseline; bench.py)."""
+    assert out.dtype == np.float32 and out.flags.c_contiguous
+    if lib().oracle_fill_uniform(_f(out), out.size, seed, threads) != 0:
+        raise RuntimeError("oracle_fill_uniform failed")
+    return out

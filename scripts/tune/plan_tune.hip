@@ -8,8 +8,10 @@
 //                     loaded before this iteration's rows move (here only)
 //   add/init  sorted  : the same permutation sorted by id1 (what a plan's
 //                     residual holds), row_op_kernel / row_wave_kernel / pf
-//   add/init  ident-dense : identity index as one dense run (launch_bucket_sum_nb
-//                     <1> / <1, ZIN>: the plan's dense form)
+//   add  ident-dense : identity index as one dense run (launch_bucket_sum_nb<1>;
+//                     the plan's dense form while it had one.  An init twin of
+//                     it, out = 0.0f + x through the sum kernels with the
+//                     master read dropped, ran at 71 %: profiles/r02/plan_tune*.txt)
 //   copy      : hipMemcpy D2D of 4 GiB (1 read + 1 write ceiling)
 // Interleaved rounds in one process, median per variant.  Usage: plan_tune [rounds]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
@@ -235,6 +237,14 @@ int main(int argc, char **argv) {
         launch_row_op<kInitFrom>(y, x, ix, R, {0, 0}, W, ~size_t(0), 0);
     };
   };
+  auto prod_sorted = [&](int op, const gp_double_index *ix) {
+    return [=] {
+      if (op == kAddFrom)
+        launch_row_op<kAddFrom>(y, x, ix, R, {0, 0}, W, ~size_t(0), 0, true);
+      else
+        launch_row_op<kInitFrom>(y, x, ix, R, {0, 0}, W, ~size_t(0), 0, true);
+    };
+  };
   auto wave = [&](int op, const gp_double_index *ix) {
     return [=] {
       size_t grid = std::min((R + kBlock - 1) / kBlock, cap);
@@ -313,11 +323,6 @@ int main(int argc, char **argv) {
     b.p[0] = x;
     launch_bucket_sum_nb<1>(y, y, b, n, 0);
   };
-  auto dense_init = [&] {
-    BucketPtrs b = {};
-    b.p[0] = x;
-    launch_bucket_sum_nb<1, true>(y, nullptr, b, n, 0);
-  };
   auto copy = [&] { CK(hipMemcpyAsync(y, x, n * 4, hipMemcpyDeviceToDevice, 0)); };
   const double add_b = 3.0 * n * 4 + 16.0 * R, init_b = 2.0 * n * 4 + 16.0 * R;
   struct V {
@@ -327,23 +332,20 @@ int main(int argc, char **argv) {
   };
   const double gat_b = 2.0 * n * 4 + 16.0 * R;
   std::vector<V> vs = {
-      {"add  rand   row_op (prod /8)", rowop(kAddFrom, rnd), add_b},
-      {"add  rand   wave8 ntld+st /3", wvar(kAddFrom, rnd, 8, true, true, 3), add_b},
-      {"add  rand   wave8 plain /3", wvar(kAddFrom, rnd, 8, false, false, 3), add_b},
-      {"add  rand   wave8 ntst /3", wvar(kAddFrom, rnd, 8, false, true, 3), add_b},
-      {"add  rand   wave4 plain /5", wvar(kAddFrom, rnd, 4, false, false, 5), add_b},
+      {"add  rand   row_op (prod)", rowop(kAddFrom, rnd), add_b},
       {"add  ident  dense", dense_add, 3.0 * n * 4},
-      {"add  ident  wave8 ntld+st /3", wvar(kAddFrom, idn, 8, true, true, 3), add_b},
+      {"add  ident  prod sorted (wave)", prod_sorted(kAddFrom, idn), add_b},
+      {"add  sorted prod sorted (wave)", prod_sorted(kAddFrom, srt), add_b},
       {"add  sorted wave8 ntld+st /3", wvar(kAddFrom, srt, 8, true, true, 3), add_b},
-      {"add  sorted wave8 ntst /3", wvar(kAddFrom, srt, 8, false, true, 3), add_b},
-      {"gath rand   wave8 (prod /8)", rowop(kAssignTo, rnd), gat_b},
-      {"gath rand   wave8 /2", gath(rnd, 2), gat_b},
-      {"gath rand   wave8 /4", gath(rnd, 4), gat_b},
-      {"gath ident  wave8 /2", gath(idn, 2), gat_b},
-      {"init rand   row_op (prod /8)", rowop(kInitFrom, rnd), init_b},
+      {"gath rand   prod (wave /8)", rowop(kAssignTo, rnd), gat_b},
+      {"gath rand   wave /4", gath(rnd, 4), gat_b},
+      {"gath rand   wave /8", gath(rnd, 8), gat_b},
+      {"gath ident  prod (wave /8)", rowop(kAssignTo, idn), gat_b},
+      {"gath ident  wave /4", gath(idn, 4), gat_b},
+      {"init rand   prod (wave)", rowop(kInitFrom, rnd), init_b},
       {"init rand   wave8 ntst /4", wvar(kInitFrom, rnd, 8, false, true, 4), init_b},
-      {"init ident  dense ZIN", dense_init, 2.0 * n * 4},
-      {"init ident  wave8 ntst /4", wvar(kInitFrom, idn, 8, false, true, 4), init_b},
+      {"init ident  prod (wave)", rowop(kInitFrom, idn), init_b},
+      {"init sorted prod (wave)", rowop(kInitFrom, srt), init_b},
       {"init sorted wave8 ntst /4", wvar(kInitFrom, srt, 8, false, true, 4), init_b},
       {"copy D2D 4 GiB", copy, 2.0 * n * 4},
   };
