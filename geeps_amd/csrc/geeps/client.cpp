@@ -80,6 +80,15 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
   GP_CHECK_MSG(config_.port_list.empty() || config_.port_list.size() >= num_processes_,
                "port_list must have one port per host");
   GP_CALL(gp_get_device(&device_));
+  GP_CALL(gp_device_pci_bus_id(device_, pci_bus_id_, sizeof pci_bus_id_));
+  // Test hooks (fault injection; unset in production): GEEPS_STAGE_PEER_UPDATES=1
+  // stages same-node peers' buckets even on one GPU (the cross-GPU path on a
+  // one-GPU box); GEEPS_TEST_READER_DELAY_US=D delays every refresh a reader
+  // thread takes (a lagging client under SSP).
+  const char *stage = std::getenv("GEEPS_STAGE_PEER_UPDATES");
+  force_stage_ = stage && std::string(stage) == "1";
+  const char *delay = std::getenv("GEEPS_TEST_READER_DELAY_US");
+  reader_delay_us_ = delay ? std::atoi(delay) : 0;
   // Same-node peers exchange rows device to device through IPC-mapped HBM
   // (xGMI between GPUs); GEEPS_TRANSPORT=tcp forces the socket data path.
   const char *transport = std::getenv("GEEPS_TRANSPORT");
@@ -109,6 +118,7 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->client_fd.assign(num_processes_, -1);
     ch->ipc_oplogs.resize(num_processes_);
     ch->ipc_client.assign(num_processes_, 0);
+    ch->stage_from.assign(num_processes_, 0);
     ch->version_sent.assign(num_processes_, std::vector<std::set<int>>(config_.num_tables));
     ch->client_done.assign(num_processes_, 0);
     channels_[c] = std::move(ch);
@@ -146,9 +156,12 @@ void ClientLib::start_network() {
       std::string err;
       const int fd = connect_tcp(config_.host_list[s], port_of(s, ch.id), connect_timeout_s(), &err);
       GP_CHECK_MSG(fd >= 0, err);
-      // third word: this client takes same-node refreshes in place (IPC)
-      const uint32_t hello[3] = {kHelloCmd, process_id_, ipc_to(s) ? 1u : 0u};
-      GP_CHECK(send_frame(fd, {Part{hello, sizeof hello}}));
+      HelloMsg hello{};
+      hello.cmd = kHelloCmd;
+      hello.process_id = process_id_;
+      hello.ipc = ipc_to(s) ? 1u : 0u;  // takes same-node refreshes in place
+      std::memcpy(hello.pci_bus_id, pci_bus_id_, sizeof hello.pci_bus_id);
+      GP_CHECK(send_frame(fd, {Part{&hello, sizeof hello}}));
       ch.server_fd[s] = fd;
       ch.client_readers.emplace_back([this, &ch, s, fd] { client_reader(ch, s, fd); });
     }
@@ -163,15 +176,17 @@ void ClientLib::server_accept_loop(Channel &ch, int expected) {
     std::vector<RecvPart> parts;
     std::vector<std::vector<char>> scratch;
     GP_CHECK(recv_frame(fd, parts, scratch, nullptr, nullptr));
-    GP_CHECK(parts.size() == 1 && parts[0].size == 12);
-    uint32_t hello[3];
-    std::memcpy(hello, parts[0].data, 12);
-    GP_CHECK_EQ(hello[0], kHelloCmd);
-    GP_CHECK_LT(hello[1], num_processes_);
-    GP_CHECK_MSG(ch.client_fd[hello[1]] < 0, "duplicate client " << hello[1]);
-    ch.client_fd[hello[1]] = fd;
-    ch.ipc_client[hello[1]] = hello[2] && ipc_to(hello[1]);
-    const uint32_t cid = hello[1];
+    GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(HelloMsg));
+    HelloMsg hello;
+    std::memcpy(&hello, parts[0].data, sizeof hello);
+    GP_CHECK_EQ(hello.cmd, kHelloCmd);
+    const uint32_t cid = hello.process_id;
+    GP_CHECK_LT(cid, num_processes_);
+    GP_CHECK_MSG(ch.client_fd[cid] < 0, "duplicate client " << cid);
+    ch.client_fd[cid] = fd;
+    ch.ipc_client[cid] = hello.ipc && ipc_to(cid);
+    hello.pci_bus_id[sizeof hello.pci_bus_id - 1] = 0;
+    ch.stage_from[cid] = ipc_to(cid) && (force_stage_ || std::strcmp(hello.pci_bus_id, pci_bus_id_) != 0);
     ch.server_readers.emplace_back([this, &ch, cid, fd] { server_reader(ch, cid, fd); });
   }
 }
@@ -235,7 +250,7 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
         GP_CHECK_MSG(it != mapped.end(), "unmapped oplog buffer " << ref.buffer_id);
         b.device_rows = reinterpret_cast<const float *>(static_cast<const char *>(it->second) +
                                                         ref.offset);
-        b.device_remote = true;
+        b.stage = ch.stage_from[client_id];
       } else {
         GP_CHECK_EQ(parts[2].size, n * kRowBytes);
         b.host_rows = ctx.rows;
@@ -287,6 +302,7 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == SHUTDOWN) break;  // the server will send nothing more
+    if (reader_delay_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(reader_delay_us_));
     GP_CHECK((parts.size() == 3 || parts.size() == 4) &&
              parts[0].size == sizeof(sc_read_row_batch_msg_t));
     sc_read_row_batch_msg_t h;
@@ -573,6 +589,8 @@ void ClientLib::finish_virtual_iteration() {
     op.buffer.resize(std::max<size_t>(1, op.rows.size()) * ROW_DATA_SIZE);
     GP_CALL(gp_zero(op.buffer.data(), op.buffer.size(), channels_[0]->stream->get()));
     planned += op.buffer.bytes();
+    // the device DoubleIndex, and an update op's row plans (a sorted copy)
+    planned += op.rows.size() * sizeof(gp_double_index) * (op.type == OpInfo::PRE_WRITE ? 2 : 1);
     create_double_index(op);
   }
   GP_CALL(gp_device_synchronize());
@@ -659,6 +677,16 @@ void ClientLib::create_double_index(OpInfo &op) {
       GP_CHECK_EQ(hi - lo + 1, (uint64_t)per[c].size());
     }
     flat.insert(flat.end(), per[c].begin(), per[c].end());
+  }
+  // The update ops' oplog accumulate runs through a row plan per channel: the
+  // same rows visited in cache-row order (bit-identical: id1 distinct, checked
+  // above), so the scatter's read-modify-write side walks the oplog in order.
+  if (op.type == OpInfo::PRE_WRITE) {
+    op.plans.resize(num_channels_);
+    for (uint32_t c = 0; c < num_channels_; ++c)
+      if (!per[c].empty())
+        op.plans[c] = std::make_unique<RowPlan>(per[c].data(), per[c].size(), ROW_DATA_SIZE,
+                                                op.num_vals_limit);
   }
   op.index.resize(std::max<size_t>(1, flat.size()));
   if (!flat.empty())
@@ -798,23 +826,23 @@ void ClientLib::update_batch(int handle) {
     const bool fused = started_ && ch.init_ok[pre.table_id];
     auto oplog = get_oplog(pc, clock, ch.stream->get(), /*zero=*/!fused);
     if (n) {
-      const gp_double_index *idx = pre.index.data() + pre.ch_start[ch.id];
+      // add_rows_from_double_index_gpu (clientlib-data.cpp:385-394) through the
+      // op's row plan for this channel (its index, offset 0, num_vals_limit)
+      const gp_row_plan plan = pre.plans[ch.id]->get();
       if (fused)
-        GP_CALL(gp_scatter_init_rows(oplog->data(), pre.buffer.data(), idx, n,
-                                     gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
-                                     ch.stream->get()));
+        GP_CALL(gp_scatter_init_rows_planned(oplog->data(), pre.buffer.data(), plan,
+                                             ch.stream->get()));
       else
-        GP_CALL(gp_scatter_add_rows(oplog->data(), pre.buffer.data(), idx, n,
-                                    gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
-                                    ch.stream->get()));
+        GP_CALL(gp_scatter_add_rows_planned(oplog->data(), pre.buffer.data(), plan,
+                                            ch.stream->get()));
       if (config_.read_my_writes && pc.segmented)
-        GP_CALL(gp_scatter_add_rows_segmented(&pc.segs, pre.buffer.data(), idx, n,
+        GP_CALL(gp_scatter_add_rows_segmented(&pc.segs, pre.buffer.data(),
+                                              pre.index.data() + pre.ch_start[ch.id], n,
                                               gp_double_index{0, 0}, ROW_DATA_SIZE,
                                               pre.num_vals_limit, ch.stream->get()));
       else if (config_.read_my_writes)
-        GP_CALL(gp_scatter_add_rows(pc.data.data(), pre.buffer.data(), idx, n,
-                                    gp_double_index{0, 0}, ROW_DATA_SIZE, pre.num_vals_limit,
-                                    ch.stream->get()));
+        GP_CALL(gp_scatter_add_rows_planned(pc.data.data(), pre.buffer.data(), plan,
+                                            ch.stream->get()));
     }
     ch.stream->sync();
   }

@@ -62,6 +62,9 @@ struct OpInfo {
   bool table_last_write = false;
   DeviceArray<gp_double_index> index;  // channel-major
   std::vector<size_t> ch_start, ch_size;
+  // PRE_WRITE: per channel, the channel's slice of `index` as a row plan
+  // (destination-sorted), which the oplog scatter-add / fused init run through
+  std::vector<std::unique_ptr<RowPlan>> plans;
   DeviceArray<float> buffer;           // READ / PRE_WRITE op buffer
   float *local_ptr = nullptr;          // local READ: GPU-resident storage
   bool in_use = false;
@@ -154,6 +157,9 @@ struct Channel {
   // IPC handles it already has
   std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
   std::vector<uint8_t> ipc_client;                       // [client]
+  // [client]: its oplog lives on another GPU: stage its slices into local HBM
+  // (a peer copy over xGMI on the server's copy stream) before the sum
+  std::vector<uint8_t> stage_from;
   std::vector<std::vector<std::set<int>>> version_sent;  // [client][table]
   // [client]: its SHUTDOWN arrived (it reads no more, and its ACKs stop)
   std::vector<uint8_t> client_done;
@@ -220,6 +226,9 @@ class ClientLib {
   const uint32_t num_processes_;
   const uint32_t num_channels_;
   int device_ = 0;
+  char pci_bus_id_[32] = {};  // this process's GPU (gp_device_pci_bus_id)
+  bool force_stage_ = false;  // GEEPS_STAGE_PEER_UPDATES=1 (test hook)
+  int reader_delay_us_ = 0;   // GEEPS_TEST_READER_DELAY_US (test hook)
   std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)
 
   std::vector<OpInfo> opseq_;

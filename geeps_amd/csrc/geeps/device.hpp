@@ -119,6 +119,25 @@ class PinnedArray {
   size_t n_ = 0;
 };
 
+// A row plan (gp_row_plan_create): a scatter DoubleIndex compiled once, on
+// the current device, for the ops whose index is fixed after
+// FinishVirtualIteration.
+class RowPlan {
+ public:
+  RowPlan(const gp_double_index *host_index, size_t n, size_t row_size, size_t num_vals_limit) {
+    GP_CALL(gp_row_plan_create(&p_, host_index, n, gp_double_index{0, 0}, row_size, num_vals_limit));
+  }
+  ~RowPlan() {
+    if (p_) gp_row_plan_destroy(p_);
+  }
+  RowPlan(const RowPlan &) = delete;
+  RowPlan &operator=(const RowPlan &) = delete;
+  gp_row_plan get() const { return p_; }
+
+ private:
+  gp_row_plan p_ = nullptr;
+};
+
 }  // namespace geeps
 
 #endif  // GEEPS_AMD_DEVICE_HPP_

@@ -22,6 +22,16 @@ namespace geeps {
 constexpr uint32_t kFrameMagic = 0x31535047u;  // "GPS1"
 constexpr uint32_t kHelloCmd = 0x48454c4fu;    // "HELO"
 
+// First frame on a client -> server connection.
+struct HelloMsg {
+  uint32_t cmd;         // kHelloCmd
+  uint32_t process_id;  // the connecting client
+  uint32_t ipc;         // it takes same-node refreshes in place
+  uint32_t pad;
+  char pci_bus_id[32];  // its GPU (gp_device_pci_bus_id): a peer on another GPU
+                        // has its IPC-mapped buckets copied to local HBM first
+};
+
 struct Part {
   const void *data;
   size_t size;

@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstring>
 #include <future>
+#include <iostream>
 #include <sstream>
 
 #include "check.hpp"
@@ -26,6 +27,8 @@ std::string ServerStats::to_json() const {
     << ", \"nr_apply_out_of_place\": " << nr_apply_out_of_place
     << ", \"nr_buckets_applied\": " << nr_buckets_applied
     << ", \"nr_versions\": " << nr_versions
+    << ", \"nr_peer_staged\": " << nr_peer_staged
+    << ", \"version_wait_time\": " << version_wait_time
     << ", \"apply_time\": " << apply_time << ", \"stage_time\": " << stage_time
     << ", \"refresh_time\": " << refresh_time << "}";
   return o.str();
@@ -44,6 +47,7 @@ TabletServer::TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num
   GP_CHECK(num_clients_ > 0);
   tables_.resize(num_tables);
   for (auto &t : tables_) t.vec_clock.assign(num_clients_, INITIAL_DATA_AGE);
+  if (num_clients_ > 1) copy_stream_ = std::make_unique<Stream>();
   thread_ = std::thread([this] { run(); });
 }
 
@@ -89,6 +93,7 @@ void TabletServer::release(uint32_t client_id, uint32_t table_id, int version) {
                "client " << client_id << " releases master version " << version << " of table "
                          << table_id << " it does not hold");
   t.holders[version][client_id] = 0;
+  release_cv_.notify_all();
 }
 
 void TabletServer::release_all(uint32_t client_id) {
@@ -96,6 +101,7 @@ void TabletServer::release_all(uint32_t client_id) {
   GP_CHECK_LT(client_id, num_clients_);
   for (auto &t : tables_)
     for (auto &h : t.holders) h[client_id] = 0;
+  release_cv_.notify_all();
 }
 
 void TabletServer::wait_shutdown() {
@@ -218,12 +224,22 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
   GP_CHECK_EQ(t.row_count, batch_size);
 
   Pending p;
-  if (b.device_rows) {
+  if (b.device_rows && b.stage) {
+    // A same-node peer on another GPU: copy its slice into local HBM now (a
+    // peer copy over xGMI on the copy stream, overlapped with whatever else
+    // arrives), so the sum streams local HBM only.  apply_pending waits for it.
+    auto stage = stage_buffer(t);
+    GP_CALL(gp_memcpy_async(stage->data(), b.device_rows, batch_size * ROW_DATA_SIZE * sizeof(float),
+                            copy_stream_->get()));
+    p.staged = std::make_shared<Event>();
+    p.staged->record(*copy_stream_);
+    p.rows = stage->data();
+    p.keepalive = stage;
+    stats_.nr_peer_staged++;
+  } else if (b.device_rows) {
     // In-process client: its oplog slice, read in place (keepalive holds it).
-    // Same-node peer: its oplog slice mapped over IPC, also read in place (over
-    // xGMI when the peer is another GPU).  The peer reclaims an oplog only once
-    // every server's refresh covers its clock (recv_row_batch), and a refresh
-    // leaves here only after apply_pending has consumed the bucket.
+    // Same-node peer on this GPU: its oplog slice through the IPC mapping,
+    // also read in place.
     p.rows = b.device_rows;
     p.keepalive = std::move(b.keepalive);
   } else {
@@ -242,21 +258,31 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
 }
 
 // A version no client holds, other than the current one; a new one when
-// every version is held.
+// every version is held and fewer than clients + 2 exist; otherwise wait for
+// a release (see server.hpp: it always comes, from a reader thread).
 int TabletServer::free_version(DataTable &t) {
-  std::lock_guard<std::mutex> lk(hold_mu_);
-  for (size_t v = 0; v < t.versions.size(); ++v) {
-    if ((int)v == t.cur) continue;
-    bool held = false;
-    for (uint8_t h : t.holders[v]) held = held || h;
-    if (!held) return (int)v;
+  std::unique_lock<std::mutex> lk(hold_mu_);
+  const double t0 = now_s();
+  for (;;) {
+    for (size_t v = 0; v < t.versions.size(); ++v) {
+      if ((int)v == t.cur) continue;
+      bool held = false;
+      for (uint8_t h : t.holders[v]) held = held || h;
+      if (!held) {
+        stats_.version_wait_time += now_s() - t0;
+        return (int)v;
+      }
+    }
+    if (t.versions.size() < (size_t)num_clients_ + 2) {
+      t.versions.push_back(std::make_unique<DeviceArray<float>>(t.row_count * ROW_DATA_SIZE));
+      t.holders.emplace_back(num_clients_, 0);
+      stats_.nr_versions++;
+      return (int)t.versions.size() - 1;
+    }
+    if (release_cv_.wait_for(lk, std::chrono::milliseconds(12000)) == std::cv_status::timeout)
+      std::cerr << "tablet server " << server_id_ << " channel " << channel_id_
+                << ": every master version is held; waiting for a client to release one\n";
   }
-  GP_CHECK_MSG(t.versions.size() < (size_t)num_clients_ + 2,
-               "every master version is held: clients hold more than one version each");
-  t.versions.push_back(std::make_unique<DeviceArray<float>>(t.row_count * ROW_DATA_SIZE));
-  t.holders.emplace_back(num_clients_, 0);
-  stats_.nr_versions++;
-  return (int)t.versions.size() - 1;
 }
 
 // All queued buckets in arrival order, one launch: master = ((m + b0) + b1) ...
@@ -267,7 +293,10 @@ void TabletServer::apply_pending(DataTable &t) {
   const double t0 = now_s();
   std::vector<const float *> ptrs;
   ptrs.reserve(t.pending.size());
-  for (auto &p : t.pending) ptrs.push_back(p.rows);
+  for (auto &p : t.pending) {
+    ptrs.push_back(p.rows);
+    if (p.staged) GP_CALL(gp_stream_wait_event(stream_, p.staged->get()));  // peer copy landed
+  }
   const float *in = t.versions[t.cur]->data();
   if (t.cur_published) {
     bool held = false;

@@ -30,9 +30,14 @@
 // published version is never written again while any client holds it: the
 // next apply writes a new version out of place (gp_bucket_sum_into: same
 // bytes as the in-place sum), into a version no client holds, allocating one
-// when none is free.  Each client holds at most one version per table at a
-// time (two during a switch), so at most clients + 2 versions ever exist and
-// the server never waits for a release.
+// when none is free, up to clients + 2 versions.  A client is marked as
+// holding a version when the refresh is SENT, and gives the one before back
+// when its reader thread TAKES the next refresh, so under SSP a lagging reader
+// can hold several (up to slack + 2).  When every version is held and the cap
+// is reached, the apply waits for a release: releases arrive on the socket
+// reader threads (or inside this thread for the in-process client, which
+// holds only the current version), never on this thread, and each is the
+// reader catching up on refreshes already sent, so the wait always ends.
 
 #include <condition_variable>
 #include <deque>
@@ -49,10 +54,15 @@
 namespace geeps {
 
 // Rows of one client's clock update for one server: n keys and n RowOpVal.
-// Exactly one of `device_rows` (in-process client: a zero-copy slice of its
-// oplog, kept alive by `keepalive` until applied; or a same-node peer's oplog
-// slice, copied on arrival) or `host_rows` (received from a socket into pinned
-// memory) is set.
+// Exactly one of `device_rows` or `host_rows` (received from a socket into
+// pinned memory) is set.  `device_rows` is the in-process client's oplog slice
+// (kept alive by `keepalive` until applied) or a same-node peer's oplog slice
+// through an IPC mapping, which the sum reads in place when the peer is on
+// this GPU; with `stage` (the peer is on another GPU) it is first copied into
+// local HBM on the server's copy stream, so the sum reads only local HBM.  The
+// peer's buffer stays valid either way: it reclaims an oplog only once every
+// server's refresh covers its clock, and a refresh leaves a server only after
+// its apply consumed the bucket.
 struct UpdateBatch {
   uint32_t client_id = 0;
   iter_t clock = 0;
@@ -63,9 +73,7 @@ struct UpdateBatch {
   size_t num_rows = 0;
   std::shared_ptr<const void> keys_owner;
   const float *device_rows = nullptr;
-  // device_rows points into a same-node peer's HBM (IPC-mapped): stage a copy
-  // on arrival instead of holding the peer's buffer.
-  bool device_remote = false;
+  bool stage = false;
   std::shared_ptr<void> keepalive;
   std::shared_ptr<PinnedArray<float>> host_rows;
 };
@@ -107,7 +115,9 @@ struct ServerStats {
   uint64_t nr_buckets_applied = 0;
   uint64_t nr_versions = 0;            // master versions allocated (all tables)
   double apply_time = 0;         // s, including the launch sync
-  double stage_time = 0;         // s, H2D of socket-delivered buckets
+  double stage_time = 0;         // s, H2D of socket-delivered buckets (host side)
+  uint64_t nr_peer_staged = 0;   // buckets copied in from a peer GPU before the sum
+  double version_wait_time = 0;  // s, applies waiting for a master version release
   double refresh_time = 0;       // s, sending refreshed shards
   std::string to_json() const;
 };
@@ -151,6 +161,7 @@ class TabletServer {
   struct Pending {
     const float *rows;
     std::shared_ptr<void> keepalive;
+    std::shared_ptr<Event> staged;  // a peer copy into `rows` on copy_stream_
   };
   struct DataTable {
     std::vector<iter_t> vec_clock;
@@ -195,6 +206,8 @@ class TabletServer {
   std::condition_variable cv_;
   std::deque<Msg> queue_;
   std::mutex hold_mu_;  // DataTable::holders (and the versions vector's size)
+  std::condition_variable release_cv_;  // a hold ended (release / release_all)
+  std::unique_ptr<Stream> copy_stream_;  // peer copies of other GPUs' buckets
   uint32_t shutdown_count_ = 0;  // server thread only
   bool shutdown_done_ = false;    // guarded by mu_
   std::condition_variable shutdown_cv_;

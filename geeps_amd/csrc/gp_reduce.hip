@@ -1372,6 +1372,19 @@ int gp_event_elapsed_ms(float *ms, gp_event start, gp_event stop) {
   return GP_OK;
 }
 
+int gp_stream_wait_event(gp_stream s, gp_event e) {
+  if (!e) return set_error(GP_ERR_INVALID, "null event");
+  GP_HIP_TRY(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0));
+  return GP_OK;
+}
+
+int gp_device_pci_bus_id(int device, char *buf, int len) {
+  if (!buf || len < 2) return set_error(GP_ERR_INVALID, "null or short buffer");
+  GP_HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
+  buf[len - 1] = 0;
+  return GP_OK;
+}
+
 static_assert(sizeof(hipIpcMemHandle_t) <= GP_IPC_HANDLE_BYTES, "IPC handle size");
 
 int gp_ipc_get_handle(void *handle_out, void *device_base) {

@@ -89,6 +89,8 @@ _SIGNATURES = {
     "gp_event_record": (_i, [_vp, _vp]),
     "gp_event_synchronize": (_i, [_vp]),
     "gp_event_elapsed_ms": (_i, [_c.POINTER(_c.c_float), _vp, _vp]),
+    "gp_stream_wait_event": (_i, [_vp, _vp]),
+    "gp_device_pci_bus_id": (_i, [_i, _c.c_char_p, _i]),
     "gp_ipc_get_handle": (_i, [_vp, _vp]),
     "gp_ipc_open_handle": (_i, [_c.POINTER(_vp), _vp]),
     "gp_ipc_close_handle": (_i, [_vp]),

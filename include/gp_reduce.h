@@ -263,6 +263,12 @@ int gp_event_destroy(gp_event e);
 int gp_event_record(gp_event e, gp_stream s);
 int gp_event_synchronize(gp_event e);
 int gp_event_elapsed_ms(float *ms, gp_event start, gp_event stop);
+/* Work queued on `s` after this call waits for `e`'s last record. */
+int gp_stream_wait_event(gp_stream s, gp_event e);
+/* The device's PCI bus id ("0000:05:00.0"), NUL-terminated in buf[len]: a
+ * name of the physical GPU that is the same in every process, whatever
+ * device numbering (HIP_VISIBLE_DEVICES) each one sees. */
+int gp_device_pci_bus_id(int device, char *buf, int len);
 
 /* Inter-process device memory (same node; xGMI between MI355X devices):
  * export a hipMalloc'd allocation BASE as an opaque 64-byte handle, map a

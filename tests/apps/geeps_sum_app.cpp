@@ -15,6 +15,8 @@
 // differently from run to run.
 // GEEPS_TEST_EMPTY_SETUP=1: the setup clock (clock 0) carries no updates, so
 // every server's first refresh is an empty shard (all zeros).
+// GEEPS_TEST_SPREAD_DEVICES=1: process p works on GPU p % device_count (one
+// process per GPU, as on an 8-GPU node), selected before GeePs is created.
 //
 // `layers` (comma-separated row counts, summing to `rows`) switches to a
 // Caffe-like op sequence: a Read per parameter blob in forward order, then per
@@ -97,6 +99,11 @@ int main(int argc, char **argv) {
   const bool use_local = argc > 12 && std::atoi(argv[12]) != 0;
   const std::string out_dir = argc > 13 ? argv[13] : "";
 
+  if (std::getenv("GEEPS_TEST_SPREAD_DEVICES")) {
+    int count = 0;
+    HCK(hipGetDeviceCount(&count));
+    HCK(hipSetDevice(pid % count));
+  }
   GeePsConfig cfg;
   cfg.num_tables = T;
   cfg.output_dir = out_dir;

@@ -604,3 +604,33 @@ def test_row_plan_rejects_small_buffers(dev):
         plan.add(torch.zeros(14 * 128, device=dev), torch.zeros(10 * 128, device=dev))
     with pytest.raises(ValueError):
         plan.add(torch.zeros(15 * 128, device=dev), torch.zeros(9 * 128, device=dev))
+
+
+@pytest.mark.parametrize("N,out_of_place", [(3, False), (3, True), (7, False), (7, True)])
+def test_bucket_sum_sweep_then_small_leftover(dev, N, out_of_place):
+    """3 whole 64-MiB sweep chunks, then a 1-MiB leftover (below the phased
+    form's 4 MiB: the mixed dwordx4 form at offset `done`) and a 3-float scalar
+    tail, at 3 and 7 buckets, in place and out of place."""
+    import ctypes
+    from geeps_amd import native, rowops
+    n = (48 << 20) + (1 << 18) + 3
+    launches, rt, sw = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    native.check(native.lib().gp_bucket_sum_sweep_plan(n, N, ctypes.byref(launches),
+                                                        ctypes.byref(rt), ctypes.byref(sw)))
+    assert (sw.value, launches.value) == (3, 3)
+    ups = [oracle.synthetic_delta(700 + c, n) for c in range(N)]
+    m0 = np.random.default_rng(N + 40).standard_normal(n).astype(np.float32)
+    e = m0.copy()
+    oracle.apply_updates(e, ups)
+    m = T(m0, dev)
+    tb = [T(u, dev) for u in ups]
+    if out_of_place:
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+        rowops.bucket_sum_into(out, m, tb)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(m.cpu().numpy()), bits(m0))
+    else:
+        rowops.bucket_sum_apply(m, tb)
+        out = m
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()), bits(e))

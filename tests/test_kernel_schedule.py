@@ -1,0 +1,57 @@
+"""The sweep-form bucket sum's speed rests on its instruction schedule: each
+burst's loads issued together, then waited on with counted vmcnt(N).  One
+compiler choice regrouped the register tiles' adds into load -> vmcnt(0) ->
+add chains (117-224 full drains per chunk, 8.3 instead of 6.5 ms at 8 buckets;
+profiles/r01b/sweep_ab.txt).  This compiles the product kernel file to gfx950
+assembly (no GPU needed) and fails if that comes back."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not installed")
+    out = tmp_path_factory.mktemp("asm") / "gp_reduce.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I",
+                    os.path.join(REPO, "include"), "--cuda-device-only", "-S", "-o", str(out),
+                    os.path.join(REPO, "geeps_amd", "csrc", "gp_reduce.hip")],
+                   check=True, capture_output=True, cwd=str(out.parent))
+    return out.read_text()
+
+
+def _kernel(asm, pattern):
+    m = re.search(rf"^({pattern}\S*):", asm, re.M)
+    assert m, pattern
+    body = asm[m.end():asm.index(".Lfunc_end", m.end())]
+    return body
+
+
+@pytest.mark.parametrize("nb", [3, 4, 5, 6, 7, 8])
+def test_sweep_kernel_keeps_burst_schedule(asm, nb):
+    body = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi{nb}ELi6ELi4EE")
+    loads = len(re.findall(r"global_load_dwordx4", body))
+    full_drains = len(re.findall(r"s_waitcnt vmcnt\(0\)", body))
+    # (nb + 1) streams x 16 tiles x 4 block-strides, all dwordx4
+    assert loads == (nb + 1) * 16 * 4
+    assert full_drains <= 4, f"{full_drains} full vmcnt(0) drains: the burst schedule regressed"
+    assert "scratch_" not in body and "buffer_store_dword" not in body  # no spills
+
+
+def test_wave_kernels_fit_their_occupancy(asm):
+    """The scatter / gather wave-map kernels keep 3-4 waves per SIMD: the
+    limit-straddle path must not index register arrays at run time (that cost
+    86-91 more VGPRs and halved the resident blocks; profiles/r02)."""
+    for op, max_vgpr in ((0, 168), (1, 128), (3, 128)):  # add, gather, init at 128-float rows
+        pat = rf"_ZN12_GLOBAL__N_115row_wave_kernelIDv4_fLi{op}ELi32ELi8ELi0EEE"
+        name = re.search(rf"^({pat}\S*):", asm, re.M).group(1)
+        n = int(re.search(rf"\.set {re.escape(name)}\.num_vgpr, (\d+)", asm).group(1))
+        assert n <= max_vgpr, (op, n)

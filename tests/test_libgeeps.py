@@ -98,8 +98,9 @@ def _ports(n_proc, channels):
     return _free_port_base(n_proc, channels)
 
 
-def _env(transport, jitter_us=0, empty_setup=False):
+def _env(transport, jitter_us=0, empty_setup=False, extra=None):
     env = dict(os.environ)
+    env.update(extra or {})
     if empty_setup:
         env["GEEPS_TEST_EMPTY_SETUP"] = "1"  # first refreshes are empty shards
     env["GEEPS_TRANSPORT"] = transport  # "ipc": same-node rows over IPC-mapped HBM; "tcp": sockets
@@ -152,12 +153,13 @@ def _collect(procs, timeout):
 
 
 def _run_app(P, rows, clocks, slack, channels, rmw, mode="int", timeout=240, transport="ipc",
-             jitter_us=0, empty_setup=False):
+             jitter_us=0, empty_setup=False, extra_env=None):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, channels)
     procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
-                     str(channels), str(rmw), mode], _env(transport, jitter_us, empty_setup))
+                     str(channels), str(rmw), mode],
+                    _env(transport, jitter_us, empty_setup, extra_env))
              for p in range(P)]
     return _collect(procs, timeout)
 
@@ -315,3 +317,53 @@ def test_two_tables_local_access_and_stats_file(dev, tmp_path, transport):
         assert st["process_id"] == pid
         assert st["client"]["nr_update"] == 5 * 7      # 5 blobs x (setup clock + 6 clocks)
         assert st["servers"][0]["nr_refresh"] >= 2 * 6  # 2 tables refresh every clock
+
+
+def _stats(outs):
+    import json
+    return [json.loads(o.split("stats ", 1)[1].splitlines()[0]) for _, o, _ in outs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slack", [2, 3])
+def test_lagging_reader_holds_many_versions(dev, slack):
+    """SSP with a client whose reader thread takes every refresh 15 ms late:
+    the server marks a version held when the refresh is sent and gets it back
+    only when the reader takes the next one, so a lagging reader holds up to
+    slack + 2 versions.  Once clients + 2 versions exist and all are held, the
+    apply waits for a release instead of aborting; the reads stay
+    within the SSP bounds."""
+    outs = _run_app(2, rows=700, clocks=30, slack=slack, channels=1, rmw=0, transport="ipc",
+                    extra_env={"GEEPS_TEST_READER_DELAY_US": "15000"}, timeout=300)
+    st = _stats(outs)
+    srv = [s["servers"][0] for s in st]
+    print("lagging-reader servers:", [(v["nr_versions"], round(v["version_wait_time"], 4)) for v in srv])
+    assert all(v["nr_versions"] <= 2 + 2 for v in srv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,slack,channels", [(2, 0, 1), (3, 1, 2), (4, 2, 1)])
+def test_peer_buckets_staged_into_local_hbm(dev, P, slack, channels):
+    """The cross-GPU bucket path: a same-node peer's oplog slice is copied into
+    the server's HBM on its copy stream before the sum (forced on one GPU by
+    GEEPS_STAGE_PEER_UPDATES=1); exact sums, and every server staged buckets."""
+    outs = _run_app(P, rows=900, clocks=10, slack=slack, channels=channels, rmw=0, transport="ipc",
+                    extra_env={"GEEPS_STAGE_PEER_UPDATES": "1"})
+    for s in _stats(outs):
+        assert all(srv["nr_peer_staged"] > 0 for srv in s["servers"])
+
+
+@pytest.mark.gpu
+def test_one_process_per_gpu(dev):
+    """One process per GPU (process p on device p % count), as on an 8-GPU
+    node: peers' buckets cross xGMI by the staged peer copy and refreshes are
+    read in place from the other GPUs' master versions.  Needs 2+ GPUs."""
+    import torch
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("one GPU on this box")
+    P = min(n, 4)
+    outs = _run_app(P, rows=1200, clocks=8, slack=1, channels=1, rmw=0, transport="ipc",
+                    extra_env={"GEEPS_TEST_SPREAD_DEVICES": "1"})
+    for s in _stats(outs):
+        assert all(srv["nr_peer_staged"] > 0 for srv in s["servers"])
