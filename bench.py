@@ -97,6 +97,8 @@ def parse(argv=None):
     p.add_argument("--no-rowops", action="store_true")
     p.add_argument("--rowops-only", nargs="*", default=None, choices=list(ROWOP_LEGS),
                    help="run only these client row-op legs (PMC passes)")
+    p.add_argument("--rowops-index", nargs="*", default=["random", "identity"],
+                   choices=["random", "identity"], help="DoubleIndex kinds of the row-op legs")
     p.add_argument("--no-config2", action="store_true")
     p.add_argument("--no-hbm-probe", action="store_true")
     p.add_argument("--layout", choices=["arena", "separate"], default="arena",
@@ -610,7 +612,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
         torch.cuda.empty_cache()
         if not args.no_rowops:
             log("[rank 0] client row-op leg")
-            rowops_res = rowops_leg(R, W, dev, only=args.rowops_only)
+            rowops_res = rowops_leg(R, W, dev, indexes=tuple(args.rowops_index),
+                                    only=args.rowops_only)
             torch.cuda.empty_cache()
         if not args.no_host_inclusive:
             log("[rank 0] host-inclusive leg")

@@ -339,6 +339,7 @@ def test_lagging_reader_holds_many_versions(dev, slack):
     srv = [s["servers"][0] for s in st]
     print("lagging-reader servers:", [(v["nr_versions"], round(v["version_wait_time"], 4)) for v in srv])
     assert all(v["nr_versions"] <= 2 + 2 for v in srv)
+    assert max(v["nr_versions"] for v in srv) == 2 + 2  # the lag reached the cap
 
 
 @pytest.mark.gpu
