@@ -195,3 +195,44 @@ def test_row_plan_rejects_repeated_destinations():
     h = ctypes.c_void_p()
     assert L.gp_row_plan_create(ctypes.byref(h), None, 4, native.DoubleIndex(0, 0), 128, 0) == 1
     assert L.gp_scatter_add_rows_planned(None, None, None, None) == 1
+
+
+def test_launch_plans_stable_while_device_is_set_concurrently():
+    """The CU count behind every launch plan is cached per device and never
+    reset (gp_set_device used to zero a process-global that
+    other threads were sizing grids from).  Several threads plan sums while
+    another keeps calling gp_set_device; every plan must equal the one made
+    before.  (ctypes releases the GIL during each call, so the calls overlap.)"""
+    import threading
+    L = native.lib()
+
+    def plan(n, nb):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        assert L.gp_bucket_sum_sweep_plan(n, nb, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == 0
+        return a.value, b.value, c.value
+
+    cases = [((1 << 30) + 7, 8), ((1 << 28) + 5, 2), (100 << 20, 3), (30 << 18, 5)]
+    want = {k: plan(*k) for k in cases}
+    stop = threading.Event()
+    bad = []
+
+    def planner():
+        while not stop.is_set():
+            for k in cases:
+                if plan(*k) != want[k]:
+                    bad.append(k)
+
+    def setter():
+        while not stop.is_set():
+            L.gp_set_device(0)  # fails without a GPU; must never disturb the plans
+
+    ts = [threading.Thread(target=planner) for _ in range(4)] + [threading.Thread(target=setter)]
+    for t in ts:
+        t.start()
+    import time
+    time.sleep(1.0)
+    stop.set()
+    for t in ts:
+        t.join()
+    assert not bad
+    assert want[cases[0]][2] > 0  # the 4-GiB 8-way shard takes sweep chunks

@@ -360,6 +360,43 @@ def test_full_size_8way_bucket_sum(dev):
 
 
 @pytest.mark.slow
+def test_full_size_config1_two_clients(dev):
+    """BASELINE configs[1]: 1M rows x 1024 fp32, one shard, 2 clients (16 GiB
+    resident with the reference copy).  The plan is 35 launches of the
+    register-tile phased kernel (120-MiB chunks, the last partial); every
+    element against a plain torch fp32 reference adding the 2 buckets in client
+    order, and sampled rows against the C oracle."""
+    import ctypes
+    from geeps_amd import native, rowops
+    R, W, N = 1 << 20, 1024, 2
+    n = R * W
+    launches, rt = ctypes.c_int(0), ctypes.c_int(0)
+    native.check(native.lib().gp_bucket_sum_plan(n, N, ctypes.byref(launches), ctypes.byref(rt)))
+    assert (launches.value, rt.value) == (35, 20)
+    g = torch.Generator(device=dev)
+    buckets = []
+    for c in range(N):
+        g.manual_seed(1000 + c)
+        buckets.append(torch.rand(n, generator=g, device=dev) - 0.5)
+    g.manual_seed(78)
+    master = torch.rand(n, generator=g, device=dev) - 0.5
+    rows = _sample_rows(np.random.default_rng(2), R)
+    ridx = torch.from_numpy(rows).to(dev)
+    m0 = master.view(R, W)[ridx].cpu().numpy().ravel()
+    bs = [b.view(R, W)[ridx].cpu().numpy().ravel() for b in buckets]
+    expect = master.clone()
+    for b in buckets:
+        expect += b
+    rowops.bucket_sum_apply(master, buckets)
+    torch.cuda.synchronize()
+    assert torch.equal(master.view(torch.int32), expect.view(torch.int32))
+    del expect
+    oracle.apply_updates(m0, bs)
+    got = master.view(R, W)[ridx].cpu().numpy().ravel()
+    assert np.array_equal(bits(got), bits(m0))
+
+
+@pytest.mark.slow
 def test_full_size_scatter_add_permuted(dev):
     """8M RowData rows (the 1M x 1024 table through the 128-float API), random
     permutation DoubleIndex; every row vs a torch reference and sampled rows vs
