@@ -19,6 +19,9 @@ gather_rows_segmented              assign_rows_to_double_index_gpu over a param 
                                    split into row-range buffers (libgeeps in-place refreshes)
 add_rows_segmented                 add_rows_from_double_index_gpu into such a cache
                                    (read-my-writes, clientlib-data.cpp:387-392)
+RowPlan.add / RowPlan.init         add_rows_from_double_index_gpu (+ zerofy) over an
+                                   index compiled once (vi_create_double_index,
+                                   clientlib-viter.cpp:817-883), rows in cache order
 =================================  ===============================================
 
 Differences from the reference (deliberate, documented in DESIGN.md): launches
