@@ -192,34 +192,52 @@ def timed_apply(red, steps, warmup, world, dev):
     return wall, kernel_ms
 
 
-def hbm_copy_probe(src, dst, reps=5):
-    """Same-box context for roofline.frac: a device-to-device copy of one 4 GiB
-    bucket (gp_memcpy_async = hipMemcpyAsync, 1 read + 1 write stream), timed
-    with HIP events on the launch stream.  HBM boxes differ by several percent
-    (DESIGN.md §5), and a write stream costs more than a read one, so this
-    says how much of the spec peak the same box gives a plain copy."""
+def hbm_probe(src, dst, reps=5):
+    """Same-box HBM context for every kernel's roofline.frac, timed with HIP
+    events on the launch stream over one 4 GiB bucket:
+      read   gp_hbm_probe(GP_PROBE_READ): the buffer streamed once, read-only
+      write  gp_hbm_probe(GP_PROBE_WRITE): written once (the runtime's fill)
+      copy   gp_memcpy_async D2D (hipMemcpyAsync: 1 read + 1 write stream)
+    each the fastest shape found for that stream alone.  A kernel reading R and
+    writing W bytes is then modelled as R / read_rate + W / write_rate
+    (`model_ms`): a best case, since it charges nothing for mixing reads and
+    writes on HBM, and HBM boxes differ by several percent."""
     from geeps_amd import native
     lib = native.lib()
     stream = torch.cuda.current_stream()
     nbytes = src.numel() * src.element_size()
 
-    def one():
-        native.check(lib.gp_memcpy_async(dst.data_ptr(), src.data_ptr(), nbytes,
-                                         stream.cuda_stream), "gp_memcpy_async")
+    def timed(fn):
+        fn()
+        ms = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn()
+            b.record(stream)
+            b.synchronize()
+            ms.append(a.elapsed_time(b))
+        return sum(ms) / len(ms)
 
-    one()
-    ms = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        one()
-        b.record(stream)
-        b.synchronize()
-        ms.append(a.elapsed_time(b))
-    avg = sum(ms) / len(ms)
-    return {"copy_GBps": round(2 * nbytes / (avg / 1e3) / 1e9, 1), "bytes": 2 * nbytes,
-            "avg_ms": round(avg, 4),
-            "note": "same-box D2D copy of one bucket (hipMemcpyAsync: 1 read + 1 write stream)"}
+    t_copy = timed(lambda: native.check(lib.gp_memcpy_async(dst.data_ptr(), src.data_ptr(), nbytes,
+                                                            stream.cuda_stream), "gp_memcpy_async"))
+    t_read = timed(lambda: native.check(lib.gp_hbm_probe(0, src.data_ptr(), src.numel(),
+                                                         stream.cuda_stream), "gp_hbm_probe"))
+    t_write = timed(lambda: native.check(lib.gp_hbm_probe(1, dst.data_ptr(), dst.numel(),
+                                                          stream.cuda_stream), "gp_hbm_probe"))
+    return {"read_GBps": round(nbytes / (t_read / 1e3) / 1e9, 1),
+            "write_GBps": round(nbytes / (t_write / 1e3) / 1e9, 1),
+            "copy_GBps": round(2 * nbytes / (t_copy / 1e3) / 1e9, 1), "bytes": nbytes,
+            "read_ms": round(t_read, 4), "write_ms": round(t_write, 4), "copy_ms": round(t_copy, 4),
+            "note": "one 4 GiB buffer: read-only and write-only streams (gp_hbm_probe) and a "
+                    "hipMemcpyAsync D2D copy, on this box"}
+
+
+def model_ms(read_bytes, write_bytes, probe):
+    """The same box's two-rate HBM model of a kernel's bytes (hbm_probe)."""
+    if not probe:
+        return None
+    return read_bytes / (probe["read_GBps"] * 1e9) * 1e3 + write_bytes / (probe["write_GBps"] * 1e9) * 1e3
 
 
 def timed_exchange(red, deltas, steps, warmup, world, dev):
@@ -351,7 +369,7 @@ def _time_calls(fn, reps, stream):
     return sum(ms) / len(ms)
 
 
-def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None):
+def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, probe=None):
     """The client half of the path at the same table size: the 1M x 1024 table
     through the 128-float API is R = 8M RowData rows.  Per DoubleIndex
     (random permutation of the destinations, and identity -- libgeeps' cache
@@ -386,6 +404,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None):
                 continue
             planned = name.endswith("_planned")
             nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * R
+            writes = R * 512
             if name == "scatter_add":
                 fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                    validate=False)
@@ -407,6 +426,10 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None):
             leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),
                    "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes": nbytes, "kernel": kernel,
                    "launches": launches, "avg_launch_ms": round(avg / launches, 5)}
+            mm = model_ms(nbytes - writes, writes, probe)
+            if mm:
+                leg["model_ms"] = round(mm, 4)
+                leg["frac_of_model"] = round(mm / avg, 4)
             if planned:
                 leg["plan"] = info
             traffic = load_traffic(f"rowops_{name}_{kind}_r{R}_w128", kernel)
@@ -513,7 +536,7 @@ def load_traffic(workload_key, kernel):
         return None
 
 
-def config2_leg(deltas, master, dev, reps=5):
+def config2_leg(deltas, master, dev, probe=None, reps=5):
     """BASELINE configs[1]: the same 1M x 1024 shard, 2 client buckets (the
     first two resident deltas, client order 0, 1) summed into the master by one
     gp_bucket_sum_apply.  Algorithmic bytes (2 + 2) * shard bytes."""
@@ -530,7 +553,8 @@ def config2_leg(deltas, master, dev, reps=5):
             "delta_GBps": round(2 * n * 4 / (avg / 1e3) / 1e9, 1), "bytes": nbytes,
             "kernel": plan["kernel"], "launches": plan["launches"],
             "avg_launch_ms": round(avg / plan["launches"], 5),
-            "traffic_source": load_traffic(f"r{rows}_w1024_c2_g1", plan["kernel"])}
+            "traffic_source": load_traffic(f"r{rows}_w1024_c2_g1", plan["kernel"]),
+            "model_ms": (round(model_ms(3 * n * 4, n * 4, probe), 4) if probe else None)}
 
 
 def main(argv=None, backend="nccl", apply_fn=None):
@@ -599,13 +623,13 @@ def main(argv=None, backend="nccl", apply_fn=None):
     config2 = None
     if rank == 0 and world == 1 and dev.type == "cuda":
         if not args.no_hbm_probe:
-            log("[rank 0] HBM copy probe")
+            log("[rank 0] HBM probes")
             scratch = torch.empty_like(deltas[0])
-            probe = hbm_copy_probe(deltas[0], scratch)
+            probe = hbm_probe(deltas[0], scratch)
             del scratch
         if not args.no_config2 and C >= 2 and master is not None:
             log("[rank 0] configs[1] leg (2 clients)")
-            config2 = config2_leg(deltas, master, dev)
+            config2 = config2_leg(deltas, master, dev, probe)
         del deltas
         red = None
         master = None
@@ -613,7 +637,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
         if not args.no_rowops:
             log("[rank 0] client row-op leg")
             rowops_res = rowops_leg(R, W, dev, indexes=tuple(args.rowops_index),
-                                    only=args.rowops_only)
+                                    only=args.rowops_only, probe=probe)
             torch.cuda.empty_cache()
         if not args.no_host_inclusive:
             log("[rank 0] host-inclusive leg")
@@ -669,6 +693,9 @@ def main(argv=None, backend="nccl", apply_fn=None):
             line["exchange_inclusive_alt"] = result_exchange[1]
         if probe:
             line["roofline"]["same_box_copy_GBps"] = probe["copy_GBps"]
+            mm = model_ms((C + 1) * shard_bytes, shard_bytes, probe)
+            line["roofline"]["same_box_model_ms"] = round(mm, 4)
+            line["roofline"]["frac_of_same_box_model"] = round(mm / avg_kernel_ms_max, 4)
             line["hbm_probe"] = probe
         if config2:
             line["config2"] = config2

@@ -498,6 +498,36 @@ int launch_bucket_sum(float *out, const float *in, const float *const *bk,
 }
 
 // ---------------------------------------------------------------------------
+// HBM probe (measurement only): one buffer streamed once, read-only, with
+// 16-B non-temporal loads, 4 block-strides in flight per thread, 2 blocks per
+// CU -- the fastest of 16 shapes (U 4-16, 1-8 blocks per CU, nt or plain):
+// 6.3-7.1 TB/s (profiles/r02/tune/probe_tune*.txt).  bench.py times it beside
+// the reduction, and a write-only stream beside it, to give each kernel's
+// bytes a same-box two-rate model: t = read_bytes / read_rate +
+// write_bytes / write_rate.
+// ---------------------------------------------------------------------------
+constexpr int kProbeU = 4;
+
+__global__ __launch_bounds__(kBlock) void hbm_read_probe_kernel(const f4 *__restrict__ in, size_t n4,
+                                                               float *__restrict__ sink) {
+  const size_t tile = (size_t)kBlock * kProbeU;
+  const size_t stride = (size_t)gridDim.x * tile;
+  f4 acc = f4(0.0f);
+  size_t base = (size_t)blockIdx.x * tile + threadIdx.x;
+  for (; base + (kProbeU - 1) * kBlock < n4; base += stride) {
+    f4 v[kProbeU];
+#pragma unroll
+    for (int u = 0; u < kProbeU; ++u) v[u] = __builtin_nontemporal_load(in + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < kProbeU; ++u) acc += v[u];
+  }
+  for (int u = 0; u < kProbeU; ++u)
+    if (base + u * kBlock < n4) acc += __builtin_nontemporal_load(in + base + u * kBlock);
+  // data-dependent, practically never true: keeps every load live
+  if (acc.x + acc.y + acc.z + acc.w == -1234.5f) sink[blockIdx.x % 64] = acc.x;
+}
+
+// ---------------------------------------------------------------------------
 // Row-indexed ops over a DoubleIndex.
 // ---------------------------------------------------------------------------
 
@@ -1252,6 +1282,26 @@ int gp_add(size_t n, const float *a, const float *b, float *y, gp_stream s) {
   if (!a || !b || !y) return set_error(GP_ERR_INVALID, "null pointer");
   const float *bk[1] = {b};
   return launch_bucket_sum(y, a, bk, 1, n, (hipStream_t)s);
+}
+
+int gp_hbm_probe(int kind, float *buffer, size_t num_vals, gp_stream s) {
+  if (num_vals == 0) return GP_OK;
+  if (!buffer || !aligned16(buffer)) return set_error(GP_ERR_INVALID, "null or unaligned buffer");
+  if (kind == GP_PROBE_READ) {
+    // the sink: the first 64 floats of the buffer, written only if the sum of
+    // a thread's loads hits -1234.5 exactly
+    const size_t grid = (size_t)num_cus() * 2;
+    hipLaunchKernelGGL(hbm_read_probe_kernel, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)s,
+                       reinterpret_cast<const f4 *>(buffer), num_vals / 4, buffer);
+  } else if (kind == GP_PROBE_WRITE) {
+    // the runtime's fill kernel: 6.3-6.7 TB/s, above every store-loop shape
+    // tried (5.5-6.3 TB/s; profiles/r02/tune/probe_tune*.txt)
+    GP_HIP_TRY(hipMemsetAsync(buffer, 0, num_vals * sizeof(float), (hipStream_t)s));
+  } else {
+    return set_error(GP_ERR_INVALID, "probe kind");
+  }
+  GP_HIP_TRY(hipGetLastError());
+  return GP_OK;
 }
 
 int gp_zero(float *y, size_t num_vals, gp_stream s) {

@@ -71,6 +71,7 @@ _SIGNATURES = {
     "gp_bucket_sum_sweep_plan": (_i, [_sz, _i, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
     "gp_add": (_i, [_sz, _vp, _vp, _vp, _vp]),
     "gp_zero": (_i, [_vp, _sz, _vp]),
+    "gp_hbm_probe": (_i, [_i, _vp, _sz, _vp]),
     "gp_device_count": (_i, [_c.POINTER(_i)]),
     "gp_set_device": (_i, [_i]),
     "gp_get_device": (_i, [_c.POINTER(_i)]),

@@ -237,6 +237,17 @@ int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launc
  * src/common/row-op-util.hpp:72-79) as gp_add(n, y, x, y). In-place allowed. */
 int gp_add(size_t n, const float *a, const float *b, float *y, gp_stream s);
 
+/* HBM probe for measurement tools: stream `num_vals` floats of a 16-B
+ * aligned device buffer once, read-only (GP_PROBE_READ: 16-B non-temporal
+ * loads; the buffer is left unchanged in practice: its first 64 floats are
+ * written only if a thread's running sum lands exactly on -1234.5) or
+ * write-only (GP_PROBE_WRITE: zeros, through the runtime's fill kernel).
+ * bench.py times both to model every kernel's bytes on the same box.  No
+ * reference counterpart. */
+#define GP_PROBE_READ 0
+#define GP_PROBE_WRITE 1
+int gp_hbm_probe(int kind, float *buffer, size_t num_vals, gp_stream s);
+
 /* Zero `num_vals` floats — DataStorage::zerofy_data_gpu
  * (src/common/common-util.hpp:445-456). */
 int gp_zero(float *y, size_t num_vals, gp_stream s);
