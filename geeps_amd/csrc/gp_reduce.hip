@@ -922,7 +922,8 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
   if constexpr (kWaveShape && (kWaveGather || kWaveScatter)) {
     // Wave-level index map (row_wave_kernel): the gather of rows up to 128
     // floats, the fused init always, the scatter-add when its rows are sorted
-    // by destination (a row plan's residual).  Rows in flight per group: 8 at
+    // by destination (a row plan; in op order its random read-modify-write
+    // side runs 3-8 % slower here than in row_op_kernel).  Rows in flight per group: 8 at
     // 32 lanes per row (16 spilled past 256 VGPRs: 9 % slower), 16 at 16 lanes.
     constexpr int RPG = LPR == 32 ? 8 : 16;
     if (kWaveGather || OP == kInitFrom || sorted) {
