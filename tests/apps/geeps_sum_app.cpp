@@ -17,6 +17,9 @@
 // every server's first refresh is an empty shard (all zeros).
 // GEEPS_TEST_SPREAD_DEVICES=1: process p works on GPU p % device_count (one
 // process per GPU, as on an 8-GPU node), selected before GeePs is created.
+// GEEPS_TEST_SHUFFLE_UPDATES=1: every PreUpdate lists its blob's rows in a
+// shuffled order (seeded per blob), so the update op's DoubleIndex maps op
+// rows to cache rows by a permutation and libgeeps' row plan reorders it.
 //
 // `layers` (comma-separated row counts, summing to `rows`) switches to a
 // Caffe-like op sequence: a Read per parameter blob in forward order, then per
@@ -137,6 +140,25 @@ int main(int argc, char **argv) {
     for (size_t r = 0; r < layer_rows[l]; ++r) ids[r] = first_in_table[l] + r;
     return ids;
   };
+  // upd_row[l][j]: the blob row the update op's buffer row j carries
+  const bool shuffle = std::getenv("GEEPS_TEST_SHUFFLE_UPDATES") != nullptr;
+  std::vector<std::vector<size_t>> upd_row(L);
+  for (size_t l = 0; l < L; ++l) {
+    upd_row[l].resize(layer_rows[l]);
+    for (size_t r = 0; r < layer_rows[l]; ++r) upd_row[l][r] = r;
+    uint32_t st = 0x2545f491u ^ (uint32_t)(l * 2654435761u + 17);
+    for (size_t r = layer_rows[l]; shuffle && r > 1; --r) {  // Fisher-Yates
+      st ^= st << 13;
+      st ^= st >> 17;
+      st ^= st << 5;
+      std::swap(upd_row[l][r - 1], upd_row[l][st % r]);
+    }
+  }
+  auto upd_ids_of = [&](size_t l) {
+    std::vector<size_t> ids(layer_rows[l]);
+    for (size_t j = 0; j < layer_rows[l]; ++j) ids[j] = first_in_table[l] + upd_row[l][j];
+    return ids;
+  };
   const size_t local_rows = 3;
   std::vector<size_t> local_ids(local_rows);
   for (size_t r = 0; r < local_rows; ++r) local_ids[r] = 1000 + r;
@@ -144,7 +166,7 @@ int main(int argc, char **argv) {
   if (use_local) h_local = ps->VirtualLocalAccess(local_ids, true);
   for (size_t l = 0; l < L; ++l) h_read[l] = ps->VirtualRead(table_of[l], ids_of(l), slack);
   for (size_t l = L; l-- > 0;) {
-    h_pre[l] = ps->VirtualPreUpdate(table_of[l], ids_of(l));
+    h_pre[l] = ps->VirtualPreUpdate(table_of[l], upd_ids_of(l));
     h_post[l] = ps->VirtualPostRead(h_read[l]);
     h_upd[l] = ps->VirtualUpdate(h_pre[l]);
   }
@@ -159,7 +181,10 @@ int main(int argc, char **argv) {
       RowOpVal *buf = nullptr;
       ps->PreUpdate(h_pre[l], &buf);
       const size_t e0 = first[l] * ROW_DATA_SIZE, ne = layer_rows[l] * ROW_DATA_SIZE;
-      for (size_t e = 0; e < ne; ++e) host[e0 + e] = delta(pid, c, e0 + e, fl);
+      for (size_t j = 0; j < layer_rows[l]; ++j)  // buffer row j carries blob row upd_row[l][j]
+        for (size_t v = 0; v < ROW_DATA_SIZE; ++v)
+          host[e0 + j * ROW_DATA_SIZE + v] =
+              delta(pid, c, e0 + upd_row[l][j] * ROW_DATA_SIZE + v, fl);
       HCK(hipMemcpy(buf, host.data() + e0, ne * 4, hipMemcpyHostToDevice));
       if (post_read) ps->PostRead(h_post[l]);
       ps->Update(h_upd[l]);

@@ -368,3 +368,19 @@ def test_one_process_per_gpu(dev):
                     extra_env={"GEEPS_TEST_SPREAD_DEVICES": "1"})
     for s in _stats(outs):
         assert all(srv["nr_peer_staged"] > 0 for srv in s["servers"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,mode,slack", [(1, "float", 0), (2, "int", 0), (3, "int", 1)])
+def test_shuffled_update_rows(dev, P, mode, slack):
+    """Every PreUpdate lists its blob's rows in a shuffled order, so each update
+    op's DoubleIndex is a permutation and its per-channel row plan really
+    reorders it (cache rows follow the Reads' order): Reads stay exact
+    (bit-exact with float deltas at one process)."""
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    base = _ports(P, 2)
+    env = _env("ipc", extra={"GEEPS_TEST_SHUFFLE_UPDATES": "1"})
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), "2000", "6", str(slack), "2", "0", mode,
+                     "700,5,900,395"], env) for p in range(P)]
+    _collect(procs, 240)
