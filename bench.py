@@ -380,8 +380,9 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
       scatter_init         gp_scatter_init_rows: fused zerofy + add (common-util.hpp:445-456 + a3)
       scatter_init_planned the same through the plan
       gather               gp_gather_rows (assign_rows_to_double_index_gpu, :39-72)
-    Algorithmic bytes per call: add 3*R*512 + 16*R, init / gather
-    2*R*512 + 16*R (rows + the 16-B DoubleIndex entries)."""
+    Algorithmic bytes per call: add 3*R*512, init / gather 2*R*512, plus the
+    16-B DoubleIndex entries the kernel reads (every row unplanned; a plan's
+    residual rows planned -- its dense runs read no index)."""
     from geeps_amd import rowops
     R = rows * W // 128
     stream = torch.cuda.current_stream()
@@ -403,8 +404,11 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             if only and name not in only:
                 continue
             planned = name.endswith("_planned")
-            nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * R
+            # dense runs read no index; residual rows (and unplanned calls) do
+            index_rows = info["residual_rows"] if planned else R
+            nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * index_rows
             writes = R * 512
+            launches = 1
             if name == "scatter_add":
                 fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                    validate=False)
@@ -419,8 +423,11 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                 kernel = "row_wave_kernel"
             else:
                 fn = (lambda: plan.add(y, x)) if name == "scatter_add_planned" else (lambda: plan.init(y, x))
-                kernel = "row_wave_kernel"
-            launches = 1
+                if info["dense_rows"] == R:  # one dense run: the phased 1-bucket sum (init: ZIN form)
+                    kernel = "bucket_sum_phased_kernel"
+                    launches = sum_launch_plan(R * 128, 1)["launches"]
+                else:
+                    kernel = "row_wave_kernel"
             avg = _time_calls(fn, reps, stream)
             gbps = nbytes / (avg / 1e3) / 1e9
             leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),

@@ -104,8 +104,11 @@ __device__ __forceinline__ f4 ld_stream(const f4 *p) {
 }
 
 // UNROLL consecutive block-strides per thread: (NB + 1) * UNROLL independent
-// 16-B loads are in flight per lane before the first add.
-template <int NB, int UNROLL>
+// 16-B loads are in flight per lane before the first add.  ZIN (every form
+// below has it): `in` is not read and the sum starts from +0.0f, so
+// out = 0.0f + b0 -- the fused zerofy + scatter-add of a row plan's dense run
+// (gp_scatter_init_rows_planned; 0.0f + -0.0f = +0.0f as after a memset).
+template <int NB, int UNROLL, bool ZIN = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4) {
   const size_t tile = (size_t)kBlock * UNROLL;
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
     f4 acc[UNROLL];
     f4 v[NB][UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) acc[u] = in[base + u * kBlock];
+    for (int u = 0; u < UNROLL; ++u) acc[u] = ZIN ? f4(0.0f) : in[base + u * kBlock];
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
   for (int u = 0; u < UNROLL; ++u) {
     const size_t i = base + u * kBlock;
     if (i < n4) {
-      f4 acc = in[i];
+      f4 acc = ZIN ? f4(0.0f) : in[i];
 #pragma unroll
       for (int k = 0; k < NB; ++k) acc += ld_stream(bp[k] + i);
       out[i] = acc;
@@ -146,13 +149,13 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
 }
 
 // Scalar form: unaligned pointers and the < 4-float tail.
-template <int NB>
+template <int NB, bool ZIN = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
     float *__restrict__ out, const float *__restrict__ in, BucketPtrs b,
     size_t n) {
   const size_t stride = (size_t)gridDim.x * kBlock;
   for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    float acc = in[i];
+    float acc = ZIN ? 0.0f : in[i];
 #pragma unroll
     for (int k = 0; k < NB; ++k) acc += b.p[k][i];
     out[i] = acc;
@@ -236,7 +239,7 @@ PhasePlan phase_plan(size_t n4_tiles) {
 // all compile-time: the fixed forms measured 18 % slower with the tile count
 // and chunks per launch passed at run time: "prod" rows at 200 and 512 MiB
 // in profiles/r01b/balance_tune_runtime_tiles.txt.
-template <int NB, int RT, bool BAL>
+template <int NB, int RT, bool BAL, bool ZIN = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
     size_t chunk0, int bal_tiles) {
@@ -263,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
       f4 acc[U];
       f4 v[NB][U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] = ld_stream(in + base + u * kBlock);
+      for (int u = 0; u < U; ++u) acc[u] = ZIN ? f4(0.0f) : ld_stream(in + base + u * kBlock);
 #pragma unroll
       for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -296,12 +299,12 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
   }
 }
 
-template <int NB, int RT, bool BAL>
+template <int NB, int RT, bool BAL, bool ZIN = false>
 void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_tiles,
                    const PhasePlan &p, hipStream_t s) {
   const size_t G = (size_t)num_cus();
   for (size_t l = 0; l < p.launches; ++l)
-    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT, BAL>), dim3((unsigned)G), dim3(kBlock), 0,
+    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT, BAL, ZIN>), dim3((unsigned)G), dim3(kBlock), 0,
                        s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
                        n4_tiles, l * (size_t)p.per_launch, p.tiles);
 }
@@ -411,19 +414,20 @@ BucketPtrs offset_buckets(const BucketPtrs &b, size_t off) {
 
 // out[i] = in[i] + b0[i] + ... over i < n: the phase-separated form over the
 // whole 16-KiB tiles of a large shard, the mixed dwordx4 form over what is
-// left of the 16-B-aligned part, the scalar form over the rest.  The CU count
-// is read once, so the plan and every grid of the call agree.
-template <int NB>
+// left of the 16-B-aligned part, the scalar form over the rest.  ZIN: `in` is
+// ignored (may be null) and out[i] = 0.0f + b0[i] + ...  The CU count is read
+// once, so the plan and every grid of the call agree.
+template <int NB, bool ZIN = false>
 int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
                          size_t n, hipStream_t s) {
   const size_t G = (size_t)num_cus();
-  bool vec = aligned16(out) && aligned16(in);
+  bool vec = aligned16(out) && (ZIN || aligned16(in));
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
   size_t done = 0;  // floats summed so far
   if (vec) {
     // 3-8 buckets: whole sweep chunks first, one launch each
-    const size_t sweeps = sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
-    if constexpr (NB >= kSweepMinBuckets)
+    const size_t sweeps = ZIN ? 0 : sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
+    if constexpr (NB >= kSweepMinBuckets && !ZIN)
       for (size_t c = 0; c < sweeps; ++c)
         hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB>), dim3((unsigned)G), dim3(kBlock),
                            0, s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
@@ -434,13 +438,15 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     const PhasePlan p = phase_plan<NB>(n4_tiles);
     if (p.rt >= 0) {
       const BucketPtrs bo = offset_buckets<NB>(b, done);
+      const float *ip = ZIN ? nullptr : in + done;
       if (p.balanced)
-        launch_phased<NB, phase_reg_tiles<NB>(), true>(out + done, in + done, bo, n4_tiles, p, s);
+        launch_phased<NB, phase_reg_tiles<NB>(), true, ZIN>(out + done, ip, bo, n4_tiles, p, s);
       else
-        launch_phased<NB, phase_reg_tiles<NB>(), false>(out + done, in + done, bo, n4_tiles, p, s);
+        launch_phased<NB, phase_reg_tiles<NB>(), false, ZIN>(out + done, ip, bo, n4_tiles, p, s);
       done += n4_tiles * 4;
     }
   }
+  const float *in_at = ZIN ? nullptr : in + done;
   if (vec && n - done >= 4) {
     // 4 block-strides per thread at 2 blocks per CU: (NB + 1) * 4 dwordx4 loads
     // in flight per lane.  Measured on MI355X at 8 x 4 GiB buckets: +2-3 % over
@@ -451,17 +457,18 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     const size_t tiles = (n4 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
     const size_t cap = G * kPerCU;
     const size_t grid = tiles < cap ? tiles : cap;
-    hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U, ZIN>), dim3((unsigned)grid),
                        dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out + done),
-                       reinterpret_cast<const f4 *>(in + done), offset_buckets<NB>(b, done), n4);
+                       reinterpret_cast<const f4 *>(in_at), offset_buckets<NB>(b, done), n4);
     done += n4 * 4;
+    in_at = ZIN ? nullptr : in + done;
   }
   if (done < n) {
     const size_t rem = n - done;
     size_t grid = (rem + kBlock - 1) / kBlock;
     if (grid > G * kBlocksPerCU) grid = G * kBlocksPerCU;
-    hipLaunchKernelGGL((bucket_sum_scalar_kernel<NB>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, s, out + done, in + done, offset_buckets<NB>(b, done), rem);
+    hipLaunchKernelGGL((bucket_sum_scalar_kernel<NB, ZIN>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, out + done, in_at, offset_buckets<NB>(b, done), rem);
   }
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;
@@ -922,8 +929,8 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
   if constexpr (kWaveShape && (kWaveGather || kWaveScatter)) {
     // Wave-level index map (row_wave_kernel): the gather of rows up to 128
     // floats, the fused init always, the scatter-add when its rows are sorted
-    // by destination (a row plan; in op order its random read-modify-write
-    // side runs 3-8 % slower here than in row_op_kernel).  Rows in flight per group: 8 at
+    // by destination (a row plan's residual; in op order its random
+    // read-modify-write side runs 3-8 % slower here than in row_op_kernel).  Rows in flight per group: 8 at
     // 32 lanes per row (16 spilled past 256 VGPRs: 9 % slower), 16 at 16 lanes.
     constexpr int RPG = LPR == 32 ? 8 : 16;
     if (kWaveGather || OP == kInitFrom || sorted) {
@@ -1045,24 +1052,41 @@ int launch_row_op_seg(float *flat_ptr, const gp_row_segments *t,
 // Row plans: a scatter DoubleIndex compiled once (libgeeps' indexes are fixed
 // at FinishVirtualIteration, clientlib-viter.cpp:817-883).
 //
-// The plan holds the rows ordered by destination (id1), offsets applied.
-// That is bit-neutral because destinations are distinct: every destination
-// row receives exactly the same adds whatever order the rows are visited in.
-// In that order the read-modify-write side of the scatter walks the oplog
-// front to back, like the gather's write side, and the rows go to the
-// wave-map kernel with non-temporal oplog accesses, one resident round of
-// blocks: 78-81 % of 8 TB/s for the add and 73-81 % for the fused init on
-// random / identity indexes of 8 M rows, against 63-66 % / 62-68 % for the
-// same index in op order through row_op_kernel (profiles/r02/plan_tune*.txt).
-// Dense runs moved by the bucket-sum kernels instead were measured and not
-// kept: 75-81 % for the add and 71 % for the init.
+// The plan visits the rows in destination (id1) order, offsets applied.  That
+// is bit-neutral because destinations are distinct: every destination row
+// receives exactly the same adds whatever order the rows are visited in.
+//  * Dense runs: maximal runs in which id0 and id1 both step by one and every
+//    row is clear of num_vals_limit are plain ranges y[y0 .. y0 + L*W) (+)=
+//    x[x0 .. x0 + L*W).  Runs of at least kDenseRunBytes go to the phase-
+//    separated sum kernels (one bucket; the fused init through their ZIN
+//    form), which read no index and, unlike any single-pass form, keep their
+//    rate on every allocation: over 10 fresh allocations the add ran 76.5-
+//    80.9 % of 8 TB/s this way against 63-80 % through the wave-map kernel,
+//    which fell to 63-69 % on 7 of them (profiles/r02/tune/rowop_alloc*.txt).
+//    libgeeps assigns cache rows in first-access order, so an op's rows are
+//    typically one run per channel.
+//  * The other rows keep a device index, sorted by id1, for the wave-map
+//    kernel with non-temporal oplog accesses and one resident round of blocks:
+//    the read-modify-write side walks the oplog front to back like the
+//    gather's write side: 77-79 % for a random permutation, against 63-65 %
+//    for the same index in op order through row_op_kernel (plan_tune*.txt).
 // ---------------------------------------------------------------------------
+// A dense run launches 1-3 kernels; below 4 MiB (the phased form's smallest
+// shard) the row kernel moves it without the launches.
+constexpr size_t kDenseRunBytes = 4u << 20;
+
+struct RowRun {
+  uint64_t x_row, y_row, rows;  // offsets applied
+};
+
 }  // namespace
 
 struct gp_row_plan_s {
   size_t num_rows = 0, row_size = 0, limit = 0;
-  size_t runs = 0;                   // maximal runs where id0 and id1 both step by one
-  gp_double_index *index = nullptr;  // device, offsets applied, ascending id1
+  std::vector<RowRun> dense;
+  size_t dense_rows = 0;
+  gp_double_index *residual = nullptr;  // device, offsets applied, ascending id1
+  size_t residual_rows = 0;
   int device = 0;
 };
 
@@ -1070,6 +1094,7 @@ namespace {
 
 int build_row_plan(gp_row_plan_s *p, const gp_double_index *host_index, size_t n,
                    gp_double_index off) {
+  const size_t W = p->row_size;
   std::vector<gp_double_index> rows(n);
   for (size_t r = 0; r < n; ++r)
     rows[r] = gp_double_index{host_index[r].id0 + off.id0, host_index[r].id1 + off.id1};
@@ -1080,12 +1105,28 @@ int build_row_plan(gp_row_plan_s *p, const gp_double_index *host_index, size_t n
     if (rows[r].id1 == rows[r - 1].id1)
       return set_error(GP_ERR_INVALID, "row plan: destination row " + std::to_string(rows[r].id1) +
                                            " repeats (scatter destinations must be distinct)");
-  p->runs = n ? 1 : 0;
-  for (size_t r = 1; r < n; ++r)
-    p->runs += !(rows[r].id0 == rows[r - 1].id0 + 1 && rows[r].id1 == rows[r - 1].id1 + 1);
-  if (n) {
-    GP_HIP_TRY(hipMalloc(&p->index, n * sizeof(gp_double_index)));
-    GP_HIP_TRY(hipMemcpy(p->index, rows.data(), n * sizeof(gp_double_index), hipMemcpyHostToDevice));
+  auto whole = [&](const gp_double_index &d) { return (d.id0 + 1) * W <= p->limit; };
+  const size_t min_rows = std::max<size_t>(1, kDenseRunBytes / (W * sizeof(float)));
+  std::vector<gp_double_index> rest;
+  for (size_t a = 0; a < n;) {
+    size_t b = a + 1;
+    if (whole(rows[a]))
+      while (b < n && whole(rows[b]) && rows[b].id0 == rows[b - 1].id0 + 1 &&
+             rows[b].id1 == rows[b - 1].id1 + 1)
+        ++b;
+    if (whole(rows[a]) && b - a >= min_rows) {
+      p->dense.push_back(RowRun{rows[a].id0, rows[a].id1, b - a});
+      p->dense_rows += b - a;
+    } else {
+      rest.insert(rest.end(), rows.begin() + a, rows.begin() + b);
+    }
+    a = b;
+  }
+  p->residual_rows = rest.size();
+  if (!rest.empty()) {
+    GP_HIP_TRY(hipMalloc(&p->residual, rest.size() * sizeof(gp_double_index)));
+    GP_HIP_TRY(hipMemcpy(p->residual, rest.data(), rest.size() * sizeof(gp_double_index),
+                         hipMemcpyHostToDevice));
   }
   return GP_OK;
 }
@@ -1097,12 +1138,25 @@ template <int OP>
 int launch_planned(float *y, const float *x, const gp_row_plan_s *p, hipStream_t s) {
   if (!p) return set_error(GP_ERR_INVALID, "null row plan");
   if (p->num_rows == 0) return GP_OK;
-  int dev = -1;
-  GP_HIP_TRY(hipGetDevice(&dev));
-  if (dev != p->device)
-    return set_error(GP_ERR_INVALID, "row plan used on another device than it was built on");
-  return launch_row_op<OP>(y, x, p->index, p->num_rows, gp_double_index{0, 0}, p->row_size,
-                           p->limit, s, /*sorted=*/true);
+  if (p->residual_rows) {
+    int dev = -1;
+    GP_HIP_TRY(hipGetDevice(&dev));
+    if (dev != p->device)
+      return set_error(GP_ERR_INVALID, "row plan used on another device than it was built on");
+  }
+  const size_t W = p->row_size;
+  for (const RowRun &r : p->dense) {
+    BucketPtrs b = {};
+    b.p[0] = x + r.x_row * W;
+    float *yr = y + r.y_row * W;
+    const int rc = OP == kAddFrom ? launch_bucket_sum_nb<1>(yr, yr, b, r.rows * W, s)
+                                  : launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s);
+    if (rc != GP_OK) return rc;
+  }
+  if (p->residual_rows)
+    return launch_row_op<OP>(y, x, p->residual, p->residual_rows, gp_double_index{0, 0}, W,
+                             p->limit, s, /*sorted=*/true);
+  return GP_OK;
 }
 
 }  // namespace
@@ -1182,16 +1236,18 @@ int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, siz
 
 int gp_row_plan_destroy(gp_row_plan plan) {
   if (!plan) return GP_OK;
-  const hipError_t e = plan->index ? hipFree(plan->index) : hipSuccess;
+  const hipError_t e = plan->residual ? hipFree(plan->residual) : hipSuccess;
   delete plan;
   GP_HIP_TRY(e);
   return GP_OK;
 }
 
-int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *runs) {
-  if (!plan || !num_rows || !runs) return set_error(GP_ERR_INVALID, "null pointer");
+int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *dense_runs, size_t *dense_rows) {
+  if (!plan || !num_rows || !dense_runs || !dense_rows)
+    return set_error(GP_ERR_INVALID, "null pointer");
   *num_rows = plan->num_rows;
-  *runs = plan->runs;
+  *dense_runs = plan->dense.size();
+  *dense_rows = plan->dense_rows;
   return GP_OK;
 }
 

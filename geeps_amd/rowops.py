@@ -171,7 +171,9 @@ def assign_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, inde
 
 class RowPlan:
     """A scatter DoubleIndex compiled once (gp_row_plan_create): the rows in
-    destination (id1) order on the device, run by the wave-map row kernel.
+    destination (id1) order; id0/id1-contiguous runs of >= 4 MiB moved by the
+    phase-separated sum kernels, the rest by the wave-map row kernel over an
+    id1-sorted device index.
 
     ``index``: (n, 2) int64 array or tensor (copied to the host once), as for
     add_rows_from_double_index_gpu; ``index_offset`` and ``num_vals_limit``
@@ -209,10 +211,11 @@ class RowPlan:
                                               self.row_size, self.limit), "gp_row_plan_create")
 
     def info(self) -> dict:
-        a, b = ctypes.c_size_t(), ctypes.c_size_t()
-        check(native.lib().gp_row_plan_info(self._h, ctypes.byref(a), ctypes.byref(b)),
-              "gp_row_plan_info")
-        return {"rows": a.value, "runs": b.value}
+        a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        check(native.lib().gp_row_plan_info(self._h, ctypes.byref(a), ctypes.byref(b),
+                                            ctypes.byref(c)), "gp_row_plan_info")
+        return {"rows": a.value, "dense_runs": b.value, "dense_rows": c.value,
+                "residual_rows": a.value - c.value}
 
     def _run(self, fn, y, x, stream, what):
         _dev_f32(y, "rows_y")

@@ -120,11 +120,14 @@ int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
  * Row plans: a scatter DoubleIndex compiled once, for ops whose index is fixed
  * (libgeeps builds one per op and channel at FinishVirtualIteration, where the
  * reference builds the op's device DoubleIndex: vi_create_double_index,
- * src/client/clientlib-viter.cpp:817-883).  The plan keeps the rows in
- * destination (id1) order with the offsets applied -- bit-neutral, since
- * destinations are distinct -- so the scatter's read-modify-write side walks
- * y front to back.  Results are bit-identical to gp_scatter_add_rows /
- * gp_scatter_init_rows over the same index, offset and num_vals_limit.
+ * src/client/clientlib-viter.cpp:817-883).  The plan visits the rows in
+ * destination (id1) order -- bit-neutral, since destinations are distinct.
+ * Runs in which id0 and id1 both step by one (whole rows, at least 4 MiB) are
+ * moved as dense ranges by the phase-separated sum kernels; the other rows
+ * keep a device index, sorted by id1, for the row kernels, so the scatter's
+ * read-modify-write side walks y front to back.  Results are bit-identical to
+ * gp_scatter_add_rows / gp_scatter_init_rows over the same index, offset and
+ * num_vals_limit.
  * ------------------------------------------------------------------------- */
 typedef struct gp_row_plan_s *gp_row_plan;
 
@@ -135,9 +138,9 @@ typedef struct gp_row_plan_s *gp_row_plan;
 int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
                        gp_double_index offset, size_t row_size, size_t num_vals_limit);
 int gp_row_plan_destroy(gp_row_plan plan);
-/* The plan's rows, and how many maximal runs they form in destination order
- * where id0 and id1 both step by one (1 for an identity-like index). */
-int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *runs);
+/* The plan's rows, its dense runs and the rows in them (the rest go to the
+ * row kernels). */
+int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *dense_runs, size_t *dense_rows);
 /* gp_scatter_add_rows(y, x, index, ...) through the plan (a3:
  * add_rows_from_double_index_gpu, src/common/row-op-util.cu:109-142). */
 int gp_scatter_add_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s);

@@ -167,20 +167,37 @@ def _plan(idx, offset=(0, 0), row_size=128, limit=None):
 
 
 def _info(h):
-    a, b = ctypes.c_size_t(), ctypes.c_size_t()
-    assert native.lib().gp_row_plan_info(h, ctypes.byref(a), ctypes.byref(b)) == 0
-    return a.value, b.value
+    a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    assert native.lib().gp_row_plan_info(h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == 0
+    return a.value, b.value, c.value
 
 
-def test_empty_row_plan_without_device():
-    """An empty plan holds no device memory, so it is built and freed here."""
+def test_row_plan_classifies_dense_runs_without_device():
+    """Plans whose rows all fall in dense runs need no device memory, so the
+    host-side classifier runs here: runs of >= 4 MiB where id0 and id1 both
+    step by one, found after sorting by id1 (any op row order), offsets
+    applied; empty plans too."""
     import numpy as np
     L = native.lib()
+    R = 8192  # one 4-MiB run at 128 floats
+    rc, h = _plan(np.stack([np.arange(R), np.arange(R)], 1))
+    assert rc == 0 and _info(h) == (R, 1, R)
+    L.gp_row_plan_destroy(h)
+    # two runs listed in reverse op order, the second's destinations below the first's
+    two = np.concatenate([np.stack([np.arange(R), 5 * R + np.arange(R)], 1),
+                          np.stack([R + np.arange(R), np.arange(R)], 1)])[::-1]
+    rc, h = _plan(two, offset=(3, 7))
+    assert rc == 0 and _info(h) == (2 * R, 2, 2 * R)
+    L.gp_row_plan_destroy(h)
+    # 64-float rows: a run needs 16384 rows
+    rc, h = _plan(np.stack([np.arange(2 * R), np.arange(2 * R)], 1), row_size=64)
+    assert rc == 0 and _info(h) == (2 * R, 1, 2 * R)
+    L.gp_row_plan_destroy(h)
     rc, h = _plan(np.zeros((0, 2)))
-    assert rc == 0 and _info(h) == (0, 0)
+    assert rc == 0 and _info(h) == (0, 0, 0)
     assert L.gp_row_plan_destroy(h) == 0
     assert L.gp_row_plan_destroy(None) == 0
-    assert L.gp_row_plan_info(None, None, None) == native.GP_ERR_INVALID
+    assert L.gp_row_plan_info(None, None, None, None) == native.GP_ERR_INVALID
 
 
 def test_row_plan_rejects_repeated_destinations():

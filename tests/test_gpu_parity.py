@@ -585,10 +585,12 @@ def test_row_plan_matches_oracle(dev, kind, W, limit_frac, off):
     plan = rowops.RowPlan(idx, n_op, off, W, limit)
     info = plan.info()
     assert info["rows"] == n_op
-    if kind == "identity":
-        assert info["runs"] == 1
-    if kind == "mixed":
-        assert info["runs"] >= 6
+    if kind == "identity" and limit is None:
+        assert info == {"rows": n_op, "dense_runs": 1, "dense_rows": n_op, "residual_rows": 0}
+    if kind == "mixed" and limit is None:
+        assert info["dense_runs"] == 3 and info["residual_rows"] > 0
+    if kind == "permuted":
+        assert info["dense_runs"] == 0
     # add
     e = y.copy()
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
@@ -610,8 +612,8 @@ def test_row_plan_matches_oracle(dev, kind, W, limit_frac, off):
 
 
 def test_row_plan_unaligned_and_side_stream(dev):
-    """Bases 4 B off 16-B alignment (the scalar row kernel) on a side stream:
-    still bit-exact."""
+    """Bases 4 B off 16-B alignment (a dense run takes the scalar sum form, the
+    residual the scalar row kernel) on a side stream: still bit-exact."""
     from geeps_amd import rowops
     rng = np.random.default_rng(9)
     W, n = 128, 20000
@@ -623,7 +625,7 @@ def test_row_plan_unaligned_and_side_stream(dev):
     e = y[1:].copy()
     oracle.add_rows_from_double_index(e, x[1:].copy(), idx, (0, 0), W)
     plan = rowops.RowPlan(idx, row_size=W)
-    assert plan.info()["rows"] == n and plan.info()["runs"] >= 2
+    assert plan.info()["dense_runs"] == 1 and plan.info()["residual_rows"] == n - 12000
     ty, tx = T(y, dev), T(x, dev)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
