@@ -33,7 +33,9 @@ cpu_baseline = the oracle's restatement of the reference server arithmetic
 Other legs at N = 1 (rank 0): config2 (BASELINE configs[1], 2 clients),
 client_rowops (scatter-add / fused init / gather of the table's 8M RowData
 rows, random and identity DoubleIndex, unplanned and through a row plan),
-host_inclusive (pinned H2D + sum + D2H, serialized and pipelined, full table).
+host_inclusive (pinned H2D + sum + D2H, serialized and pipelined, full table),
+libgeeps_clock (the drop-in library's clock through include/geeps.hpp, 1 and
+2 processes on the same 4 GiB table).
 """
 from __future__ import annotations
 
@@ -100,6 +102,8 @@ def parse(argv=None):
     p.add_argument("--rowops-index", nargs="*", default=["random", "identity"],
                    choices=["random", "identity"], help="DoubleIndex kinds of the row-op legs")
     p.add_argument("--no-config2", action="store_true")
+    p.add_argument("--no-e2e", action="store_true",
+                   help="skip the libgeeps end-to-end clock leg")
     p.add_argument("--no-hbm-probe", action="store_true")
     p.add_argument("--layout", choices=["arena", "separate"], default="arena",
                    help="HBM layout of buckets + master: one arena (master last) or one "
@@ -543,6 +547,36 @@ def load_traffic(workload_key, kernel):
         return None
 
 
+def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
+    """The drop-in path end to end: scripts/apps/geeps_clock_bench (built by
+    __graft_entry__.build() against libgeeps.so and include/geeps.hpp, as an
+    app links) run as P processes on this GPU, one GeePS worker + tablet server
+    each, same-node IPC transport.  The table is the bench's rows x W fp32 as
+    RowData rows (rows * W / 128 of them).  One clock = Read (gather from the
+    segmented param cache) -> PreUpdate -> device fill -> PostRead -> Update
+    (fused init through the row plan) -> Clock (push, the server's bucket sum,
+    the zero-copy refresh), through the public API.  P = 2 is configs[1]'s
+    2 loopback clients; every worker updates every row each clock.
+    delta_GBps = P * table bytes / the slowest worker's ms per clock."""
+    import importlib.util
+    path = os.path.join(REPO, "scripts", "run_clock_bench.py")
+    spec = importlib.util.spec_from_file_location("run_clock_bench", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    if not os.path.exists(mod.BIN):
+        return {"skipped": f"{os.path.relpath(mod.BIN, REPO)} not built (__graft_entry__.build())"}
+    rd_rows = rows * W // 128
+    out = {"app": "scripts/apps/geeps_clock_bench.cpp", "rows": rd_rows, "row_size": 128,
+           "table_bytes": rd_rows * 512, "transport": "ipc (same node)", "clocks": clocks,
+           "warmup": warmup}
+    for P in procs:
+        r = mod.run(P, rd_rows, clocks, warmup, 0, "ipc", timeout=300)
+        out[f"p{P}"] = {"workers": P, "ms_per_clock": r["ms_per_clock_max"],
+                        "delta_GBps": r["aggregate_delta_GBps"],
+                        "ms_per_clock_each": r["ms_per_clock"]}
+    return out
+
+
 def config2_leg(deltas, master, dev, probe=None, reps=5):
     """BASELINE configs[1]: the same 1M x 1024 shard, 2 client buckets (the
     first two resident deltas, client order 0, 1) summed into the master by one
@@ -628,6 +662,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
     rowops_res = None
     probe = None
     config2 = None
+    e2e = None
     if rank == 0 and world == 1 and dev.type == "cuda":
         if not args.no_hbm_probe:
             log("[rank 0] HBM probes")
@@ -646,6 +681,12 @@ def main(argv=None, backend="nccl", apply_fn=None):
             rowops_res = rowops_leg(R, W, dev, indexes=tuple(args.rowops_index),
                                     only=args.rowops_only, probe=probe)
             torch.cuda.empty_cache()
+        if not args.no_e2e:
+            log("[rank 0] libgeeps end-to-end clock leg")
+            try:
+                e2e = libgeeps_leg(R, W)
+            except Exception as exc:  # a side leg: report it, keep the headline line
+                e2e = {"error": f"{type(exc).__name__}: {str(exc)[-500:]}"}
         if not args.no_host_inclusive:
             log("[rank 0] host-inclusive leg")
             host_inc = host_inclusive(R, W, C, dev)
@@ -710,6 +751,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
             line["host_inclusive"] = host_inc
         if rowops_res:
             line["client_rowops"] = rowops_res
+        if e2e:
+            line["libgeeps_clock"] = e2e
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

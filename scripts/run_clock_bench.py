@@ -54,10 +54,8 @@ def free_base(P):
     return free_port_base(P, 1)
 
 
-def main():
-    P, rows, clocks, warmup, slack = (int(a) for a in sys.argv[1:6])
-    transport = sys.argv[6] if len(sys.argv) > 6 else "ipc"
-    out = sys.argv[7] if len(sys.argv) > 7 else None
+def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900):
+    """Run the P processes; return the aggregate dict (raises on a failure)."""
     env = dict(os.environ)
     # P processes share the box's ONE GPU.  At the default 4 hardware queues
     # per process, 8 processes oversubscribe the GPU's queue slots and are
@@ -85,24 +83,39 @@ def main():
     procs = [subprocess.Popen(cmd(p),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
              for p in range(P)]
-    results, failed = [], False
+    results, errors = [], []
     for p, pr in enumerate(procs):
-        o, e = pr.communicate(timeout=900)
+        try:
+            o, e = pr.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
         if pr.returncode != 0:
-            failed = True
-            sys.stderr.write(f"process {p} rc={pr.returncode}\n{e[-2000:]}\n")
+            errors.append(f"process {p} rc={pr.returncode}\n{e[-2000:]}")
             continue
         results.append(json.loads(o.strip().splitlines()[-1]))
-    if failed:
-        sys.exit(1)
+    if errors:
+        raise RuntimeError("\n".join(errors))
     worst = max(r["ms_per_clock"] for r in results)
     table = results[0]["table_bytes"]
-    line = {"workers": P, "rows": rows, "table_bytes": table, "slack": slack,
+    return {"workers": P, "rows": rows, "table_bytes": table, "slack": slack,
             "transport": transport, "clocks": clocks, "warmup": warmup,
             "ms_per_clock_max": worst,
             "ms_per_clock": [r["ms_per_clock"] for r in results],
             "aggregate_delta_GBps": round(P * table / (worst * 1e-3) / 1e9, 2),
             "probe": [r["probe"] for r in results]}
+
+
+def main():
+    P, rows, clocks, warmup, slack = (int(a) for a in sys.argv[1:6])
+    transport = sys.argv[6] if len(sys.argv) > 6 else "ipc"
+    out = sys.argv[7] if len(sys.argv) > 7 else None
+    try:
+        line = run(P, rows, clocks, warmup, slack, transport)
+    except RuntimeError as e:
+        sys.stderr.write(f"{e}\n")
+        sys.exit(1)
     print(json.dumps(line))
     if out:
         with open(out, "w") as f:
