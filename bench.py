@@ -56,13 +56,14 @@ METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roo
 def sum_launch_plan(num_vals: int, num_buckets: int) -> dict:
     """The dominant kernel of one N-way sum of num_vals floats and how many
     launches of it one sum issues, from the library's own launch plan
-    (gp_bucket_sum_sweep_plan): at 3-8 buckets, shards of at least 3 whole
-    64-MiB chunks go to bucket_sum_sweep_kernel (the 4 GiB headline shard and
-    its 1/2, 1/4, 1/8 slices are whole chunks), any rest to
-    bucket_sum_phased_kernel (`other_launches`); at 1-2 buckets the phased
-    kernel takes shards of >= 4 MiB; smaller ones bucket_sum_vec_kernel in one
-    launch.  `launches` counts the dominant kernel only, so a per-launch time
-    or byte figure divides by the launches rocprofv3 averages over."""
+    (gp_bucket_sum_sweep_plan): shards of at least 3 whole sweep chunks go to
+    bucket_sum_sweep_kernel (64-MiB chunks at 3-8 buckets: the 4 GiB headline
+    shard and its 1/2, 1/4, 1/8 slices are whole chunks; 96-MiB chunks at 1-2
+    buckets), any rest to bucket_sum_phased_kernel (`other_launches`); smaller
+    shards of >= 4 MiB to the phased kernel alone; smaller ones
+    bucket_sum_vec_kernel in one launch.  `launches` counts the dominant kernel
+    only, so a per-launch time or byte figure divides by the launches rocprofv3
+    averages over."""
     import ctypes
     from geeps_amd import native
     launches, reg_tiles, sweeps = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
@@ -412,7 +413,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             index_rows = info["residual_rows"] if planned else R
             nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * index_rows
             writes = R * 512
-            launches = 1
+            launches, other = 1, 0
             if name == "scatter_add":
                 fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                    validate=False)
@@ -426,10 +427,13 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                                                                     validate=False)
                 kernel = "row_wave_kernel"
             else:
-                fn = (lambda: plan.add(y, x)) if name == "scatter_add_planned" else (lambda: plan.init(y, x))
-                if info["dense_rows"] == R:  # one dense run: the phased 1-bucket sum (init: ZIN form)
-                    kernel = "bucket_sum_phased_kernel"
-                    launches = sum_launch_plan(R * 128, 1)["launches"]
+                init = name == "scatter_init_planned"
+                fn = (lambda: plan.init(y, x)) if init else (lambda: plan.add(y, x))
+                pl = plan.launches(init)
+                if info["dense_rows"] == R:  # one dense run: the 1-bucket sum (init: zero-input form)
+                    kernel = "bucket_sum_sweep_kernel" if pl["sweep"] else "bucket_sum_phased_kernel"
+                    launches = pl["sweep"] or pl["phased"]
+                    other = pl["sweep"] and pl["phased"]
                 else:
                     kernel = "row_wave_kernel"
             avg = _time_calls(fn, reps, stream)
@@ -437,6 +441,8 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),
                    "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes": nbytes, "kernel": kernel,
                    "launches": launches, "avg_launch_ms": round(avg / launches, 5)}
+            if other:  # a rest in another kernel form: the per-launch figure includes it
+                leg["other_launches"] = other
             mm = model_ms(nbytes - writes, writes, probe)
             if mm:
                 leg["model_ms"] = round(mm, 4)
@@ -589,11 +595,19 @@ def config2_leg(deltas, master, dev, probe=None, reps=5):
     nbytes = 4 * n * 4
     gbps = nbytes / (avg / 1e3) / 1e9
     rows = n // 1024
+    # the dominant kernel's share of the shard (the rest: `other_launches` of
+    # the tile-major form), so the per-launch figure compares with rocprofv3's
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    chunk = {"bucket_sum_sweep_kernel": (10 + (plan["reg_tiles"] or 0)) * cus * 16384 // 4}.get(
+        plan["kernel"])  # floats per chunk: (10 LDS + register) 16-KiB tiles per CU
+    share = min(1.0, plan["launches"] * chunk / n) if chunk else 1.0
     return {"workload": f"configs[1]: 2 clients, {rows} rows x 1024 fp32, 1 shard, device-resident",
             "ms": round(avg, 4), "GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4),
             "delta_GBps": round(2 * n * 4 / (avg / 1e3) / 1e9, 1), "bytes": nbytes,
             "kernel": plan["kernel"], "launches": plan["launches"],
-            "avg_launch_ms": round(avg / plan["launches"], 5),
+            "other_launches": plan["other_launches"],
+            "avg_launch_ms": round(avg * share / plan["launches"], 5),
+            "avg_launch_note": "call time x the dominant kernel's share of the shard / its launches",
             "traffic_source": load_traffic(f"r{rows}_w1024_c2_g1", plan["kernel"]),
             "model_ms": (round(model_ms(3 * n * 4, n * 4, probe), 4) if probe else None)}
 

@@ -309,42 +309,57 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
                        n4_tiles, l * (size_t)p.per_launch, p.tiles);
 }
 
-// Stream-by-stream ("sweep") form of the phased sum, for 3-8 buckets.  Same
-// chunk scheme (LDS + register tiles, then a write phase), but the read phase
-// sweeps the block's tiles once per stream, in bucket order: pass 0 parks the
-// master's (or `in`'s) tiles, pass k adds bucket k-1's tiles into them.  So at
-// any moment the chip reads one contiguous region of one stream instead of
+// Stream-by-stream ("sweep") form of the phased sum.  Same chunk scheme (LDS
+// + register tiles, then a write phase), but the read phase sweeps the
+// block's tiles once per stream, in bucket order: pass 0 parks the master's
+// (or `in`'s) tiles, pass k adds bucket k-1's tiles into them.  So at any
+// moment the chip reads one contiguous region of one stream instead of
 // NB + 1 regions at once, and each pass keeps TG tiles' loads in flight with
 // the same registers at any NB.  The per-element order is unchanged, ((in +
-// b0) + b1) + ..., so the bits are those of every other form.  Measured
-// (scripts/tune/bmaj_tune.hip, profiles/r01b/bmaj_tune_*.txt, 3 arenas): 8
-// buckets 6.42-6.57 ms against 6.62-7.03 ms for the tile-major form, 4
-// buckets 3.92-3.97 against 4.11-4.21 ms, and a far smaller spread between
-// allocations; at 1-2 buckets it ties or loses, so they keep the tile-major
-// form.  16 tiles per block (10 LDS + 6 register) make a 64-MiB chunk on 256
-// CUs, which divides the 4 GiB headline shard and its 1/2, 1/4, 1/8 slices.
+// b0) + b1) + ..., so the bits are those of every other form.  ZIN: no `in`
+// stream; pass 0 parks 0.0f + b0 (-0 -> +0, as after the memset a row plan's
+// fused init replaces).
+// Measured at 3-8 buckets (scripts/tune/bmaj_tune.hip, profiles/r01b/
+// bmaj_tune_*.txt, 3 arenas): 8 buckets 6.42-6.57 ms against 6.62-7.03 ms
+// for the tile-major form, 4 buckets 3.92-3.97 against 4.11-4.21 ms, and a
+// far smaller spread between allocations.  16 tiles per block (10 LDS + 6
+// register) make a 64-MiB chunk on 256 CUs, which divides the 4 GiB headline
+// shard and its 1/2, 1/4, 1/8 slices.
+// Measured at 0-2 buckets in round 2 (scripts/tune/lowb_tune.hip, profiles/
+// r02/tune/lowb_tune.txt, 3 arenas): the tile-major form waits for each
+// tile's loads before the next tile's issue, i.e. 16 KiB in flight per CU at
+// the zero-input form, 32 at 1 bucket, 48 at 2 -- short of the ~56 KiB per
+// CU that ~7 TB/s at ~2 us of loaded latency needs.  The sweep keeps TG tiles
+// in flight: zero-input 75.4-78.5 % of 8 TB/s against 72.0-72.1 % (64-MiB
+// chunks, TG 4); 2 buckets 80.2-80.8 % against 78.6-78.8 % and 1 bucket
+// 79.7-80.0 % against 78.8-79.4 % (96-MiB chunks: 14 register tiles, TG 8).
 // Whole chunks only (no guards: the waitcnt counts stay exact); the caller
 // hands the rest of the shard to the tile-major plan.
-constexpr int kSweepRT = 6;
-constexpr int kSweepTG = 4;  // tiles per burst of loads
-constexpr int kSweepT = kPhaseLdsTiles + kSweepRT;
-constexpr int kSweepMinBuckets = 3;
+template <int NB, bool ZIN>
+struct SweepShape {  // register tiles, tiles per burst of loads
+  static constexpr int RT = (NB <= 2 && !ZIN) ? 14 : 6;
+  static constexpr int TG = (NB <= 2 && !ZIN) ? 8 : 4;
+};
+constexpr int kSweepRT = 6;  // 3-8 buckets and the zero-input form
+constexpr int kSweepTG = 4;
+[[maybe_unused]] constexpr int kSweepT = kPhaseLdsTiles + kSweepRT;  // tuning harnesses
 
 // RT register tiles, bursts of TG tiles (template arguments so the tuning
-// harness can instantiate other shapes; production uses kSweepRT, kSweepTG).
-template <int NB, int RT = kSweepRT, int TG = kSweepTG>
+// harnesses can instantiate other shapes; production uses SweepShape).
+template <int NB, int RT = kSweepRT, int TG = kSweepTG, bool ZIN = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
     size_t chunk) {
   constexpr int U = kPhaseU;
   constexpr int kT = kPhaseLdsTiles + RT;
+  constexpr int S = ZIN ? NB : NB + 1;  // streams read
   static_assert(kT % TG == 0, "whole bursts");
   __shared__ f4 res[kPhaseLdsF4];
   f4 keep[RT][U];
-  const f4 *src[NB + 1];
-  src[0] = in;
+  const f4 *src[S];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) src[k + 1] = reinterpret_cast<const f4 *>(b.p[k]);
+  for (int k = 0; k < S; ++k)
+    src[k] = (!ZIN && k == 0) ? in : reinterpret_cast<const f4 *>(b.p[ZIN ? k : k - 1]);
   const size_t G = gridDim.x;
   const size_t lo = chunk * G * (size_t)kT * kPhaseTile;
   // Never taken (the host launches whole chunks only), but keep it: with this
@@ -352,9 +367,10 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
   // without it, short of registers, it regrouped the register tiles' adds
   // into load -> vmcnt(0) -> add chains (117-224 full drains per chunk, 8.3
   // instead of 6.5 ms at 8 buckets; profiles/r01b/sweep_ab.txt).
+  // tests/test_kernel_schedule.py checks the schedule on the assembly.
   if (lo >= n4_tiles) return;
 #pragma unroll
-  for (int k = 0; k <= NB; ++k) {
+  for (int k = 0; k < S; ++k) {
 #pragma unroll
     for (int t0 = 0; t0 < kT; t0 += TG) {
       f4 v[TG][U];
@@ -370,12 +386,13 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           // each lane owns its slots: no barrier between passes; bucket order 0..NB-1
+          const f4 first = ZIN ? f4(0.0f) + v[j][u] : v[j][u];
           if (t < kPhaseLdsTiles) {
             f4 &r = res[t * kPhaseTile + u * kBlock + threadIdx.x];
-            r = k == 0 ? v[j][u] : r + v[j][u];
+            r = k == 0 ? first : r + v[j][u];
           } else {
             f4 &r = keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u];
-            r = k == 0 ? v[j][u] : r + v[j][u];
+            r = k == 0 ? first : r + v[j][u];
           }
         }
       }
@@ -394,12 +411,12 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
   }
 }
 
-// Whole sweep chunks in a shard of n4_tiles f4: used when NB >= 3 and there
-// are at least kPhaseMinChunks of them, else 0.
-template <int NB>
+// Whole sweep chunks in a shard of n4_tiles f4, when there are at least
+// kPhaseMinChunks of them; else 0 (the tile-major plan takes the shard).
+template <int NB, bool ZIN = false>
 size_t sweep_chunks(size_t n4_tiles) {
-  if (NB < kSweepMinBuckets) return 0;
-  const size_t chunk_f4 = (size_t)num_cus() * kSweepT * kPhaseTile;
+  constexpr int kT = kPhaseLdsTiles + SweepShape<NB, ZIN>::RT;
+  const size_t chunk_f4 = (size_t)num_cus() * kT * kPhaseTile;
   const size_t c = n4_tiles / chunk_f4;
   return c >= (size_t)kPhaseMinChunks ? c : 0;
 }
@@ -425,14 +442,14 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
   size_t done = 0;  // floats summed so far
   if (vec) {
-    // 3-8 buckets: whole sweep chunks first, one launch each
-    const size_t sweeps = ZIN ? 0 : sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
-    if constexpr (NB >= kSweepMinBuckets && !ZIN)
-      for (size_t c = 0; c < sweeps; ++c)
-        hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB>), dim3((unsigned)G), dim3(kBlock),
-                           0, s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
-                           n / 4, c);
-    done = sweeps * G * kSweepT * kPhaseTile * 4;
+    // whole sweep chunks first, one launch each
+    using SS = SweepShape<NB, ZIN>;
+    const size_t sweeps = sweep_chunks<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
+    for (size_t c = 0; c < sweeps; ++c)
+      hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN>), dim3((unsigned)G),
+                         dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out),
+                         reinterpret_cast<const f4 *>(in), b, n / 4, c);
+    done = sweeps * G * (kPhaseLdsTiles + SS::RT) * kPhaseTile * 4;
     // the rest (all of it below 3 sweep chunks): the tile-major phased form
     const size_t n4_tiles = (n - done) / 4 / kPhaseTile * kPhaseTile;
     const PhasePlan p = phase_plan<NB>(n4_tiles);
@@ -474,17 +491,41 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   return GP_OK;
 }
 
-// Launch plan of one pass of nb buckets over n 16-B-aligned floats (bench.py
-// prices the phased kernel per launch with it).
-template <int NB>
-void bucket_sum_plan_nb(size_t n, int *launches, int *reg_tiles, int *sweep_launches) {
-  const size_t sweeps = sweep_chunks<NB>(n / 4 / kPhaseTile * kPhaseTile);
-  const size_t done = sweeps * (size_t)num_cus() * kSweepT * kPhaseTile * 4;
+// Launch plan of one pass of NB buckets over n 16-B-aligned floats, as
+// launch_bucket_sum_nb issues it (bench.py prices the dominant kernel per
+// launch with it).
+struct SumLaunches {
+  size_t sweep = 0, phased = 0, other = 0;
+  int reg_tiles = -1;  // the dominant phased form's register tiles
+};
+
+template <int NB, bool ZIN = false>
+SumLaunches sum_launches(size_t n) {
+  constexpr int RT = SweepShape<NB, ZIN>::RT;
+  SumLaunches l;
+  l.sweep = sweep_chunks<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
+  size_t done = l.sweep * (size_t)num_cus() * (kPhaseLdsTiles + RT) * kPhaseTile * 4;
   const size_t n4_tiles = (n - done) / 4 / kPhaseTile * kPhaseTile;
   const PhasePlan p = phase_plan<NB>(n4_tiles);
-  *sweep_launches = (int)sweeps;
-  *reg_tiles = sweeps ? kSweepRT : p.rt;
-  *launches = (int)(sweeps + (p.rt >= 0 ? p.launches : 0));
+  if (p.rt >= 0) {
+    l.phased = p.launches;
+    done += n4_tiles * 4;
+  }
+  l.reg_tiles = l.sweep ? RT : p.rt;
+  if (n - done >= 4) {
+    l.other++;
+    done += (n - done) / 4 * 4;
+  }
+  if (done < n) l.other++;
+  return l;
+}
+
+template <int NB>
+void bucket_sum_plan_nb(size_t n, int *launches, int *reg_tiles, int *sweep_launches) {
+  const SumLaunches l = sum_launches<NB>(n);
+  *sweep_launches = (int)l.sweep;
+  *reg_tiles = l.reg_tiles;
+  *launches = (int)(l.sweep + l.phased);
 }
 
 int launch_bucket_sum(float *out, const float *in, const float *const *bk,
@@ -1248,6 +1289,24 @@ int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *dense_runs, siz
   *num_rows = plan->num_rows;
   *dense_runs = plan->dense.size();
   *dense_rows = plan->dense_rows;
+  return GP_OK;
+}
+
+int gp_row_plan_launches(gp_row_plan plan, int init, int *sweep_launches, int *phased_launches,
+                         int *other_launches) {
+  if (!plan || !sweep_launches || !phased_launches || !other_launches)
+    return set_error(GP_ERR_INVALID, "null pointer");
+  size_t sw = 0, ph = 0, ot = plan->residual_rows ? 1 : 0;
+  for (const RowRun &r : plan->dense) {
+    const size_t n = r.rows * plan->row_size;
+    const SumLaunches l = init ? sum_launches<1, true>(n) : sum_launches<1>(n);
+    sw += l.sweep;
+    ph += l.phased;
+    ot += l.other;
+  }
+  *sweep_launches = (int)sw;
+  *phased_launches = (int)ph;
+  *other_launches = (int)ot;
   return GP_OK;
 }
 

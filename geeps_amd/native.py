@@ -59,6 +59,7 @@ _SIGNATURES = {
     "gp_row_plan_create": (_i, [_c.POINTER(_vp), _vp, _sz, DoubleIndex, _sz, _sz]),
     "gp_row_plan_destroy": (_i, [_vp]),
     "gp_row_plan_info": (_i, [_vp, _c.POINTER(_sz), _c.POINTER(_sz), _c.POINTER(_sz)]),
+    "gp_row_plan_launches": (_i, [_vp, _i, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
     "gp_scatter_add_rows_planned": (_i, [_vp, _vp, _vp, _vp]),
     "gp_scatter_init_rows_planned": (_i, [_vp, _vp, _vp, _vp]),
     "gp_gather_rows_segmented": (_i, [_vp, _c.POINTER(RowSegments), _vp, _sz, DoubleIndex, _sz,

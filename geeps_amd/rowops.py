@@ -217,6 +217,16 @@ class RowPlan:
         return {"rows": a.value, "dense_runs": b.value, "dense_rows": c.value,
                 "residual_rows": a.value - c.value}
 
+    def launches(self, init: bool = False) -> dict:
+        """Launch plan of one planned add (or fused init) over 16-B-aligned
+        buffers: sweep / tile-major phased sum launches over the dense runs,
+        and the rest (mixed / scalar sum forms, the residual's row kernel)."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(native.lib().gp_row_plan_launches(self._h, int(bool(init)), ctypes.byref(a),
+                                                ctypes.byref(b), ctypes.byref(c)),
+              "gp_row_plan_launches")
+        return {"sweep": a.value, "phased": b.value, "other": c.value}
+
     def _run(self, fn, y, x, stream, what):
         _dev_f32(y, "rows_y")
         _dev_f32(x, "rows_x")

@@ -123,7 +123,8 @@ int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
  * src/client/clientlib-viter.cpp:817-883).  The plan visits the rows in
  * destination (id1) order -- bit-neutral, since destinations are distinct.
  * Runs in which id0 and id1 both step by one (whole rows, at least 4 MiB) are
- * moved as dense ranges by the phase-separated sum kernels; the other rows
+ * moved as dense ranges by the phase-separated sum kernels (the init by their
+ * zero-input form); the other rows
  * keep a device index, sorted by id1, for the row kernels, so the scatter's
  * read-modify-write side walks y front to back.  Results are bit-identical to
  * gp_scatter_add_rows / gp_scatter_init_rows over the same index, offset and
@@ -141,6 +142,14 @@ int gp_row_plan_destroy(gp_row_plan plan);
 /* The plan's rows, its dense runs and the rows in them (the rest go to the
  * row kernels). */
 int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *dense_runs, size_t *dense_rows);
+/* Launch plan of one planned add (init = 0) or fused init (init = 1) over
+ * 16-B-aligned buffers; launches nothing.  *sweep_launches = launches of the
+ * stream-by-stream sum kernel over the dense runs (1 bucket; the init's
+ * zero-input form), *phased_launches = tile-major phase-separated launches,
+ * *other_launches = everything else (mixed / scalar sum forms, and one row
+ * kernel launch for the residual rows).  For measurement tools (bench.py). */
+int gp_row_plan_launches(gp_row_plan plan, int init, int *sweep_launches, int *phased_launches,
+                         int *other_launches);
 /* gp_scatter_add_rows(y, x, index, ...) through the plan (a3:
  * add_rows_from_double_index_gpu, src/common/row-op-util.cu:109-142). */
 int gp_scatter_add_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s);
@@ -221,16 +230,17 @@ int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
  * tile-major together (0 when the shard is too small for them and the mixed
  * form sums it in one launch);
  * *reg_tiles = 16-KiB tiles per block held in registers beside the 10 in LDS
- * by the dominant form (sweep: 6; tile-major: 20 at 1-2 buckets, 12 at 3-4,
- * 4 at 5-8; -1: not phased).  For measurement tools: bench.py prices the
+ * by the dominant form (sweep: 6 at 3-8 buckets, 14 at 1-2; tile-major: 20
+ * at 1-2 buckets, 12 at 3-4, 4 at 5-8; -1: not phased).  For measurement tools: bench.py prices the
  * dominant kernel per launch with it, as rocprofv3 reports it.
  * Returns GP_ERR_INVALID for num_buckets outside 1..8. */
 int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
                        int *reg_tiles);
 
 /* The same plan, plus *sweep_launches = how many of the phased launches are
- * the stream-by-stream sweep kernel (64-MiB chunks on 256 CUs; 3-8 buckets,
- * shards of at least 3 chunks; the tile-major form takes the rest). */
+ * the stream-by-stream sweep kernel (shards of at least 3 whole chunks: 64-MiB
+ * chunks on 256 CUs at 3-8 buckets, 96-MiB at 1-2; the tile-major form takes
+ * the rest).  *reg_tiles is then the sweep's: 6 at 3-8 buckets, 14 at 1-2. */
 int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launches,
                              int *reg_tiles, int *sweep_launches);
 

@@ -116,8 +116,9 @@ def test_product_does_not_import_oracle():
 def test_bucket_sum_plan_without_device():
     """gp_bucket_sum_plan launches nothing.  Without a device the library
     assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 64 MiB
-    for the sweep form (3-8 buckets, 6 register tiles beside 10 LDS tiles per
-    block, shards of at least 3 such chunks); tile-major 56 / 88 / 120 MiB
+    for the sweep form at 3-8 buckets (6 register tiles beside 10 LDS tiles
+    per block), 96 MiB at 1-2 (14 register tiles), on shards of at least 3
+    such chunks; tile-major 56 / 88 / 120 MiB
     with 4 / 12 / 20 register tiles for the rest; balanced chunks from 4 MiB
     (one 16-KiB tile per block) up."""
     L = native.lib()
@@ -136,7 +137,10 @@ def test_bucket_sum_plan_without_device():
 
     assert sweep_plan(1 << 30, 8) == (64, 6, 64)  # the 4 GiB headline shard: 64 sweep chunks
     assert plan(1 << 30, 8) == (64, 6)
-    assert sweep_plan(1 << 30, 2) == (35, 20, 0)  # 1-2 buckets: tile-major only
+    # 1-2 buckets: 96-MiB sweep chunks (14 register tiles), the 64-MiB rest tile-major
+    assert sweep_plan(1 << 30, 2) == (43, 14, 42)
+    assert sweep_plan(1 << 30, 1) == (43, 14, 42)
+    assert sweep_plan(288 << 18, 2) == (3, 14, 3)
     assert sweep_plan(1 << 30, 4) == (64, 6, 64)
     assert sweep_plan(1 << 27, 8) == (8, 6, 8)    # the 8-GPU shard (512 MiB)
     assert sweep_plan(1 << 28, 3) == (16, 6, 16)  # the 4-GPU shard (1 GiB)
@@ -170,6 +174,36 @@ def _info(h):
     a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
     assert native.lib().gp_row_plan_info(h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == 0
     return a.value, b.value, c.value
+
+
+def test_row_plan_launches_without_device():
+    """gp_row_plan_launches reports what a planned add / init issues (no
+    device: an index that is one dense run allocates nothing).  The 4 GiB
+    identity plan (1M rows of 1024 floats): the add as 42 sweep chunks of 96
+    MiB + the 64-MiB rest tile-major, the init as 64 zero-input sweep chunks of
+    64 MiB."""
+    import numpy as np
+    n = 1 << 20
+    rc, h = _plan(np.stack([np.arange(n), np.arange(n)], 1), row_size=1024)
+    assert rc == 0
+    a, b, c = ctypes.c_int(-1), ctypes.c_int(-1), ctypes.c_int(-1)
+
+    def launches(plan, init):
+        assert native.lib().gp_row_plan_launches(plan, init, ctypes.byref(a), ctypes.byref(b),
+                                                 ctypes.byref(c)) == 0
+        return a.value, b.value, c.value
+
+    assert launches(h, 0) == (42, 1, 0)
+    assert launches(h, 1) == (64, 0, 0)
+    assert native.lib().gp_row_plan_destroy(h) == 0
+    # a 4.9-MiB run: one balanced tile-major chunk (312 whole tiles on 256
+    # CUs), then the half tile left in one mixed-form launch
+    rc, h = _plan(np.stack([np.arange(10000), 7 + np.arange(10000)], 1), row_size=128)
+    assert rc == 0 and _info(h) == (10000, 1, 10000)
+    assert launches(h, 0) == (0, 1, 1) and launches(h, 1) == (0, 1, 1)
+    assert native.lib().gp_row_plan_destroy(h) == 0
+    assert native.lib().gp_row_plan_launches(None, 0, ctypes.byref(a), ctypes.byref(b),
+                                             ctypes.byref(c)) == 1
 
 
 def test_row_plan_classifies_dense_runs_without_device():

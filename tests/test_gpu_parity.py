@@ -180,22 +180,21 @@ def large_deltas():
 @pytest.mark.parametrize("N,out_of_place", [(1, False), (2, True), (3, False), (4, False),
                                             (5, True), (6, True), (8, False), (8, True)])
 def test_bucket_sum_register_tiles_path(dev, large_deltas, N, out_of_place):
-    """400-MiB shards: at 1-2 buckets the register-extended tile-major form
-    (20 register tiles beside the 10 LDS ones, 120-MiB chunks, the last one
-    partial); at 3-8 buckets 6 whole 64-MiB sweep chunks, then the 16-MiB rest
-    in one balanced tile-major chunk; then one dwordx4 for the mixed form and a
-    3-float scalar tail: every element checked bit for bit, and the plan the
-    library reports is that form."""
+    """400-MiB shards: at 1-2 buckets 4 whole 96-MiB sweep chunks (14 register
+    tiles beside the 10 LDS ones); at 3-8 buckets 6 whole 64-MiB sweep chunks;
+    then the 16-MiB rest in one balanced tile-major chunk, one dwordx4 for the
+    mixed form and a 3-float scalar tail: every element checked bit for bit,
+    and the plan the library reports is that form."""
     import ctypes
     from geeps_amd import native, rowops
     n, allups = large_deltas
     launches, rt = ctypes.c_int(0), ctypes.c_int(0)
     native.check(native.lib().gp_bucket_sum_plan(n, N, ctypes.byref(launches), ctypes.byref(rt)))
-    assert rt.value == (20 if N <= 2 else 6) and launches.value >= 3
+    assert rt.value == (14 if N <= 2 else 6) and launches.value >= 3
     sw = ctypes.c_int(-1)
     native.check(native.lib().gp_bucket_sum_sweep_plan(n, N, ctypes.byref(launches),
                                                         ctypes.byref(rt), ctypes.byref(sw)))
-    assert (sw.value, launches.value) == ((0, 4) if N <= 2 else (6, 7))
+    assert (sw.value, launches.value) == ((4, 5) if N <= 2 else (6, 7))
     ups = allups[:N]
     m0 = np.random.default_rng(N).standard_normal(n).astype(np.float32)
     e = m0.copy()
@@ -362,17 +361,18 @@ def test_full_size_8way_bucket_sum(dev):
 @pytest.mark.slow
 def test_full_size_config1_two_clients(dev):
     """BASELINE configs[1]: 1M rows x 1024 fp32, one shard, 2 clients (16 GiB
-    resident with the reference copy).  The plan is 35 launches of the
-    register-tile phased kernel (120-MiB chunks, the last partial); every
-    element against a plain torch fp32 reference adding the 2 buckets in client
-    order, and sampled rows against the C oracle."""
+    resident with the reference copy).  The plan is 42 launches of the sweep
+    kernel (96-MiB chunks) and one balanced tile-major launch for the 64-MiB
+    rest; every element against a plain torch fp32 reference adding the 2
+    buckets in client order, and sampled rows against the C oracle."""
     import ctypes
     from geeps_amd import native, rowops
     R, W, N = 1 << 20, 1024, 2
     n = R * W
-    launches, rt = ctypes.c_int(0), ctypes.c_int(0)
-    native.check(native.lib().gp_bucket_sum_plan(n, N, ctypes.byref(launches), ctypes.byref(rt)))
-    assert (launches.value, rt.value) == (35, 20)
+    launches, rt, sw = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    native.check(native.lib().gp_bucket_sum_sweep_plan(n, N, ctypes.byref(launches),
+                                                        ctypes.byref(rt), ctypes.byref(sw)))
+    assert (sw.value, launches.value, rt.value) == (42, 43, 14)
     g = torch.Generator(device=dev)
     buckets = []
     for c in range(N):
@@ -608,6 +608,55 @@ def test_row_plan_matches_oracle(dev, kind, W, limit_frac, off):
     plan.init(ty, T(x, dev))
     torch.cuda.synchronize()
     assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", kind, W)
+    plan.close()
+
+
+def test_row_plan_long_run_takes_sweep_forms(dev):
+    """A 620,000-row dense run (303 MiB at 128 floats) moves through the sweep
+    kernels: the add as 3 whole 96-MiB chunks (1 bucket) and the fused init as
+    4 whole 64-MiB chunks of the zero-input form, each rest through the
+    tile-major form; the run starts at x row 3 / y row 11, -0.0 deltas become
+    +0.0 under init, and the last 100 rows (past num_vals_limit, one
+    straddling it) plus 500 scattered rows take the residual path.  Bit for bit
+    against the oracle (init: listed rows zeroed, then the add)."""
+    import ctypes
+    from geeps_amd import native, rowops
+    rng = np.random.default_rng(620)
+    W, run, scattered = 128, 620_000, 500
+    n_op = run + scattered
+    n_cache = n_op + 64
+    dense = np.stack([3 + np.arange(run), 11 + np.arange(run)], 1)
+    free = np.setdiff1d(np.arange(n_cache), dense[:, 1])
+    extra = np.stack([np.setdiff1d(np.arange(n_op + 3), dense[:, 0])[:scattered],
+                      rng.choice(free, scattered, replace=False)], 1)
+    idx = np.concatenate([dense, extra])[rng.permutation(n_op)].astype(np.int64)
+    limit = (3 + run - 100) * W + 37
+    for nb, expect in ((1, 3),):
+        launches, rt, sw = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        native.check(native.lib().gp_bucket_sum_sweep_plan((run - 100) * W, nb, ctypes.byref(launches),
+                                                            ctypes.byref(rt), ctypes.byref(sw)))
+        assert sw.value == expect and rt.value == 14
+    x = rng.standard_normal((n_op + 3) * W).astype(np.float32)
+    x[rng.choice(x.size, 5000, replace=False)] = np.float32(-0.0)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    plan = rowops.RowPlan(idx, n_op, (0, 0), W, limit)
+    info = plan.info()
+    assert info["dense_runs"] == 1 and info["dense_rows"] == run - 100
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, (0, 0), W, limit)
+    ty = T(y, dev)
+    plan.add(ty, T(x, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), "add"
+    e = y.copy()
+    listed = np.zeros(n_cache, bool)
+    listed[idx[:, 1]] = True
+    e.reshape(n_cache, W)[listed] = 0.0
+    oracle.add_rows_from_double_index(e, x, idx, (0, 0), W, limit)
+    ty = T(y, dev)
+    plan.init(ty, T(x, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), "init"
     plan.close()
 
 

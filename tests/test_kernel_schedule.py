@@ -35,14 +35,21 @@ def _kernel(asm, pattern):
     return body
 
 
-@pytest.mark.parametrize("nb", [3, 4, 5, 6, 7, 8])
-def test_sweep_kernel_keeps_burst_schedule(asm, nb):
-    body = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi{nb}ELi6ELi4EE")
+# (buckets, register tiles, tiles per burst, zero-input): every production
+# instantiation (gp_reduce.hip SweepShape)
+SWEEP_SHAPES = [(nb, 6, 4, 0) for nb in range(3, 9)] + [(1, 14, 8, 0), (2, 14, 8, 0), (1, 6, 4, 1)]
+
+
+@pytest.mark.parametrize("nb,rt,tg,zin", SWEEP_SHAPES)
+def test_sweep_kernel_keeps_burst_schedule(asm, nb, rt, tg, zin):
+    body = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi{nb}ELi{rt}ELi{tg}ELb{zin}EE")
     loads = len(re.findall(r"global_load_dwordx4", body))
     full_drains = len(re.findall(r"s_waitcnt vmcnt\(0\)", body))
-    # (nb + 1) streams x 16 tiles x 4 block-strides, all dwordx4
-    assert loads == (nb + 1) * 16 * 4
-    assert full_drains <= 4, f"{full_drains} full vmcnt(0) drains: the burst schedule regressed"
+    streams = nb if zin else nb + 1
+    # streams x (10 LDS + rt register) tiles x 4 block-strides, all dwordx4
+    assert loads == streams * (10 + rt) * 4
+    # production: 0-6 full drains per chunk (the regressed schedule had 117-224)
+    assert full_drains <= 8, f"{full_drains} full vmcnt(0) drains: the burst schedule regressed"
     assert "scratch_" not in body and "buffer_store_dword" not in body  # no spills
 
 
