@@ -12,9 +12,10 @@ hosted on rank c % N; its delta buffer is uniform in [-0.5, 0.5) (seed 1000+c).
 A *step* is one device-resident N-way reduction: each shard adds the 8 client
 buckets for its rows into its master copy in client order 0..7 with one
 gp_bucket_sum_apply call (the reference's TabletStorage::apply_updates x 8,
-src/server/tablet-server.cpp:119-134); for a 4 GiB shard that call issues 64
-launches of the phase-separated sweep kernel, each summing a 64-MiB chunk of
-the shard (gp_bucket_sum_sweep_plan gives the count).  At N > 1 the buckets were first moved
+src/server/tablet-server.cpp:119-134); for a 4 GiB shard that call issues 42
+launches of the phase-separated sweep kernel, each summing a 96-MiB chunk of
+the shard, and one for the last 64 MiB (gp_bucket_sum_launch_plan gives every
+launch by form).  At N > 1 the buckets were first moved
 to their shard by RCCL all-to-all (untimed here; the exchange-inclusive step
 exchange + apply + all-gather refresh is timed separately and reported as
 `exchange_inclusive`).  Total work is fixed as N grows: scaling "strong".
@@ -56,27 +57,36 @@ METRIC = "GB/s gradient rows reduced (device-resident N-way fp32 sum); % HBM roo
 def sum_launch_plan(num_vals: int, num_buckets: int) -> dict:
     """The dominant kernel of one N-way sum of num_vals floats and how many
     launches of it one sum issues, from the library's own launch plan
-    (gp_bucket_sum_sweep_plan): shards of at least 3 whole sweep chunks go to
-    bucket_sum_sweep_kernel (64-MiB chunks at 3-8 buckets: the 4 GiB headline
-    shard and its 1/2, 1/4, 1/8 slices are whole chunks; 96-MiB chunks at 1-2
-    buckets), any rest to bucket_sum_phased_kernel (`other_launches`); smaller
-    shards of >= 4 MiB to the phased kernel alone; smaller ones
-    bucket_sum_vec_kernel in one launch.  `launches` counts the dominant kernel
-    only, so a per-launch time or byte figure divides by the launches rocprofv3
-    averages over."""
+    (gp_bucket_sum_launch_plan).  Shards of at least 3 whole 96-MiB chunks go
+    to bucket_sum_sweep_kernel<NB, 14, 8> (the 4 GiB headline shard: 42 of
+    them), then whole 64-MiB chunks to bucket_sum_sweep_kernel<NB, 6, 4> (the
+    4 GiB shard: 1), the rest to the tile-major bucket_sum_phased_kernel and
+    the mixed / scalar forms; smaller shards start at the 64-MiB sweep or the
+    phased kernel.  `launches` counts the dominant kernel only and `share` is
+    its part of the shard, so a per-launch time or byte figure (call time x
+    share / launches) compares with rocprofv3's average for that kernel;
+    `kernel_id` names the instantiation (as rocprofv3 prints it, up to the
+    burst depth)."""
     import ctypes
     from geeps_amd import native
-    launches, reg_tiles, sweeps = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
-    native.check(native.lib().gp_bucket_sum_sweep_plan(
-        num_vals, num_buckets, ctypes.byref(launches), ctypes.byref(reg_tiles),
-        ctypes.byref(sweeps)), "gp_bucket_sum_sweep_plan")
-    if sweeps.value > 0:
-        return {"kernel": "bucket_sum_sweep_kernel", "launches": sweeps.value,
-                "other_launches": launches.value - sweeps.value, "reg_tiles": reg_tiles.value}
-    if launches.value > 0:
-        return {"kernel": "bucket_sum_phased_kernel", "launches": launches.value,
-                "other_launches": 0, "reg_tiles": reg_tiles.value}
-    return {"kernel": "bucket_sum_vec_kernel", "launches": 1, "other_launches": 0, "reg_tiles": None}
+    p = native.SumPlan()
+    native.check(native.lib().gp_bucket_sum_launch_plan(num_vals, num_buckets, ctypes.byref(p)),
+                 "gp_bucket_sum_launch_plan")
+    cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
+    tile_floats = cus * 16384 // 4  # one 16-KiB tile per CU
+    forms = [("bucket_sum_sweep_kernel", p.sweep_launches, p.sweep_reg_tiles),
+             ("bucket_sum_sweep_kernel", p.small_sweep_launches, 6),
+             ("bucket_sum_phased_kernel", p.phased_launches, p.phased_reg_tiles)]
+    total = p.sweep_launches + p.small_sweep_launches + p.phased_launches + p.other_launches
+    for kernel, n, rt in forms:
+        if n > 0:
+            share = 1.0
+            if kernel == "bucket_sum_sweep_kernel":
+                share = min(1.0, n * (10 + rt) * tile_floats / num_vals)
+            return {"kernel": kernel, "kernel_id": f"{kernel}<{num_buckets}, {rt},", "launches": n,
+                    "other_launches": total - n, "reg_tiles": rt, "share": share}
+    return {"kernel": "bucket_sum_vec_kernel", "kernel_id": f"bucket_sum_vec_kernel<{num_buckets},",
+            "launches": 1, "other_launches": total - 1, "reg_tiles": None, "share": 1.0}
 
 
 def log(*a):
@@ -413,7 +423,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             index_rows = info["residual_rows"] if planned else R
             nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * index_rows
             writes = R * 512
-            launches, other = 1, 0
+            launches, other, share, kernel_id = 1, 0, 1.0, None
             if name == "scatter_add":
                 fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                    validate=False)
@@ -429,27 +439,36 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             else:
                 init = name == "scatter_init_planned"
                 fn = (lambda: plan.init(y, x)) if init else (lambda: plan.add(y, x))
-                pl = plan.launches(init)
                 if info["dense_rows"] == R:  # one dense run: the 1-bucket sum (init: zero-input form)
-                    kernel = "bucket_sum_sweep_kernel" if pl["sweep"] else "bucket_sum_phased_kernel"
-                    launches = pl["sweep"] or pl["phased"]
-                    other = pl["sweep"] and pl["phased"]
+                    if init:  # one sweep shape (64-MiB chunks), then the tile-major rest
+                        pl = plan.launches(True)
+                        kernel = "bucket_sum_sweep_kernel" if pl["sweep"] else "bucket_sum_phased_kernel"
+                        kernel_id = "bucket_sum_sweep_kernel<1, 6, 4, true>" if pl["sweep"] else None
+                        launches = pl["sweep"] or pl["phased"]
+                        other = pl["phased"] + pl["other"] if pl["sweep"] else pl["other"]
+                        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                        share = min(1.0, pl["sweep"] * 16 * cus * 4096 / (R * 128)) if pl["sweep"] else 1.0
+                    else:
+                        sp = sum_launch_plan(R * 128, 1)
+                        kernel, kernel_id = sp["kernel"], sp["kernel_id"]
+                        launches, other, share = sp["launches"], sp["other_launches"], sp["share"]
                 else:
                     kernel = "row_wave_kernel"
             avg = _time_calls(fn, reps, stream)
             gbps = nbytes / (avg / 1e3) / 1e9
             leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),
                    "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes": nbytes, "kernel": kernel,
-                   "launches": launches, "avg_launch_ms": round(avg / launches, 5)}
-            if other:  # a rest in another kernel form: the per-launch figure includes it
+                   "launches": launches, "avg_launch_ms": round(avg * share / launches, 5)}
+            if other:  # the rest in other kernel forms; avg_launch_ms is the dominant one's share
                 leg["other_launches"] = other
+                leg["dominant_share"] = round(share, 6)
             mm = model_ms(nbytes - writes, writes, probe)
             if mm:
                 leg["model_ms"] = round(mm, 4)
                 leg["frac_of_model"] = round(mm / avg, 4)
             if planned:
                 leg["plan"] = info
-            traffic = load_traffic(f"rowops_{name}_{kind}_r{R}_w128", kernel)
+            traffic = load_traffic(f"rowops_{name}_{kind}_r{R}_w128", kernel_id or kernel)
             if traffic:
                 leg["traffic"] = traffic["bytes_per_launch"] * launches
                 leg["traffic_source"] = traffic
@@ -595,12 +614,7 @@ def config2_leg(deltas, master, dev, probe=None, reps=5):
     nbytes = 4 * n * 4
     gbps = nbytes / (avg / 1e3) / 1e9
     rows = n // 1024
-    # the dominant kernel's share of the shard (the rest: `other_launches` of
-    # the tile-major form), so the per-launch figure compares with rocprofv3's
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    chunk = {"bucket_sum_sweep_kernel": (10 + (plan["reg_tiles"] or 0)) * cus * 16384 // 4}.get(
-        plan["kernel"])  # floats per chunk: (10 LDS + register) 16-KiB tiles per CU
-    share = min(1.0, plan["launches"] * chunk / n) if chunk else 1.0
+    share = plan["share"]  # the dominant kernel's part of the shard
     return {"workload": f"configs[1]: 2 clients, {rows} rows x 1024 fp32, 1 shard, device-resident",
             "ms": round(avg, 4), "GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4),
             "delta_GBps": round(2 * n * 4 / (avg / 1e3) / 1e9, 1), "bytes": nbytes,
@@ -608,7 +622,7 @@ def config2_leg(deltas, master, dev, probe=None, reps=5):
             "other_launches": plan["other_launches"],
             "avg_launch_ms": round(avg * share / plan["launches"], 5),
             "avg_launch_note": "call time x the dominant kernel's share of the shard / its launches",
-            "traffic_source": load_traffic(f"r{rows}_w1024_c2_g1", plan["kernel"]),
+            "traffic_source": load_traffic(f"r{rows}_w1024_c2_g1", plan["kernel_id"]),
             "model_ms": (round(model_ms(3 * n * 4, n * 4, probe), 4) if probe else None)}
 
 
@@ -709,7 +723,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
             cpu = cpu_baseline(min(args.cpu_rows, R), W, C, args.cpu_seconds)
 
     if rank == 0:
-        traffic = load_traffic(workload_key, kernel_name)
+        traffic = load_traffic(workload_key, plan["kernel_id"])
+        share = plan["share"]
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -738,15 +753,19 @@ def main(argv=None, backend="nccl", apply_fn=None):
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic,
                          "kernel": kernel_name,
+                         "kernel_id": plan["kernel_id"],
                          "launches_per_step": launches,
                          "other_launches_per_step": plan["other_launches"],
                          "register_tiles": plan["reg_tiles"],
                          # HIP events around each step's launches on their stream
                          "avg_kernel_ms": round(avg_kernel_ms_max, 4),
-                         # per launch, comparable with rocprofv3's average for the kernel
-                         "avg_launch_ms": round(avg_kernel_ms_max / launches, 5),
+                         # per launch of the dominant kernel (its share of the step:
+                         # the other launches move the rest of the shard), comparable
+                         # with rocprofv3's average for that kernel
+                         "avg_launch_ms": round(avg_kernel_ms_max * share / launches, 5),
+                         "dominant_share": round(share, 6),
                          "algorithmic_bytes_per_step": algo_bytes,
-                         "algorithmic_bytes_per_launch": algo_bytes // launches},
+                         "algorithmic_bytes_per_launch": int(algo_bytes * share / launches)},
             "hbm_GBps_algorithmic": round((C + 2) * R * W * 4 / step_s / 1e9, 1),
             "cpu_baseline": cpu,
         }

@@ -333,14 +333,22 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
 // in flight: zero-input 75.4-78.5 % of 8 TB/s against 72.0-72.1 % (64-MiB
 // chunks, TG 4); 2 buckets 80.2-80.8 % against 78.6-78.8 % and 1 bucket
 // 79.7-80.0 % against 78.8-79.4 % (96-MiB chunks: 14 register tiles, TG 8).
-// Whole chunks only (no guards: the waitcnt counts stay exact); the caller
-// hands the rest of the shard to the tile-major plan.
+// The same 96-MiB shape then measured faster at 3-8 buckets too (scripts/
+// tune/hib_tune.hip, profiles/r02/tune/hib_tune.txt, 3 arenas): per byte
+// +0.8-2.7 % at 8 buckets, +1.4-2.7 % at 4, +2.3-3.5 % at 3 against 64-MiB
+// chunks with bursts of 4.  96 MiB does not divide the 4 GiB shard, so a
+// plan takes whole 96-MiB chunks first ("big"), then whole 64-MiB chunks of
+// the 6-register-tile shape ("small": the 4 GiB shard is 42 + 1), and hands
+// the rest to the tile-major plan (at 1-2 buckets the 64-MiB sweep ran 75-80 %
+// against the tile-major form's 78.6-79.4 %, so there the rest goes straight
+// to tile-major).  Whole chunks only (no guards: the waitcnt counts stay
+// exact).  The zero-input form has one shape, 64-MiB chunks.
 template <int NB, bool ZIN>
-struct SweepShape {  // register tiles, tiles per burst of loads
-  static constexpr int RT = (NB <= 2 && !ZIN) ? 14 : 6;
-  static constexpr int TG = (NB <= 2 && !ZIN) ? 8 : 4;
+struct SweepShape {  // register tiles, tiles per burst of loads: the big chunks
+  static constexpr int RT = ZIN ? 6 : 14;
+  static constexpr int TG = ZIN ? 4 : 8;
 };
-constexpr int kSweepRT = 6;  // 3-8 buckets and the zero-input form
+constexpr int kSweepRT = 6;  // the small (64-MiB) chunks and the zero-input form
 constexpr int kSweepTG = 4;
 [[maybe_unused]] constexpr int kSweepT = kPhaseLdsTiles + kSweepRT;  // tuning harnesses
 
@@ -411,14 +419,30 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
   }
 }
 
-// Whole sweep chunks in a shard of n4_tiles f4, when there are at least
-// kPhaseMinChunks of them; else 0 (the tile-major plan takes the shard).
+// Whole sweep chunks of a shard of n4_tiles f4: `big` chunks of the
+// SweepShape (when there are at least kPhaseMinChunks of them), then, at 3-8
+// buckets, `small` 64-MiB chunks of what is left (any number after big
+// chunks, else at least kPhaseMinChunks); the tile-major plan takes the rest.
+struct SweepSplit {
+  size_t big = 0, small = 0;
+  size_t big_f4 = 0, small_f4 = 0;  // f4 per chunk
+  size_t done_f4() const { return big * big_f4 + small * small_f4; }
+};
+
 template <int NB, bool ZIN = false>
-size_t sweep_chunks(size_t n4_tiles) {
-  constexpr int kT = kPhaseLdsTiles + SweepShape<NB, ZIN>::RT;
-  const size_t chunk_f4 = (size_t)num_cus() * kT * kPhaseTile;
-  const size_t c = n4_tiles / chunk_f4;
-  return c >= (size_t)kPhaseMinChunks ? c : 0;
+SweepSplit sweep_split(size_t n4_tiles) {
+  constexpr int RT = SweepShape<NB, ZIN>::RT;
+  const size_t G = (size_t)num_cus();
+  SweepSplit sp;
+  sp.big_f4 = G * (size_t)(kPhaseLdsTiles + RT) * kPhaseTile;
+  sp.small_f4 = G * (size_t)(kPhaseLdsTiles + kSweepRT) * kPhaseTile;
+  sp.big = n4_tiles / sp.big_f4;
+  if (sp.big < (size_t)kPhaseMinChunks) sp.big = 0;
+  if (RT != kSweepRT && NB >= 3) {  // at 1-2 buckets the 64-MiB sweep lost to tile-major
+    sp.small = (n4_tiles - sp.big * sp.big_f4) / sp.small_f4;
+    if (sp.big == 0 && sp.small < (size_t)kPhaseMinChunks) sp.small = 0;
+  }
+  return sp;
 }
 
 // Buckets advanced by `off` floats.
@@ -442,14 +466,23 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
   size_t done = 0;  // floats summed so far
   if (vec) {
-    // whole sweep chunks first, one launch each
+    // whole sweep chunks first, one launch each: big, then small
     using SS = SweepShape<NB, ZIN>;
-    const size_t sweeps = sweep_chunks<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
-    for (size_t c = 0; c < sweeps; ++c)
+    const SweepSplit sp = sweep_split<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
+    for (size_t c = 0; c < sp.big; ++c)
       hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN>), dim3((unsigned)G),
                          dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out),
                          reinterpret_cast<const f4 *>(in), b, n / 4, c);
-    done = sweeps * G * (kPhaseLdsTiles + SS::RT) * kPhaseTile * 4;
+    done = sp.big * sp.big_f4 * 4;
+    if constexpr (SS::RT != kSweepRT) {
+      const BucketPtrs bo = offset_buckets<NB>(b, done);
+      for (size_t c = 0; c < sp.small; ++c)
+        hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN>), dim3((unsigned)G),
+                           dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out + done),
+                           reinterpret_cast<const f4 *>(ZIN ? nullptr : in + done), bo,
+                           (n - done) / 4, c);
+      done += sp.small * sp.small_f4 * 4;
+    }
     // the rest (all of it below 3 sweep chunks): the tile-major phased form
     const size_t n4_tiles = (n - done) / 4 / kPhaseTile * kPhaseTile;
     const PhasePlan p = phase_plan<NB>(n4_tiles);
@@ -495,23 +528,27 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
 // launch_bucket_sum_nb issues it (bench.py prices the dominant kernel per
 // launch with it).
 struct SumLaunches {
-  size_t sweep = 0, phased = 0, other = 0;
+  size_t sweep = 0, sweep_small = 0, phased = 0, other = 0;
   int reg_tiles = -1;  // the dominant phased form's register tiles
+  int phased_reg_tiles = -1;
 };
 
 template <int NB, bool ZIN = false>
 SumLaunches sum_launches(size_t n) {
   constexpr int RT = SweepShape<NB, ZIN>::RT;
   SumLaunches l;
-  l.sweep = sweep_chunks<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
-  size_t done = l.sweep * (size_t)num_cus() * (kPhaseLdsTiles + RT) * kPhaseTile * 4;
+  const SweepSplit sp = sweep_split<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
+  l.sweep = sp.big;
+  l.sweep_small = sp.small;
+  size_t done = sp.done_f4() * 4;
   const size_t n4_tiles = (n - done) / 4 / kPhaseTile * kPhaseTile;
   const PhasePlan p = phase_plan<NB>(n4_tiles);
   if (p.rt >= 0) {
     l.phased = p.launches;
+    l.phased_reg_tiles = p.rt;
     done += n4_tiles * 4;
   }
-  l.reg_tiles = l.sweep ? RT : p.rt;
+  l.reg_tiles = sp.big ? RT : sp.small ? kSweepRT : p.rt;
   if (n - done >= 4) {
     l.other++;
     done += (n - done) / 4 * 4;
@@ -523,9 +560,20 @@ SumLaunches sum_launches(size_t n) {
 template <int NB>
 void bucket_sum_plan_nb(size_t n, int *launches, int *reg_tiles, int *sweep_launches) {
   const SumLaunches l = sum_launches<NB>(n);
-  *sweep_launches = (int)l.sweep;
+  *sweep_launches = (int)(l.sweep + l.sweep_small);
   *reg_tiles = l.reg_tiles;
-  *launches = (int)(l.sweep + l.phased);
+  *launches = (int)(l.sweep + l.sweep_small + l.phased);
+}
+
+template <int NB>
+void sum_plan_nb(size_t n, gp_sum_plan *out) {
+  const SumLaunches l = sum_launches<NB>(n);
+  out->sweep_launches = (int)l.sweep;
+  out->sweep_reg_tiles = l.sweep ? SweepShape<NB, false>::RT : -1;
+  out->small_sweep_launches = (int)l.sweep_small;
+  out->phased_launches = (int)l.phased;
+  out->phased_reg_tiles = l.phased_reg_tiles;
+  out->other_launches = (int)l.other;
 }
 
 int launch_bucket_sum(float *out, const float *in, const float *const *bk,
@@ -1300,7 +1348,7 @@ int gp_row_plan_launches(gp_row_plan plan, int init, int *sweep_launches, int *p
   for (const RowRun &r : plan->dense) {
     const size_t n = r.rows * plan->row_size;
     const SumLaunches l = init ? sum_launches<1, true>(n) : sum_launches<1>(n);
-    sw += l.sweep;
+    sw += l.sweep + l.sweep_small;
     ph += l.phased;
     ot += l.other;
   }
@@ -1334,6 +1382,22 @@ int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launc
     case 6: bucket_sum_plan_nb<6>(num_vals, l, r, w); break;
     case 7: bucket_sum_plan_nb<7>(num_vals, l, r, w); break;
     case 8: bucket_sum_plan_nb<8>(num_vals, l, r, w); break;
+    default: return set_error(GP_ERR_INVALID, "bucket count out of range");
+  }
+  return GP_OK;
+}
+
+int gp_bucket_sum_launch_plan(size_t num_vals, int num_buckets, gp_sum_plan *plan) {
+  if (!plan) return set_error(GP_ERR_INVALID, "null pointer");
+  switch (num_buckets) {
+    case 1: sum_plan_nb<1>(num_vals, plan); break;
+    case 2: sum_plan_nb<2>(num_vals, plan); break;
+    case 3: sum_plan_nb<3>(num_vals, plan); break;
+    case 4: sum_plan_nb<4>(num_vals, plan); break;
+    case 5: sum_plan_nb<5>(num_vals, plan); break;
+    case 6: sum_plan_nb<6>(num_vals, plan); break;
+    case 7: sum_plan_nb<7>(num_vals, plan); break;
+    case 8: sum_plan_nb<8>(num_vals, plan); break;
     default: return set_error(GP_ERR_INVALID, "bucket count out of range");
   }
   return GP_OK;

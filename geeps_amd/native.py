@@ -44,6 +44,15 @@ class RowSegments(ctypes.Structure):
                 ("base", ctypes.c_void_p * GP_MAX_SEGMENTS)]
 
 
+class SumPlan(ctypes.Structure):
+    """``gp_sum_plan``: every launch of one bucket-sum pass, by kernel form."""
+
+    _fields_ = [("sweep_launches", ctypes.c_int), ("sweep_reg_tiles", ctypes.c_int),
+                ("small_sweep_launches", ctypes.c_int),
+                ("phased_launches", ctypes.c_int), ("phased_reg_tiles", ctypes.c_int),
+                ("other_launches", ctypes.c_int)]
+
+
 _c = ctypes
 _vp = _c.c_void_p
 _sz = _c.c_size_t
@@ -70,6 +79,7 @@ _SIGNATURES = {
     "gp_bucket_sum_into": (_i, [_vp, _vp, _c.POINTER(_vp), _i, _sz, _vp]),
     "gp_bucket_sum_plan": (_i, [_sz, _i, _c.POINTER(_i), _c.POINTER(_i)]),
     "gp_bucket_sum_sweep_plan": (_i, [_sz, _i, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
+    "gp_bucket_sum_launch_plan": (_i, [_sz, _i, _c.POINTER(SumPlan)]),
     "gp_add": (_i, [_sz, _vp, _vp, _vp, _vp]),
     "gp_zero": (_i, [_vp, _sz, _vp]),
     "gp_hbm_probe": (_i, [_i, _vp, _sz, _vp]),

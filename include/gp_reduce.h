@@ -230,19 +230,37 @@ int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
  * tile-major together (0 when the shard is too small for them and the mixed
  * form sums it in one launch);
  * *reg_tiles = 16-KiB tiles per block held in registers beside the 10 in LDS
- * by the dominant form (sweep: 6 at 3-8 buckets, 14 at 1-2; tile-major: 20
- * at 1-2 buckets, 12 at 3-4, 4 at 5-8; -1: not phased).  For measurement tools: bench.py prices the
+ * by the first phased form (sweep: 14 with 96-MiB chunks, 6 with 64-MiB;
+ * tile-major: 20 at 1-2 buckets, 12 at 3-4, 4 at 5-8; -1: not phased).  For measurement tools: bench.py prices the
  * dominant kernel per launch with it, as rocprofv3 reports it.
  * Returns GP_ERR_INVALID for num_buckets outside 1..8. */
 int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
                        int *reg_tiles);
 
 /* The same plan, plus *sweep_launches = how many of the phased launches are
- * the stream-by-stream sweep kernel (shards of at least 3 whole chunks: 64-MiB
- * chunks on 256 CUs at 3-8 buckets, 96-MiB at 1-2; the tile-major form takes
- * the rest).  *reg_tiles is then the sweep's: 6 at 3-8 buckets, 14 at 1-2. */
+ * the stream-by-stream sweep kernel, big and small chunks together
+ * (gp_bucket_sum_launch_plan splits them); *reg_tiles is then the first sweep
+ * form's: 14 (96-MiB chunks) or 6 (64-MiB chunks). */
 int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launches,
                              int *reg_tiles, int *sweep_launches);
+
+/* Every launch of one pass of num_buckets (1..8) over num_vals floats in
+ * 16-B-aligned buffers, by kernel form, in launch order; launches nothing:
+ *   sweep_launches       the stream-by-stream kernel's big chunks (96 MiB on
+ *                        256 CUs: 14 register tiles beside the 10 LDS ones),
+ *   small_sweep_launches then its 64-MiB chunks (6 register tiles),
+ *   phased_launches      then the tile-major phase-separated form
+ *                        (phased_reg_tiles: 20 at 1-2 buckets, 12 at 3-4, 4 at 5-8),
+ *   other_launches       then the mixed dwordx4 and scalar forms (0-2).
+ * A reg_tiles field is -1 when its form has no launch.  For measurement
+ * tools: bench.py prices each kernel per launch, as rocprofv3 reports it. */
+typedef struct gp_sum_plan {
+  int sweep_launches, sweep_reg_tiles;
+  int small_sweep_launches;
+  int phased_launches, phased_reg_tiles;
+  int other_launches;
+} gp_sum_plan;
+int gp_bucket_sum_launch_plan(size_t num_vals, int num_buckets, gp_sum_plan *plan);
 
 /* y[i] = a[i] + b[i] — device form of cpu_add / vsAdd
  * (src/common/gpu-util/math_functions.hpp:60-61, mkl_alternate.hpp:59-74).

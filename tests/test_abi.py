@@ -135,16 +135,19 @@ def test_bucket_sum_plan_without_device():
                                           ctypes.byref(sweeps)) == 0
         return launches.value, rt.value, sweeps.value
 
-    assert sweep_plan(1 << 30, 8) == (64, 6, 64)  # the 4 GiB headline shard: 64 sweep chunks
-    assert plan(1 << 30, 8) == (64, 6)
-    # 1-2 buckets: 96-MiB sweep chunks (14 register tiles), the 64-MiB rest tile-major
+    # the 4 GiB headline shard: 42 sweep chunks of 96 MiB, then one of 64 MiB
+    assert sweep_plan(1 << 30, 8) == (43, 14, 43)
+    assert plan(1 << 30, 8) == (43, 14)
+    # 1-2 buckets: the rest after the 96-MiB chunks goes to the tile-major form
     assert sweep_plan(1 << 30, 2) == (43, 14, 42)
     assert sweep_plan(1 << 30, 1) == (43, 14, 42)
+    assert sweep_plan(1 << 30, 4) == (43, 14, 43)
     assert sweep_plan(288 << 18, 2) == (3, 14, 3)
-    assert sweep_plan(1 << 30, 4) == (64, 6, 64)
-    assert sweep_plan(1 << 27, 8) == (8, 6, 8)    # the 8-GPU shard (512 MiB)
-    assert sweep_plan(1 << 28, 3) == (16, 6, 16)  # the 4-GPU shard (1 GiB)
-    # 200 MiB: 3 sweep chunks (192 MiB), then the 8-MiB rest in 1 balanced tile-major chunk
+    # the 8-GPU shard (512 MiB): 5 x 96 MiB, the 32-MiB rest in one balanced tile-major chunk
+    assert sweep_plan(1 << 27, 8) == (6, 14, 5)
+    assert sweep_plan(1 << 28, 3) == (11, 14, 11)  # the 4-GPU shard (1 GiB): 10 x 96 + 64 MiB
+    # 200 MiB: under 3 big chunks, so 3 64-MiB sweep chunks, then the 8-MiB
+    # rest in 1 balanced tile-major chunk
     assert sweep_plan(200 << 18, 8) == (4, 6, 3)
     assert sweep_plan(120 << 18, 8) == (3, 4, 0)  # under 3 sweep chunks: tile-major only
     # below 3 register-form chunks: <= 3 balanced chunks of the same form, one per launch
@@ -158,6 +161,17 @@ def test_bucket_sum_plan_without_device():
     assert L.gp_bucket_sum_plan(16, 9, ctypes.byref(launches), ctypes.byref(rt)) == 1
     assert L.gp_bucket_sum_plan(16, 0, ctypes.byref(launches), ctypes.byref(rt)) == 1
     assert L.gp_bucket_sum_plan(16, 1, None, None) == 1
+    # every launch by form
+    sp = native.SumPlan()
+    assert L.gp_bucket_sum_launch_plan(1 << 30, 8, ctypes.byref(sp)) == 0
+    assert (sp.sweep_launches, sp.sweep_reg_tiles, sp.small_sweep_launches, sp.phased_launches,
+            sp.phased_reg_tiles, sp.other_launches) == (42, 14, 1, 0, -1, 0)
+    n = (1 << 27) + 4 + 3  # 512 MiB + one dwordx4 + 3 floats
+    assert L.gp_bucket_sum_launch_plan(n, 5, ctypes.byref(sp)) == 0
+    assert (sp.sweep_launches, sp.small_sweep_launches, sp.phased_launches, sp.phased_reg_tiles,
+            sp.other_launches) == (5, 0, 1, 4, 2)
+    assert L.gp_bucket_sum_launch_plan(n, 9, ctypes.byref(sp)) == 1
+    assert L.gp_bucket_sum_launch_plan(n, 2, None) == 1
 
 
 def _plan(idx, offset=(0, 0), row_size=128, limit=None):

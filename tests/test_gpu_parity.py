@@ -180,21 +180,20 @@ def large_deltas():
 @pytest.mark.parametrize("N,out_of_place", [(1, False), (2, True), (3, False), (4, False),
                                             (5, True), (6, True), (8, False), (8, True)])
 def test_bucket_sum_register_tiles_path(dev, large_deltas, N, out_of_place):
-    """400-MiB shards: at 1-2 buckets 4 whole 96-MiB sweep chunks (14 register
-    tiles beside the 10 LDS ones); at 3-8 buckets 6 whole 64-MiB sweep chunks;
-    then the 16-MiB rest in one balanced tile-major chunk, one dwordx4 for the
-    mixed form and a 3-float scalar tail: every element checked bit for bit,
-    and the plan the library reports is that form."""
+    """400-MiB shards: 4 whole 96-MiB sweep chunks (14 register tiles beside
+    the 10 LDS ones), then the 16-MiB rest in one balanced tile-major chunk,
+    one dwordx4 for the mixed form and a 3-float scalar tail: every element
+    checked bit for bit, and the plan the library reports is that form."""
     import ctypes
     from geeps_amd import native, rowops
     n, allups = large_deltas
     launches, rt = ctypes.c_int(0), ctypes.c_int(0)
     native.check(native.lib().gp_bucket_sum_plan(n, N, ctypes.byref(launches), ctypes.byref(rt)))
-    assert rt.value == (14 if N <= 2 else 6) and launches.value >= 3
+    assert rt.value == 14 and launches.value >= 3
     sw = ctypes.c_int(-1)
     native.check(native.lib().gp_bucket_sum_sweep_plan(n, N, ctypes.byref(launches),
                                                         ctypes.byref(rt), ctypes.byref(sw)))
-    assert (sw.value, launches.value) == ((4, 5) if N <= 2 else (6, 7))
+    assert (sw.value, launches.value) == (4, 5)
     ups = allups[:N]
     m0 = np.random.default_rng(N).standard_normal(n).astype(np.float32)
     e = m0.copy()
@@ -362,9 +361,9 @@ def test_full_size_8way_bucket_sum(dev):
 def test_full_size_config1_two_clients(dev):
     """BASELINE configs[1]: 1M rows x 1024 fp32, one shard, 2 clients (16 GiB
     resident with the reference copy).  The plan is 42 launches of the sweep
-    kernel (96-MiB chunks) and one balanced tile-major launch for the 64-MiB
-    rest; every element against a plain torch fp32 reference adding the 2
-    buckets in client order, and sampled rows against the C oracle."""
+    kernel's 96-MiB chunks and one tile-major launch for the 64-MiB rest;
+    every element against a plain torch fp32 reference adding the 2 buckets in
+    client order, and sampled rows against the C oracle."""
     import ctypes
     from geeps_amd import native, rowops
     R, W, N = 1 << 20, 1024, 2
