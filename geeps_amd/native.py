@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 6  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 7  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
