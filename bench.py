@@ -368,7 +368,7 @@ def host_inclusive(rows, W, clients, dev, chunk_rows=16384, steps=2):
 
 
 ROWOP_LEGS = ("scatter_add", "scatter_add_planned", "scatter_init", "scatter_init_planned",
-              "gather")
+              "gather", "gather_planned")
 
 
 def _time_calls(fn, reps, stream):
@@ -395,6 +395,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
       scatter_init         gp_scatter_init_rows: fused zerofy + add (common-util.hpp:445-456 + a3)
       scatter_init_planned the same through the plan
       gather               gp_gather_rows (assign_rows_to_double_index_gpu, :39-72)
+      gather_planned       the same through a gather plan (what libgeeps' Read runs)
     Algorithmic bytes per call: add 3*R*512, init / gather 2*R*512, plus the
     16-B DoubleIndex entries the kernel reads (every row unplanned; a plan's
     residual rows planned -- its dense runs read no index)."""
@@ -413,14 +414,17 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             dst = torch.arange(R, device=dev)
         idx = torch.stack([torch.arange(R, device=dev), dst], 1).contiguous()
         plan = rowops.RowPlan(idx, R, (0, 0), 128, R * 128)
+        gplan = rowops.RowPlan(idx, R, (0, 0), 128, R * 128, kind="gather")
         info = plan.info()
+        ginfo = gplan.info()
         legs = {}
         for name in ROWOP_LEGS:
             if only and name not in only:
                 continue
             planned = name.endswith("_planned")
+            pinfo = ginfo if name.startswith("gather") else info
             # dense runs read no index; residual rows (and unplanned calls) do
-            index_rows = info["residual_rows"] if planned else R
+            index_rows = pinfo["residual_rows"] if planned else R
             nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * index_rows
             writes = R * 512
             launches, other, share, kernel_id = 1, 0, 1.0, None
@@ -436,6 +440,18 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                 fn = lambda: rowops.assign_rows_to_double_index_gpu(x, y, idx, R, (0, 0), 128, R * 128,
                                                                     validate=False)
                 kernel = "row_wave_kernel"
+            elif name == "gather_planned":
+                fn = lambda: gplan.gather(x, y)
+                if ginfo["dense_rows"] == R:  # one dense run: the no-bucket sweep copy
+                    pl = gplan.launches()
+                    kernel = "bucket_sum_sweep_kernel" if pl["sweep"] else "bucket_sum_phased_kernel"
+                    kernel_id = "bucket_sum_sweep_kernel<0, 6, 4, false>" if pl["sweep"] else None
+                    launches = pl["sweep"] or pl["phased"]
+                    other = pl["phased"] + pl["other"] if pl["sweep"] else pl["other"]
+                    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                    share = min(1.0, pl["sweep"] * 16 * cus * 4096 / (R * 128)) if pl["sweep"] else 1.0
+                else:
+                    kernel = "row_wave_kernel"
             else:
                 init = name == "scatter_init_planned"
                 fn = (lambda: plan.init(y, x)) if init else (lambda: plan.add(y, x))
@@ -467,7 +483,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                 leg["model_ms"] = round(mm, 4)
                 leg["frac_of_model"] = round(mm / avg, 4)
             if planned:
-                leg["plan"] = info
+                leg["plan"] = pinfo
             traffic = load_traffic(f"rowops_{name}_{kind}_r{R}_w128", kernel_id or kernel)
             if traffic:
                 leg["traffic"] = traffic["bytes_per_launch"] * launches
@@ -476,6 +492,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
         out[kind] = dict(rows=R, row_size=128, index=f"{kind} permutation of destinations"
                          if kind == "random" else "identity", **legs)
         plan.close()
+        gplan.close()
         del idx, dst
     return out
 

@@ -589,8 +589,9 @@ void ClientLib::finish_virtual_iteration() {
     op.buffer.resize(std::max<size_t>(1, op.rows.size()) * ROW_DATA_SIZE);
     GP_CALL(gp_zero(op.buffer.data(), op.buffer.size(), channels_[0]->stream->get()));
     planned += op.buffer.bytes();
-    // the device DoubleIndex, and an update op's row plans (a sorted copy)
-    planned += op.rows.size() * sizeof(gp_double_index) * (op.type == OpInfo::PRE_WRITE ? 2 : 1);
+    // the device DoubleIndex, and an update or read op's row plans (a sorted copy)
+    planned += op.rows.size() * sizeof(gp_double_index) *
+               (op.type == OpInfo::PRE_WRITE || op.type == OpInfo::READ ? 2 : 1);
     create_double_index(op);
   }
   GP_CALL(gp_device_synchronize());
@@ -681,12 +682,16 @@ void ClientLib::create_double_index(OpInfo &op) {
   // The update ops' oplog accumulate runs through a row plan per channel: the
   // same rows visited in cache-row order (bit-identical: id1 distinct, checked
   // above), so the scatter's read-modify-write side walks the oplog in order.
-  if (op.type == OpInfo::PRE_WRITE) {
+  // The read ops' gather runs through a gather plan per channel: its dense
+  // runs (first-access order makes an op's rows one run per channel) are
+  // copied by the phase-separated kernels, which hold their rate on every
+  // allocation.
+  if (op.type == OpInfo::PRE_WRITE || op.type == OpInfo::READ) {
     op.plans.resize(num_channels_);
     for (uint32_t c = 0; c < num_channels_; ++c)
       if (!per[c].empty())
         op.plans[c] = std::make_unique<RowPlan>(per[c].data(), per[c].size(), ROW_DATA_SIZE,
-                                                op.num_vals_limit);
+                                                op.num_vals_limit, op.type == OpInfo::READ);
   }
   op.index.resize(std::max<size_t>(1, flat.size()));
   if (!flat.empty())
@@ -740,16 +745,13 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
       }
     }
     waited += now_s() - w0;
+    // assign_rows_to_double_index_gpu (clientlib-data.cpp:254-278) through the
+    // op's gather plan for this channel (its index, offset 0, num_vals_limit)
+    float *const y = reinterpret_cast<float *>(op.buffer.data());
     if (op.ch_size[ch.id] && pc.segmented)
-      GP_CALL(gp_gather_rows_segmented(reinterpret_cast<float *>(op.buffer.data()), &pc.segs,
-                                       op.index.data() + op.ch_start[ch.id], op.ch_size[ch.id],
-                                       gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit,
-                                       ch.stream->get()));
+      GP_CALL(gp_gather_rows_segmented_planned(y, &pc.segs, op.plans[ch.id]->get(), ch.stream->get()));
     else if (op.ch_size[ch.id])
-      GP_CALL(gp_gather_rows(reinterpret_cast<float *>(op.buffer.data()), pc.data.data(),
-                             op.index.data() + op.ch_start[ch.id], op.ch_size[ch.id],
-                             gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit,
-                             ch.stream->get()));
+      GP_CALL(gp_gather_rows_planned(y, pc.data.data(), op.plans[ch.id]->get(), ch.stream->get()));
     ch.stream->sync();
   }
   *buffer = reinterpret_cast<RowData *>(op.buffer.data());

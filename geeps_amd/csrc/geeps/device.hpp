@@ -119,13 +119,18 @@ class PinnedArray {
   size_t n_ = 0;
 };
 
-// A row plan (gp_row_plan_create): a scatter DoubleIndex compiled once, on
-// the current device, for the ops whose index is fixed after
-// FinishVirtualIteration.
+// A row plan: a DoubleIndex compiled once, on the current device, for the ops
+// whose index is fixed after FinishVirtualIteration -- a scatter plan
+// (gp_row_plan_create) for Update, a gather plan (gp_gather_plan_create) for
+// Read.
 class RowPlan {
  public:
-  RowPlan(const gp_double_index *host_index, size_t n, size_t row_size, size_t num_vals_limit) {
-    GP_CALL(gp_row_plan_create(&p_, host_index, n, gp_double_index{0, 0}, row_size, num_vals_limit));
+  RowPlan(const gp_double_index *host_index, size_t n, size_t row_size, size_t num_vals_limit,
+          bool gather = false) {
+    if (gather)
+      GP_CALL(gp_gather_plan_create(&p_, host_index, n, gp_double_index{0, 0}, row_size, num_vals_limit));
+    else
+      GP_CALL(gp_row_plan_create(&p_, host_index, n, gp_double_index{0, 0}, row_size, num_vals_limit));
   }
   ~RowPlan() {
     if (p_) gp_row_plan_destroy(p_);

@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4) {
   const size_t tile = (size_t)kBlock * UNROLL;
   const size_t stride = (size_t)gridDim.x * tile;
-  const f4 *bp[NB];
+  const f4 *bp[NB > 0 ? NB : 1];  // NB = 0: a plain copy out = in (a gather plan's dense runs)
 #pragma unroll
   for (int k = 0; k < NB; ++k) bp[k] = reinterpret_cast<const f4 *>(b.p[k]);
 
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
   // Full tiles: no bounds checks inside.
   for (; base + (UNROLL - 1) * kBlock < n4; base += stride) {
     f4 acc[UNROLL];
-    f4 v[NB][UNROLL];
+    f4 v[NB > 0 ? NB : 1][UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) acc[u] = ZIN ? f4(0.0f) : in[base + u * kBlock];
 #pragma unroll
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
   constexpr int per_launch = BAL ? 1 : (RT > 0 ? 1 : 2);
   __shared__ f4 res[kPhaseLdsF4];
   f4 keep[RT > 0 ? RT : 1][U];
-  const f4 *bp[NB];
+  const f4 *bp[NB > 0 ? NB : 1];  // NB = 0: a plain copy out = in (a gather plan's dense runs)
 #pragma unroll
   for (int k = 0; k < NB; ++k) bp[k] = reinterpret_cast<const f4 *>(b.p[k]);
   const size_t G = gridDim.x;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
       if (t >= tiles || tile0 >= n4_tiles) break;  // block-uniform; later tiles are further out
       const size_t base = tile0 + threadIdx.x;
       f4 acc[U];
-      f4 v[NB][U];
+      f4 v[NB > 0 ? NB : 1][U];
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = ZIN ? f4(0.0f) : ld_stream(in + base + u * kBlock);
 #pragma unroll
@@ -345,8 +345,9 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
 // exact).  The zero-input form has one shape, 64-MiB chunks.
 template <int NB, bool ZIN>
 struct SweepShape {  // register tiles, tiles per burst of loads: the big chunks
-  static constexpr int RT = ZIN ? 6 : 14;
-  static constexpr int TG = ZIN ? 4 : 8;
+  // one stream (the zero-input form, the NB = 0 copy): 64-MiB chunks, bursts of 4
+  static constexpr int RT = (ZIN || NB == 0) ? 6 : 14;
+  static constexpr int TG = (ZIN || NB == 0) ? 4 : 8;
 };
 constexpr int kSweepRT = 6;  // the small (64-MiB) chunks and the zero-input form
 constexpr int kSweepTG = 4;
@@ -367,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
   const f4 *src[S];
 #pragma unroll
   for (int k = 0; k < S; ++k)
-    src[k] = (!ZIN && k == 0) ? in : reinterpret_cast<const f4 *>(b.p[ZIN ? k : k - 1]);
+    src[k] = (!ZIN && k == 0) ? in : reinterpret_cast<const f4 *>(b.p[ZIN ? k : (k > 0 ? k - 1 : 0)]);
   const size_t G = gridDim.x;
   const size_t lo = chunk * G * (size_t)kT * kPhaseTile;
   // Never taken (the host launches whole chunks only), but keep it: with this
@@ -1172,28 +1173,36 @@ struct RowRun {
 
 struct gp_row_plan_s {
   size_t num_rows = 0, row_size = 0, limit = 0;
+  bool gather = false;  // a gather plan (y[id0] = x[id1]); else a scatter plan
   std::vector<RowRun> dense;
   size_t dense_rows = 0;
-  gp_double_index *residual = nullptr;  // device, offsets applied, ascending id1
+  // device, offsets applied, ascending destination (scatter: id1, gather: id0)
+  gp_double_index *residual = nullptr;
   size_t residual_rows = 0;
   int device = 0;
 };
 
 namespace {
 
+// Scatter plans (y[id1] (+)= x[id0], the limit on the source x) sort by id1;
+// gather plans (y[id0] = x[id1], assign_rows_to_double_index, the limit on
+// the destination y) sort by id0.  Either way the limit guards the id0 side
+// and the destination must not repeat.
 int build_row_plan(gp_row_plan_s *p, const gp_double_index *host_index, size_t n,
                    gp_double_index off) {
   const size_t W = p->row_size;
+  const bool g = p->gather;
   std::vector<gp_double_index> rows(n);
   for (size_t r = 0; r < n; ++r)
     rows[r] = gp_double_index{host_index[r].id0 + off.id0, host_index[r].id1 + off.id1};
-  std::sort(rows.begin(), rows.end(), [](const gp_double_index &a, const gp_double_index &b) {
-    return a.id1 < b.id1;
+  auto dst = [g](const gp_double_index &d) { return g ? d.id0 : d.id1; };
+  std::sort(rows.begin(), rows.end(), [&](const gp_double_index &a, const gp_double_index &b) {
+    return dst(a) < dst(b);
   });
   for (size_t r = 1; r < n; ++r)
-    if (rows[r].id1 == rows[r - 1].id1)
-      return set_error(GP_ERR_INVALID, "row plan: destination row " + std::to_string(rows[r].id1) +
-                                           " repeats (scatter destinations must be distinct)");
+    if (dst(rows[r]) == dst(rows[r - 1]))
+      return set_error(GP_ERR_INVALID, "row plan: destination row " + std::to_string(dst(rows[r])) +
+                                           " repeats (destinations must be distinct)");
   auto whole = [&](const gp_double_index &d) { return (d.id0 + 1) * W <= p->limit; };
   const size_t min_rows = std::max<size_t>(1, kDenseRunBytes / (W * sizeof(float)));
   std::vector<gp_double_index> rest;
@@ -1204,7 +1213,8 @@ int build_row_plan(gp_row_plan_s *p, const gp_double_index *host_index, size_t n
              rows[b].id1 == rows[b - 1].id1 + 1)
         ++b;
     if (whole(rows[a]) && b - a >= min_rows) {
-      p->dense.push_back(RowRun{rows[a].id0, rows[a].id1, b - a});
+      p->dense.push_back(g ? RowRun{rows[a].id1, rows[a].id0, b - a}
+                           : RowRun{rows[a].id0, rows[a].id1, b - a});
       p->dense_rows += b - a;
     } else {
       rest.insert(rest.end(), rows.begin() + a, rows.begin() + b);
@@ -1223,16 +1233,25 @@ int build_row_plan(gp_row_plan_s *p, const gp_double_index *host_index, size_t n
 // OP kAddFrom: y += x over the plan's rows; kInitFrom: y = 0.0f + x (0.0f past
 // the limit), as gp_scatter_add_rows / gp_scatter_init_rows with the plan's
 // index, offset and limit.
-template <int OP>
-int launch_planned(float *y, const float *x, const gp_row_plan_s *p, hipStream_t s) {
+int check_plan(const gp_row_plan_s *p, bool gather) {
   if (!p) return set_error(GP_ERR_INVALID, "null row plan");
-  if (p->num_rows == 0) return GP_OK;
+  if (p->gather != gather)
+    return set_error(GP_ERR_INVALID, gather ? "a scatter row plan passed to a gather"
+                                            : "a gather row plan passed to a scatter");
   if (p->residual_rows) {
     int dev = -1;
     GP_HIP_TRY(hipGetDevice(&dev));
     if (dev != p->device)
       return set_error(GP_ERR_INVALID, "row plan used on another device than it was built on");
   }
+  return GP_OK;
+}
+
+template <int OP>
+int launch_planned(float *y, const float *x, const gp_row_plan_s *p, hipStream_t s) {
+  const int rc0 = check_plan(p, false);
+  if (rc0 != GP_OK) return rc0;
+  if (p->num_rows == 0) return GP_OK;
   const size_t W = p->row_size;
   for (const RowRun &r : p->dense) {
     BucketPtrs b = {};
@@ -1247,6 +1266,56 @@ int launch_planned(float *y, const float *x, const gp_row_plan_s *p, hipStream_t
                              p->limit, s, /*sorted=*/true);
   return GP_OK;
 }
+
+// A gather plan: y[id0] = x[id1] over the plan's rows, x flat (xs == nullptr)
+// or a segmented cache.  Dense runs are plain copies through the bucket-sum
+// kernels with no bucket (NB = 0: the sweep's 64-MiB chunks, then the
+// tile-major and mixed forms), split where a run crosses a segment boundary;
+// the residual rows through the gather row kernels, in destination order.
+int launch_gather_planned(float *y, const float *x, const gp_row_segments *xs,
+                          const gp_row_plan_s *p, hipStream_t s) {
+  const int rc0 = check_plan(p, true);
+  if (rc0 != GP_OK) return rc0;
+  if (p->num_rows == 0) return GP_OK;
+  bool seg_aligned = false;
+  if (xs) {
+    const int rc = check_segments(xs, p->row_size, &seg_aligned);
+    if (rc != GP_OK) return rc;
+  }
+  const size_t W = p->row_size;
+  const BucketPtrs none = {};
+  for (const RowRun &r : p->dense) {
+    uint64_t row = r.x_row, left = r.rows;  // source (cache) rows still to copy
+    float *yr = y + r.y_row * W;
+    while (left) {
+      const float *src = nullptr;
+      uint64_t take = left;
+      if (!xs) {
+        src = x + row * W;
+      } else {
+        uint32_t i = 0;  // the segment holding `row`: the last one starting at or before it
+        while (i + 1 < xs->count && xs->first_row[i + 1] <= row) ++i;
+        src = xs->base[i] + (row - xs->first_row[i]) * W;
+        if (i + 1 < xs->count) take = std::min<uint64_t>(take, xs->first_row[i + 1] - row);
+      }
+      const int rc = launch_bucket_sum_nb<0>(yr, src, none, take * W, s);
+      if (rc != GP_OK) return rc;
+      yr += take * W;
+      row += take;
+      left -= take;
+    }
+  }
+  if (p->residual_rows) {
+    if (xs) return launch_row_op_seg<kAssignTo, kSegX>(y, xs, p->residual, p->residual_rows,
+                                                       gp_double_index{0, 0}, W, p->limit, s);
+    return launch_row_op<kAssignTo>(y, x, p->residual, p->residual_rows, gp_double_index{0, 0}, W,
+                                    p->limit, s, /*sorted=*/true);
+  }
+  return GP_OK;
+}
+
+int create_plan(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
+                gp_double_index offset, size_t row_size, size_t num_vals_limit, bool gather);
 
 }  // namespace
 
@@ -1305,6 +1374,30 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
 
 int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
                        gp_double_index offset, size_t row_size, size_t num_vals_limit) {
+  return create_plan(plan, host_index, num_rows, offset, row_size, num_vals_limit, false);
+}
+
+int gp_gather_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
+                          gp_double_index offset, size_t row_size, size_t num_vals_limit) {
+  return create_plan(plan, host_index, num_rows, offset, row_size, num_vals_limit, true);
+}
+
+int gp_gather_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s) {
+  if (!y || !x) return set_error(GP_ERR_INVALID, "null pointer");
+  return launch_gather_planned(y, x, nullptr, plan, (hipStream_t)s);
+}
+
+int gp_gather_rows_segmented_planned(float *y, const gp_row_segments *x_segments, gp_row_plan plan,
+                                     gp_stream s) {
+  if (!y || !x_segments) return set_error(GP_ERR_INVALID, "null pointer");
+  return launch_gather_planned(y, nullptr, x_segments, plan, (hipStream_t)s);
+}
+
+}  // extern "C"
+
+namespace {
+int create_plan(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
+                gp_double_index offset, size_t row_size, size_t num_vals_limit, bool gather) {
   if (!plan) return set_error(GP_ERR_INVALID, "null pointer");
   *plan = nullptr;
   if (num_rows && !host_index) return set_error(GP_ERR_INVALID, "null index");
@@ -1313,6 +1406,7 @@ int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, siz
   p->num_rows = num_rows;
   p->row_size = row_size;
   p->limit = num_vals_limit;
+  p->gather = gather;
   if (hipGetDevice(&p->device) != hipSuccess) p->device = 0;
   const int rc = build_row_plan(p, host_index, num_rows, offset);
   if (rc != GP_OK) {
@@ -1322,6 +1416,9 @@ int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, siz
   *plan = p;
   return GP_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int gp_row_plan_destroy(gp_row_plan plan) {
   if (!plan) return GP_OK;
@@ -1347,7 +1444,9 @@ int gp_row_plan_launches(gp_row_plan plan, int init, int *sweep_launches, int *p
   size_t sw = 0, ph = 0, ot = plan->residual_rows ? 1 : 0;
   for (const RowRun &r : plan->dense) {
     const size_t n = r.rows * plan->row_size;
-    const SumLaunches l = init ? sum_launches<1, true>(n) : sum_launches<1>(n);
+    const SumLaunches l = plan->gather ? sum_launches<0>(n)
+                          : init       ? sum_launches<1, true>(n)
+                                       : sum_launches<1>(n);
     sw += l.sweep + l.sweep_small;
     ph += l.phased;
     ot += l.other;

@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 7  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 8  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -69,6 +69,9 @@ _SIGNATURES = {
     "gp_row_plan_destroy": (_i, [_vp]),
     "gp_row_plan_info": (_i, [_vp, _c.POINTER(_sz), _c.POINTER(_sz), _c.POINTER(_sz)]),
     "gp_row_plan_launches": (_i, [_vp, _i, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
+    "gp_gather_plan_create": (_i, [_c.POINTER(_vp), _vp, _sz, DoubleIndex, _sz, _sz]),
+    "gp_gather_rows_planned": (_i, [_vp, _vp, _vp, _vp]),
+    "gp_gather_rows_segmented_planned": (_i, [_vp, _c.POINTER(RowSegments), _vp, _vp]),
     "gp_scatter_add_rows_planned": (_i, [_vp, _vp, _vp, _vp]),
     "gp_scatter_init_rows_planned": (_i, [_vp, _vp, _vp, _vp]),
     "gp_gather_rows_segmented": (_i, [_vp, _c.POINTER(RowSegments), _vp, _sz, DoubleIndex, _sz,

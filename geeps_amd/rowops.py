@@ -170,19 +170,27 @@ def assign_rows_from_double_index_gpu(rows_y, rows_x, index, num_rows=None, inde
 
 
 class RowPlan:
-    """A scatter DoubleIndex compiled once (gp_row_plan_create): the rows in
-    destination (id1) order; id0/id1-contiguous runs of >= 4 MiB moved by the
-    phase-separated sum kernels, the rest by the wave-map row kernel over an
-    id1-sorted device index.
+    """A DoubleIndex compiled once.  ``kind="scatter"`` (gp_row_plan_create):
+    the rows in destination (id1) order; id0/id1-contiguous runs of >= 4 MiB
+    moved by the phase-separated sum kernels, the rest by the wave-map row
+    kernel over an id1-sorted device index.  ``kind="gather"``
+    (gp_gather_plan_create): the same for assign_rows_to_double_index_gpu's
+    index, in destination (id0) order, dense runs copied by the
+    phase-separated kernels.
 
-    ``index``: (n, 2) int64 array or tensor (copied to the host once), as for
-    add_rows_from_double_index_gpu; ``index_offset`` and ``num_vals_limit``
-    are baked in.  ``add(y, x)`` / ``init(y, x)`` are bit-identical to
+    ``index``: (n, 2) int64 array or tensor (copied to the host once);
+    ``index_offset`` and ``num_vals_limit`` are baked in.  Scatter plans:
+    ``add(y, x)`` / ``init(y, x)`` are bit-identical to
     add_rows_from_double_index_gpu / init_rows_from_double_index_gpu over the
-    same index.  Destinations must be distinct (ValueError otherwise)."""
+    same index.  Gather plans: ``gather(y, x)`` / ``gather_segmented(y,
+    segments)`` to assign_rows_to_double_index_gpu / gather_rows_segmented.
+    Destinations must be distinct (ValueError otherwise)."""
 
     def __init__(self, index, num_rows=None, index_offset=None, row_size=ROW_DATA_SIZE,
-                 num_vals_limit=None):
+                 num_vals_limit=None, kind="scatter"):
+        if kind not in ("scatter", "gather"):
+            raise ValueError("kind must be 'scatter' or 'gather'")
+        self.kind = kind
         import numpy as np
         if isinstance(index, torch.Tensor):
             index = index.detach().cpu().numpy()
@@ -203,12 +211,19 @@ class RowPlan:
         r0 = idx[:, 0] + self.offset.id0 if n else idx[:, 0]
         r1 = idx[:, 1] + self.offset.id1 if n else idx[:, 1]
         active = r0 * self.row_size < self.limit if self.limit < (1 << 62) else np.ones(n, bool)
-        # bounds the row kernels need: source rows below the limit, every destination
-        self.x_need = min((int(r0[active].max()) + 1) * self.row_size, self.limit) if active.any() else 0
-        self.y_need = (int(r1.max()) + 1) * self.row_size if n else 0
+        if kind == "scatter":
+            # bounds the row kernels need: source rows below the limit, every destination
+            self.x_need = min((int(r0[active].max()) + 1) * self.row_size, self.limit) if active.any() else 0
+            self.y_need = (int(r1.max()) + 1) * self.row_size if n else 0
+        else:
+            # destinations (id0) below the limit, and whole source rows for them
+            self.y_need = min((int(r0[active].max()) + 1) * self.row_size, self.limit) if active.any() else 0
+            self.x_need = (int(r1[active].max()) + 1) * self.row_size if active.any() else 0
+            self._src_rows = r1[active]
         self._h = ctypes.c_void_p()
-        check(native.lib().gp_row_plan_create(ctypes.byref(self._h), idx.ctypes.data, n, self.offset,
-                                              self.row_size, self.limit), "gp_row_plan_create")
+        create = native.lib().gp_row_plan_create if kind == "scatter" else native.lib().gp_gather_plan_create
+        check(create(ctypes.byref(self._h), idx.ctypes.data, n, self.offset, self.row_size, self.limit),
+              "gp_row_plan_create" if kind == "scatter" else "gp_gather_plan_create")
 
     def info(self) -> dict:
         a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
@@ -227,7 +242,9 @@ class RowPlan:
               "gp_row_plan_launches")
         return {"sweep": a.value, "phased": b.value, "other": c.value}
 
-    def _run(self, fn, y, x, stream, what):
+    def _run(self, fn, y, x, stream, what, kind="scatter"):
+        if self.kind != kind:
+            raise ValueError(f"a {self.kind} plan cannot run {what}")
         _dev_f32(y, "rows_y")
         _dev_f32(x, "rows_x")
         if self.x_need > x.numel():
@@ -243,6 +260,24 @@ class RowPlan:
     def init(self, rows_y, rows_x, stream=None) -> None:
         self._run(native.lib().gp_scatter_init_rows_planned, rows_y, rows_x, stream,
                   "gp_scatter_init_rows_planned")
+
+    def gather(self, rows_y, rows_x, stream=None) -> None:
+        self._run(native.lib().gp_gather_rows_planned, rows_y, rows_x, stream,
+                  "gp_gather_rows_planned", kind="gather")
+
+    def gather_segmented(self, rows_y, segments, stream=None) -> None:
+        """``segments`` = [(first_row, tensor), ...] as for gather_rows_segmented."""
+        if self.kind != "gather":
+            raise ValueError("a scatter plan cannot run gp_gather_rows_segmented_planned")
+        _dev_f32(rows_y, "rows_y")
+        t, ranges = _segments(segments, self.row_size)
+        if self.y_need > rows_y.numel():
+            raise ValueError("destination row out of range for rows_y")
+        if self.num_rows:
+            _validate_segment_rows(torch.as_tensor(self._src_rows, device=rows_y.device), ranges)
+        check(native.lib().gp_gather_rows_segmented_planned(rows_y.data_ptr(), ctypes.byref(t), self._h,
+                                                            _stream_ptr(stream)),
+              "gp_gather_rows_segmented_planned")
 
     def close(self) -> None:
         if self._h:

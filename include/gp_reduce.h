@@ -41,7 +41,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 7
+#define GP_ABI_VERSION 8
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -143,7 +143,8 @@ int gp_row_plan_destroy(gp_row_plan plan);
  * row kernels). */
 int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *dense_runs, size_t *dense_rows);
 /* Launch plan of one planned add (init = 0) or fused init (init = 1) over
- * 16-B-aligned buffers; launches nothing.  *sweep_launches = launches of the
+ * 16-B-aligned buffers (a gather plan: its gather, `init` ignored, flat
+ * cache); launches nothing.  *sweep_launches = launches of the
  * stream-by-stream sum kernel over the dense runs (1 bucket; the init's
  * zero-input form), *phased_launches = tile-major phase-separated launches,
  * *other_launches = everything else (mixed / scalar sum forms, and one row
@@ -191,6 +192,23 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
                                   const gp_double_index *index, size_t num_rows,
                                   gp_double_index offset, size_t row_size,
                                   size_t num_vals_limit, gp_stream s);
+
+/* A GATHER plan: the same compilation for gp_gather_rows' index (y[id0] =
+ * x[id1], assign_rows_to_double_index_gpu, src/common/row-op-util.cu:39-72:
+ * num_vals_limit guards the destination y).  libgeeps builds one per Read op
+ * and channel.  Rows are visited in destination (id0) order, so destinations
+ * must be distinct (GP_ERR_INVALID otherwise); dense runs are plain copies
+ * through the phase-separated kernels, the rest goes to the gather row
+ * kernels.  A gather plan works only with the gp_gather_rows_*planned calls,
+ * a scatter plan only with the scatter ones (GP_ERR_INVALID otherwise). */
+int gp_gather_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
+                          gp_double_index offset, size_t row_size, size_t num_vals_limit);
+/* gp_gather_rows(y, x, index, ...) through a gather plan. */
+int gp_gather_rows_planned(float *y, const float *x, gp_row_plan plan, gp_stream s);
+/* gp_gather_rows_segmented(y, x_segments, index, ...) through a gather plan:
+ * a dense run that crosses a segment boundary is copied piece by piece. */
+int gp_gather_rows_segmented_planned(float *y, const gp_row_segments *x_segments, gp_row_plan plan,
+                                     gp_stream s);
 
 /* ---------------------------------------------------------------------------
  * Dense reductions (server side).

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 7
+    assert L.gp_abi_version() == native.ABI_VERSION == 8
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -218,6 +218,39 @@ def test_row_plan_launches_without_device():
     assert native.lib().gp_row_plan_destroy(h) == 0
     assert native.lib().gp_row_plan_launches(None, 0, ctypes.byref(a), ctypes.byref(b),
                                              ctypes.byref(c)) == 1
+
+
+def test_gather_plan_without_device():
+    """Gather plans (gp_gather_plan_create): destinations are id0, which must
+    not repeat; an identity index is one dense run, copied by the no-bucket
+    sweep in 64-MiB chunks (a 4 GiB table: 64 launches); plans of one kind
+    are refused by the other kind's calls before anything launches."""
+    import numpy as np
+    L = native.lib()
+    h = ctypes.c_void_p()
+    n = 1 << 20
+    a = np.ascontiguousarray(np.stack([np.arange(n), 5 + np.arange(n)], 1), dtype=np.int64)
+    assert L.gp_gather_plan_create(ctypes.byref(h), a.ctypes.data, n, native.DoubleIndex(0, 0), 1024,
+                                   (1 << 64) - 1) == 0
+    assert _info(h) == (n, 1, n)
+    x, y, z = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert L.gp_row_plan_launches(h, 0, ctypes.byref(x), ctypes.byref(y), ctypes.byref(z)) == 0
+    assert (x.value, y.value, z.value) == (64, 0, 0)
+    # a gather plan is not a scatter plan, and the other way round
+    fake = ctypes.c_void_p(16)
+    assert L.gp_scatter_add_rows_planned(fake, fake, h, None) == 1
+    assert b"gather row plan" in L.gp_last_error()
+    assert L.gp_row_plan_destroy(h) == 0
+    rc, hs = _plan(a, row_size=1024)
+    assert rc == 0
+    assert L.gp_gather_rows_planned(fake, fake, hs, None) == 1
+    assert b"scatter row plan" in L.gp_last_error()
+    assert L.gp_row_plan_destroy(hs) == 0
+    # repeated destination rows (id0) are refused
+    dup = np.ascontiguousarray([[0, 1], [1, 2], [1, 3]], dtype=np.int64)
+    assert L.gp_gather_plan_create(ctypes.byref(h), dup.ctypes.data, 3, native.DoubleIndex(0, 0), 128,
+                                   (1 << 64) - 1) == 1
+    assert b"repeats" in L.gp_last_error()
 
 
 def test_row_plan_classifies_dense_runs_without_device():

@@ -659,6 +659,84 @@ def test_row_plan_long_run_takes_sweep_forms(dev):
     plan.close()
 
 
+@pytest.mark.parametrize("kind", ["identity", "permuted", "mixed"])
+@pytest.mark.parametrize("W,limit_frac,off,nseg", [(128, None, (0, 0), 0), (64, None, (5, 3), 0),
+                                                    (128, 0.83, (0, 0), 0), (1024, None, (0, 2), 0),
+                                                    (130, None, (0, 0), 0), (4, 0.5, (1, 1), 0),
+                                                    (128, None, (0, 0), 3), (128, 0.9, (2, 1), 7),
+                                                    (64, None, (0, 0), 64)])
+def test_gather_plan_matches_oracle(dev, kind, W, limit_frac, off, nseg):
+    """gp_gather_rows_planned / gp_gather_rows_segmented_planned (the Read
+    side's plan: dense runs copied by the phase-separated kernels, the rest by
+    the gather row kernels in destination order) equal the oracle's
+    assign_rows_to_double_index bit for bit, with offsets, num_vals_limit on
+    the destination, and segment boundaries cutting the dense runs; rows not
+    listed are untouched (the scatter plans' indexes: the mixed case has 3
+    dense runs of >= 4 MiB, short runs and scattered rows)."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(W * 5 + len(kind) + nseg + int((limit_frac or 0) * 10))
+    n_cache = 5 * ((4 << 20) // (W * 4)) + 8000
+    # id0: op-buffer rows (the destinations, distinct), id1: cache rows
+    idx, n_op = _plan_index(rng, kind, n_cache - off[1], W)
+    n_y = int(idx[:, 0].max()) + 1 + off[0] + 3
+    limit = None if limit_frac is None else int(n_y * W * limit_frac) + 3
+    x = rng.standard_normal(n_cache * W).astype(np.float32)
+    x[rng.choice(x.size, 300, replace=False)] = np.float32(-0.0)
+    y = rng.standard_normal(n_y * W).astype(np.float32)
+    e = y.copy()
+    oracle.assign_rows_to_double_index(e, x, idx, off, W, limit)
+    plan = rowops.RowPlan(idx, n_op, off, W, limit, kind="gather")
+    info = plan.info()
+    if kind == "identity" and limit is None:
+        assert info == {"rows": n_op, "dense_runs": 1, "dense_rows": n_op, "residual_rows": 0}
+    if kind == "mixed" and limit is None:
+        assert info["dense_runs"] == 3 and info["residual_rows"] > 0
+    ty = T(y, dev)
+    if nseg == 0:
+        plan.gather(ty, T(x, dev))
+    else:
+        bounds = _split(rng, n_cache, nseg)
+        segs = [(bounds[i], T(x[bounds[i] * W:bounds[i + 1] * W], dev)) for i in range(nseg)]
+        plan.gather_segmented(ty, segs)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), (kind, W, nseg)
+    with pytest.raises(ValueError):
+        plan.add(ty, T(x, dev))
+    plan.close()
+
+
+def test_gather_plan_long_run_takes_sweep(dev):
+    """A 420,000-row identity-like gather (205 MiB at 128 floats: 3 whole
+    64-MiB copy sweeps, then the tile-major rest) from a cache split in 2
+    segments at a row inside the run: bit for bit, -0.0 and NaN payloads
+    copied unchanged."""
+    import ctypes
+    from geeps_amd import native, rowops
+    rng = np.random.default_rng(42)
+    W, n = 128, 420_000
+    idx = np.stack([np.arange(n), 9 + np.arange(n)], 1).astype(np.int64)
+    x = rng.standard_normal((n + 20) * W).astype(np.float32)
+    x[:5000] = np.float32(-0.0)
+    x.view(np.uint32)[5000:5010] = 0x7FC00123  # NaN with a payload
+    y = np.zeros(n * W, np.float32)
+    plan = rowops.RowPlan(idx, row_size=W, kind="gather")
+    a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    native.check(native.lib().gp_row_plan_launches(plan._h, 0, ctypes.byref(a), ctypes.byref(b),
+                                                   ctypes.byref(c)))
+    assert a.value == 3 and b.value == 1
+    cut = 9 + 250_000
+    segs = [(0, T(x[:cut * W], dev)), (cut, T(x[cut * W:], dev))]
+    ty = T(y, dev)
+    plan.gather_segmented(ty, segs)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(x[9 * W:(9 + n) * W]))
+    ty.zero_()
+    plan.gather(ty, T(x, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(x[9 * W:(9 + n) * W]))
+    plan.close()
+
+
 def test_row_plan_unaligned_and_side_stream(dev):
     """Bases 4 B off 16-B alignment (a dense run takes the scalar sum form, the
     residual the scalar row kernel) on a side stream: still bit-exact."""
