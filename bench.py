@@ -612,7 +612,7 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
            "table_bytes": rd_rows * 512, "transport": "ipc (same node)", "clocks": clocks,
            "warmup": warmup}
     for P in procs:
-        r = mod.run(P, rd_rows, clocks, warmup, 0, "ipc", timeout=300)
+        r = mod.run(P, rd_rows, clocks, warmup, 0, "ipc", timeout=120)
         out[f"p{P}"] = {"workers": P, "ms_per_clock": r["ms_per_clock_max"],
                         "delta_GBps": r["aggregate_delta_GBps"],
                         "ms_per_clock_each": r["ms_per_clock"]}
