@@ -440,6 +440,12 @@ SweepSplit sweep_split(size_t n4_tiles) {
   sp.big = n4_tiles / sp.big_f4;
   if (sp.big < (size_t)kPhaseMinChunks) sp.big = 0;
   if (RT != kSweepRT && NB >= 3) {  // at 1-2 buckets the 64-MiB sweep lost to tile-major
+    // One big chunk fewer when that lets whole small chunks take more of the
+    // rest: a 512-MiB shard is 4 x 96 + 2 x 64 MiB, not 5 x 96 + 32 MiB
+    // through the tile-major form.
+    if (sp.big > (size_t)kPhaseMinChunks &&
+        (n4_tiles - (sp.big - 1) * sp.big_f4) % sp.small_f4 < (n4_tiles - sp.big * sp.big_f4) % sp.small_f4)
+      --sp.big;
     sp.small = (n4_tiles - sp.big * sp.big_f4) / sp.small_f4;
     if (sp.big == 0 && sp.small < (size_t)kPhaseMinChunks) sp.small = 0;
   }

@@ -143,8 +143,9 @@ def test_bucket_sum_plan_without_device():
     assert sweep_plan(1 << 30, 1) == (43, 14, 42)
     assert sweep_plan(1 << 30, 4) == (43, 14, 43)
     assert sweep_plan(288 << 18, 2) == (3, 14, 3)
-    # the 8-GPU shard (512 MiB): 5 x 96 MiB, the 32-MiB rest in one balanced tile-major chunk
-    assert sweep_plan(1 << 27, 8) == (6, 14, 5)
+    # the 8-GPU shard (512 MiB): 4 x 96 + 2 x 64 MiB (not 5 x 96 + a 32-MiB tile-major rest)
+    assert sweep_plan(1 << 27, 8) == (6, 14, 6)
+    assert sweep_plan(1 << 29, 8) == (22, 14, 22)  # the 2-GPU shard: 20 x 96 + 2 x 64 MiB
     assert sweep_plan(1 << 28, 3) == (11, 14, 11)  # the 4-GPU shard (1 GiB): 10 x 96 + 64 MiB
     # 200 MiB: under 3 big chunks, so 3 64-MiB sweep chunks, then the 8-MiB
     # rest in 1 balanced tile-major chunk
@@ -169,7 +170,14 @@ def test_bucket_sum_plan_without_device():
     n = (1 << 27) + 4 + 3  # 512 MiB + one dwordx4 + 3 floats
     assert L.gp_bucket_sum_launch_plan(n, 5, ctypes.byref(sp)) == 0
     assert (sp.sweep_launches, sp.small_sweep_launches, sp.phased_launches, sp.phased_reg_tiles,
-            sp.other_launches) == (5, 0, 1, 4, 2)
+            sp.other_launches) == (4, 2, 0, -1, 2)
+    n = (1 << 27) + (16 << 18)  # 528 MiB: 4 x 96 + 2 x 64 MiB, 16 MiB tile-major (not 48)
+    assert L.gp_bucket_sum_launch_plan(n, 5, ctypes.byref(sp)) == 0
+    assert (sp.sweep_launches, sp.small_sweep_launches, sp.phased_launches, sp.phased_reg_tiles,
+            sp.other_launches) == (4, 2, 1, 4, 0)
+    n = (1 << 27) + (64 << 18)  # 576 MiB = 6 x 96 MiB exactly
+    assert L.gp_bucket_sum_launch_plan(n, 8, ctypes.byref(sp)) == 0
+    assert (sp.sweep_launches, sp.small_sweep_launches, sp.phased_launches) == (6, 0, 0)
     assert L.gp_bucket_sum_launch_plan(n, 9, ctypes.byref(sp)) == 1
     assert L.gp_bucket_sum_launch_plan(n, 2, None) == 1
 

@@ -324,6 +324,38 @@ def _sample_rows(rng, R, k=2048):
     return np.unique(np.concatenate([[0, R - 1], rng.choice(R, size=k, replace=False)]))
 
 
+@pytest.mark.parametrize("N,out_of_place", [(3, False), (5, True), (8, False), (8, True)])
+def test_bucket_sum_big_and_small_sweeps(dev, N, out_of_place):
+    """528 MiB + 7 floats: 4 sweep chunks of 96 MiB, 2 of 64 MiB, a 16-MiB
+    tile-major chunk, one dwordx4 of the mixed form and a 3-float scalar
+    tail, as the launch plan reports; every element bit for bit against a
+    plain torch fp32 reference adding the buckets in client order."""
+    import ctypes
+    from geeps_amd import native, rowops
+    n = (132 << 20) + 7
+    sp = native.SumPlan()
+    native.check(native.lib().gp_bucket_sum_launch_plan(n, N, ctypes.byref(sp)))
+    assert (sp.sweep_launches, sp.small_sweep_launches, sp.phased_launches, sp.other_launches) == (4, 2, 1, 2)
+    g = torch.Generator(device=dev)
+    g.manual_seed(528 + N)
+    buckets = [torch.rand(n, generator=g, device=dev) - 0.5 for _ in range(N)]
+    master = torch.rand(n, generator=g, device=dev) - 0.5
+    expect = master.clone()
+    for b in buckets:
+        expect += b
+    if out_of_place:
+        m0 = master.clone()
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+        rowops.bucket_sum_into(out, master, buckets)
+        torch.cuda.synchronize()
+        assert torch.equal(master.view(torch.int32), m0.view(torch.int32))
+    else:
+        rowops.bucket_sum_apply(master, buckets)
+        out = master
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), expect.view(torch.int32))
+
+
 @pytest.mark.slow
 def test_full_size_8way_bucket_sum(dev):
     """1M rows x 1024 fp32, 8 clients (36 GiB resident).  Every element against a
