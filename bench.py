@@ -589,7 +589,7 @@ def load_traffic(workload_key, kernel):
         return None
 
 
-def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2), alexnet=True):
+def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
     """The drop-in path end to end: scripts/apps/geeps_clock_bench (built by
     __graft_entry__.build() against libgeeps.so and include/geeps.hpp, as an
     app links) run as P processes on this GPU, one GeePS worker + tablet server
@@ -598,8 +598,7 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2), alexnet=True):
     segmented param cache) -> PreUpdate -> device fill -> PostRead -> Update
     (fused init through the row plan) -> Clock (push, the server's bucket sum,
     the zero-copy refresh), through the public API.  P = 2 is configs[1]'s
-    2 loopback clients; every worker updates every row each clock.  Then
-    configs[4]'s shape: 8 workers on an AlexNet-sized table, staleness 1.
+    2 loopback clients; every worker updates every row each clock.
     delta_GBps = P * table bytes / the slowest worker's ms per clock."""
     import importlib.util
     path = os.path.join(REPO, "scripts", "run_clock_bench.py")
@@ -617,17 +616,6 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2), alexnet=True):
         out[f"p{P}"] = {"workers": P, "ms_per_clock": r["ms_per_clock_max"],
                         "delta_GBps": r["aggregate_delta_GBps"],
                         "ms_per_clock_each": r["ms_per_clock"]}
-    if alexnet:
-        # BASELINE configs[4]: an AlexNet-sized table (~61 M params = 476,292
-        # RowData rows), 8 workers x 8 tablet servers, staleness 1; here the 8
-        # processes share this one GPU (2 hardware queues each)
-        rows_a = 476292
-        r = mod.run(8, rows_a, 20, 3, 1, "ipc", timeout=120)
-        out["configs4_alexnet_p8_s1"] = {"workers": 8, "rows": rows_a, "table_bytes": rows_a * 512,
-                                         "slack": 1, "ms_per_clock": r["ms_per_clock_max"],
-                                         "delta_GBps": r["aggregate_delta_GBps"],
-                                         "note": "8 processes on one GPU; one process per GPU "
-                                                 "is the deployment"}
     return out
 
 
