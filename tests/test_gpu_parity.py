@@ -769,6 +769,91 @@ def test_gather_plan_long_run_takes_sweep(dev):
     plan.close()
 
 
+def _fuzz_index(rng, n_cache, W):
+    """An op index built from random pieces: dense runs (some past the 4-MiB
+    plan threshold), short runs, single rows, in shuffled op order; id0 are
+    the op rows (distinct), id1 distinct cache rows."""
+    big = max(1, (4 << 20) // (W * 4))
+    free = rng.permutation(n_cache)
+    taken = np.zeros(n_cache, bool)
+    parts, j0 = [], 0
+    for _ in range(int(rng.integers(1, 6))):
+        L = int(rng.choice([1, 2, 7, big - 1, big, big + 13, 2 * big]))
+        start = int(rng.integers(0, max(1, n_cache - L)))
+        seg = np.arange(start, min(n_cache, start + L))
+        seg = seg[~taken[seg]]
+        if seg.size == 0:
+            continue
+        # keep only the longest stretch of consecutive untaken rows
+        cuts = np.flatnonzero(np.diff(seg) != 1) + 1
+        seg = max(np.split(seg, cuts), key=len)
+        taken[seg] = True
+        parts.append(np.stack([j0 + np.arange(seg.size), seg], 1))
+        j0 += seg.size
+    rest = free[~taken[free]][:int(rng.integers(0, 2000))]
+    if rest.size:
+        parts.append(np.stack([j0 + np.arange(rest.size), rest], 1))
+        j0 += rest.size
+    idx = np.concatenate(parts).astype(np.int64)
+    return idx[rng.permutation(idx.shape[0])], idx.shape[0]
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_row_plans_fuzz(dev, case):
+    """Random op indexes (dense runs around the plan threshold, short runs,
+    scattered rows), row sizes, offsets and num_vals_limit: the scatter plan's
+    add and init and the gather plan's flat and segmented gather all equal the
+    oracle bit for bit."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(9000 + case)
+    W = int(rng.choice([4, 8, 64, 128, 132, 256]))
+    n_cache = 3 * max(1, (4 << 20) // (W * 4)) + int(rng.integers(100, 5000))
+    off = (int(rng.integers(0, 4)), int(rng.integers(0, 4)))
+    idx, n_op = _fuzz_index(rng, n_cache - off[1], W)
+    n_x = n_op + off[0]
+    limit = None if rng.random() < 0.5 else int(rng.integers(1, n_x * W + 1))
+    x = rng.standard_normal(n_x * W).astype(np.float32)
+    x[rng.choice(x.size, min(x.size, 200), replace=False)] = np.float32(-0.0)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    tx = T(x, dev)
+    # scatter plan: add, init
+    plan = rowops.RowPlan(idx, n_op, off, W, limit)
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    ty = T(y, dev)
+    plan.add(ty, tx)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", case, W, off, limit)
+    e = y.copy()
+    listed = np.zeros(n_cache, bool)
+    listed[idx[:, 1] + off[1]] = True
+    e.reshape(n_cache, W)[listed] = 0.0
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    ty = T(y, dev)
+    plan.init(ty, tx)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", case, W, off, limit)
+    plan.close()
+    # gather plan: y_op[id0] = cache[id1], the limit on the op side
+    gplan = rowops.RowPlan(idx, n_op, off, W, limit, kind="gather")
+    cache = y
+    dst = rng.standard_normal(n_x * W).astype(np.float32)
+    e = dst.copy()
+    oracle.assign_rows_to_double_index(e, cache, idx, off, W, limit)
+    td = T(dst, dev)
+    gplan.gather(td, T(cache, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(td.cpu().numpy()), bits(e)), ("gather", case, W, off, limit)
+    nseg = int(rng.integers(1, 9))
+    bounds = _split(rng, n_cache, nseg)
+    segs = [(bounds[i], T(cache[bounds[i] * W:bounds[i + 1] * W], dev)) for i in range(nseg)]
+    td = T(dst, dev)
+    gplan.gather_segmented(td, segs)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(td.cpu().numpy()), bits(e)), ("gather_seg", case, W, off, limit, nseg)
+    gplan.close()
+
+
 def test_row_plan_unaligned_and_side_stream(dev):
     """Bases 4 B off 16-B alignment (a dense run takes the scalar sum form, the
     residual the scalar row kernel) on a side stream: still bit-exact."""
