@@ -802,8 +802,8 @@ def _fuzz_index(rng, n_cache, W):
 def test_row_plans_fuzz(dev, case):
     """Random op indexes (dense runs around the plan threshold, short runs,
     scattered rows), row sizes, offsets and num_vals_limit: the scatter plan's
-    add and init and the gather plan's flat and segmented gather all equal the
-    oracle bit for bit."""
+    add and init and the gather plan's flat and segmented gather (segments
+    16-B aligned or not) all equal the oracle bit for bit."""
     from geeps_amd import rowops
     rng = np.random.default_rng(9000 + case)
     W = int(rng.choice([4, 8, 64, 128, 132, 256]))
@@ -846,7 +846,15 @@ def test_row_plans_fuzz(dev, case):
     assert np.array_equal(bits(td.cpu().numpy()), bits(e)), ("gather", case, W, off, limit)
     nseg = int(rng.integers(1, 9))
     bounds = _split(rng, n_cache, nseg)
-    segs = [(bounds[i], T(cache[bounds[i] * W:bounds[i + 1] * W], dev)) for i in range(nseg)]
+    pad = int(rng.integers(0, 2))  # 1: every segment a view one float into its buffer (unaligned)
+
+    def seg(i):
+        a, b = bounds[i] * W, bounds[i + 1] * W
+        big = torch.empty(b - a + pad, dtype=torch.float32, device=dev)
+        big[pad:].copy_(T(cache[a:b], dev))
+        return big[pad:]
+
+    segs = [(bounds[i], seg(i)) for i in range(nseg)]
     td = T(dst, dev)
     gplan.gather_segmented(td, segs)
     torch.cuda.synchronize()
