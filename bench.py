@@ -36,7 +36,8 @@ client_rowops (scatter-add / fused init / gather of the table's 8M RowData
 rows, random and identity DoubleIndex, unplanned and through a row plan),
 host_inclusive (pinned H2D + sum + D2H, serialized and pipelined, full table),
 libgeeps_clock (the drop-in library's clock through include/geeps.hpp, 1 and
-2 processes on the same 4 GiB table).
+2 processes on the same 4 GiB table), per_rank_emulation (each N-GPU rank's
+shard sum timed on this GPU, emulated: true).
 """
 from __future__ import annotations
 
@@ -113,6 +114,8 @@ def parse(argv=None):
     p.add_argument("--rowops-index", nargs="*", default=["random", "identity"],
                    choices=["random", "identity"], help="DoubleIndex kinds of the row-op legs")
     p.add_argument("--no-config2", action="store_true")
+    p.add_argument("--no-per-rank", action="store_true",
+                   help="skip the one-GPU emulation of the N-GPU runs' per-rank work")
     p.add_argument("--no-e2e", action="store_true",
                    help="skip the libgeeps end-to-end clock leg")
     p.add_argument("--no-hbm-probe", action="store_true")
@@ -619,6 +622,31 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
     return out
 
 
+def per_rank_leg(deltas, master, rows, W, dev, ranks=(2, 4, 8), reps=10):
+    """The per-rank work of the N-GPU runs, timed on this one GPU (emulated:
+    true): at N GPUs each rank sums the 8 client buckets into a shard of
+    rows / N rows (the exchange that moved them there is not in the step).
+    Here the shard is the leading rows / N rows of the resident buckets and
+    master, so no new allocation; `predicted_speedup` = the N = 1 step time
+    (this run's headline kernel time) / the rank's time.  DESIGN.md §7."""
+    from geeps_amd import rowops
+    stream = torch.cuda.current_stream()
+    out = {}
+    for N in ranks:
+        n = (rows // N) * W
+        bk = [d[:n] for d in deltas]
+        m = master[:n]
+        avg = _time_calls(lambda: rowops.bucket_sum_apply(m, bk), reps, stream)
+        plan = sum_launch_plan(n, len(bk))
+        gbps = (len(bk) + 2) * n * 4 / (avg / 1e3) / 1e9
+        out[str(N)] = {"shard_rows": rows // N, "ms": round(avg, 4), "frac": round(gbps / HBM_PEAK_GBPS, 4),
+                       "kernel_id": plan["kernel_id"], "launches": plan["launches"],
+                       "other_launches": plan["other_launches"]}
+    return {"emulated": True, "ranks": out,
+            "note": "one rank's shard sum at N GPUs, on this GPU; the driver's N-GPU runs measure "
+                    "the real thing"}
+
+
 def config2_leg(deltas, master, dev, probe=None, reps=5):
     """BASELINE configs[1]: the same 1M x 1024 shard, 2 client buckets (the
     first two resident deltas, client order 0, 1) summed into the master by one
@@ -708,6 +736,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
     probe = None
     config2 = None
     e2e = None
+    per_rank = None
     if rank == 0 and world == 1 and dev.type == "cuda":
         if not args.no_hbm_probe:
             log("[rank 0] HBM probes")
@@ -717,6 +746,11 @@ def main(argv=None, backend="nccl", apply_fn=None):
         if not args.no_config2 and C >= 2 and master is not None:
             log("[rank 0] configs[1] leg (2 clients)")
             config2 = config2_leg(deltas, master, dev, probe)
+        if not args.no_per_rank and master is not None:
+            log("[rank 0] per-rank (emulated N-GPU) leg")
+            per_rank = per_rank_leg(deltas, master, R, W, dev)
+            for v in per_rank["ranks"].values():
+                v["predicted_speedup"] = round(avg_kernel_ms / v["ms"], 3)
         del deltas
         red = None
         master = None
@@ -797,6 +831,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
             line["hbm_probe"] = probe
         if config2:
             line["config2"] = config2
+        if per_rank:
+            line["per_rank_emulation"] = per_rank
         if host_inc:
             line["host_inclusive"] = host_inc
         if rowops_res:
