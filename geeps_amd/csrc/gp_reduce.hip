@@ -11,16 +11,24 @@
 //    per element per client); here one pass reads master + N buckets once and
 //    writes master once, summing in bucket order so every element is
 //    bit-identical to the sequential form.  Shards of 4 MiB and up use the
-//    phase-separated form (reads of a chunk summed into LDS and registers,
-//    then written), smaller ones and leftovers the mixed dwordx4 form, then a
-//    scalar tail.
+//    phase-separated forms (reads of a chunk summed into LDS and registers,
+//    then written): whole 96-MiB / 64-MiB chunks by the stream-by-stream
+//    sweep, the rest tile-major; smaller ones and leftovers the mixed dwordx4
+//    form, then a scalar tail.  NB = 0 is a plain copy and the zero-input
+//    (ZIN) form computes 0.0f + b0: the row plans' dense runs (below).
 //
-//  * row_op_kernel — the row-indexed scatter-add / gather / scatter-assign
-//    over a DoubleIndex (reference: src/common/row-op-util.cu:39-142).  The
-//    reference launches one thread per ELEMENT with a 64-bit div/mod and a
-//    16-B index load per element; here a group of LPR lanes owns a row, the
-//    row's index is loaded once per row, and each lane moves 16 B per access
-//    (dwordx4), RPG rows per group in flight.
+//  * row_op_kernel / row_wave_kernel — the row-indexed scatter-add / gather /
+//    scatter-assign over a DoubleIndex (reference: src/common/row-op-util.cu:
+//    39-142).  The reference launches one thread per ELEMENT with a 64-bit
+//    div/mod and a 16-B index load per element; here a group of LPR lanes
+//    owns a row, the row's index is loaded once per row (or once per wave and
+//    shared by __shfl), and each lane moves 16 B per access (dwordx4), RPG
+//    rows per group in flight.
+//
+//  * row plans — a fixed DoubleIndex compiled once (libgeeps' ops): dense
+//    id0/id1 runs go to the bucket-sum kernels above (1 bucket for the
+//    scatter-add, ZIN for the fused init, NB = 0 for the gather), the other
+//    rows to the row kernels in destination order.
 //
 // Wave64 throughout: 256-thread workgroups = 4 waves, one per SIMD.
 
