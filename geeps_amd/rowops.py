@@ -274,7 +274,10 @@ class RowPlan:
         if self.y_need > rows_y.numel():
             raise ValueError("destination row out of range for rows_y")
         if self.num_rows:
-            _validate_segment_rows(torch.as_tensor(self._src_rows, device=rows_y.device), ranges)
+            src = getattr(self, "_src_rows_dev", None)
+            if src is None or src.device != rows_y.device:  # copied to the device once
+                src = self._src_rows_dev = torch.as_tensor(self._src_rows, device=rows_y.device)
+            _validate_segment_rows(src, ranges)
         check(native.lib().gp_gather_rows_segmented_planned(rows_y.data_ptr(), ctypes.byref(t), self._h,
                                                             _stream_ptr(stream)),
               "gp_gather_rows_segmented_planned")
