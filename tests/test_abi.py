@@ -342,3 +342,25 @@ def test_launch_plans_stable_while_device_is_set_concurrently():
         t.join()
     assert not bad
     assert want[cases[0]][2] > 0  # the 4-GiB 8-way shard takes sweep chunks
+
+
+def test_c_abi_consumer_builds_as_c99(tmp_path):
+    """include/gp_reduce.h is a plain C header: tests/apps/c_abi_check.c, a C99
+    consumer of the C-ABI, compiles with -pedantic -Werror and links against the
+    product library with gcc (no HIP or C++ types needed).  Run without a GPU it
+    exercises the error convention (GP_ERR_INVALID + gp_last_error) from C, then
+    stops at the device count; tests/test_gpu_parity.py runs it whole."""
+    exe = tmp_path / "c_abi_check"
+    oracle_dir = os.path.join(REPO, "oracle", "build")
+    subprocess.run(["gcc", "-std=c99", "-pedantic", "-Wall", "-Wextra", "-Werror", "-O2",
+                    "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "apps", "c_abi_check.c"), "-o", str(exe),
+                    "-L", os.path.dirname(native.LIB_PATH), "-lgp_reduce", "-L", oracle_dir, "-loracle",
+                    f"-Wl,-rpath,{os.path.dirname(native.LIB_PATH)}:{oracle_dir}",
+                    "-Wl,-rpath-link,/opt/rocm/lib"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert "error convention: GP_ERR_INVALID + gp_last_error() ok" in r.stdout, r.stdout + r.stderr
+    if r.returncode != 0:  # no GPU here: the device count fails loudly, nothing falls back
+        assert r.returncode == 1 and "gp_device_count" in r.stderr, r.stdout + r.stderr
+    else:
+        assert "c_abi_check ok" in r.stdout

@@ -924,3 +924,21 @@ def test_bucket_sum_sweep_then_small_leftover(dev, N, out_of_place):
         out = m
     torch.cuda.synchronize()
     assert np.array_equal(bits(out.cpu().numpy()), bits(e))
+
+
+def test_c_abi_consumer_on_gpu(dev):
+    """tests/apps/c_abi_check.c — a plain C99 program calling the C-ABI (built by
+    __graft_entry__.build() with gcc): the 8-way bucket sum, the scatter-add
+    (op order and row plan), the fused init and the gather (flat and planned),
+    each bit-exact against the oracle, from C with no torch or HIP type."""
+    import os
+    import subprocess
+    from conftest import REPO
+    exe = os.path.join(REPO, "build", "tests", "c_abi_check")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    torch.cuda.synchronize()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "c_abi_check ok" in r.stdout, r.stdout + r.stderr
+    for what in ("gp_bucket_sum_apply 8 buckets", "gp_scatter_add_rows", "gp_scatter_add_rows_planned",
+                 "gp_scatter_init_rows_planned", "gp_gather_rows", "gp_gather_rows_planned"):
+        assert f"{what}: " in r.stdout and "bit-exact" in r.stdout
