@@ -1,0 +1,282 @@
+// big_tune.hip — bigger sweep chunks with shallower bursts, and a sweep whose
+// last pass stores each tile as soon as it is summed (tuning harness, not
+// product code; it #includes the product kernels).  Production (round 2): 96-MiB
+// chunks = 10 LDS + 14 register tiles per block, bursts of 8 tiles.  Each
+// launch pays a few us of ramp and drain (persist_tune.hip); larger chunks pay
+// it fewer times: 18 register tiles (112 MiB) with bursts of 4 or 7, 16 (104
+// MiB) with bursts of 2, against production at 1, 2 and 8 buckets, on whole
+// chunks (bytes priced on the covered part), bit-checking every covered float.
+// "fused last" writes each tile out in the last stream's pass instead of a
+// separate write phase.  Pass 1 (profiles/r02/tune/big_tune.txt): 104 MiB with
+// bursts of 2 ran +2-3 % at 8 buckets; fused last lost 5-12 %.  Pass 2 (this
+// version) separates burst depth from chunk size: bursts of 1-8 at 96-120 MiB
+// (profiles/r02/tune/big_tune2.txt): bursts of 2 at 96 MiB ran +2.3-3.5 % at 8
+// buckets.  Pass 3 (this version): bursts of 1-3 at 64-96 MiB and 1-8 buckets,
+// and the zero-input form (label NB0: out = 0.0f + b0, 2 streams)
+// (profiles/r02/tune/big_tune3.txt): bursts of 2 +1.3-3.0 % at 3-8 buckets, tie
+// at 2, -1 % at 1 and for the zero-input form.  Pass 4 (this version): the
+// write phase throttled to WT stores in flight per wave (s_waitcnt vmcnt(WT)
+// after each tile), since the read side gained from a narrower address window.
+// Usage: big_tune [rounds] [arenas]
+#include "../../geeps_amd/csrc/gp_reduce.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                           \
+  do {                                                                                  \
+    hipError_t e = (x);                                                                 \
+    if (e != hipSuccess) {                                                              \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      std::exit(2);                                                                     \
+    }                                                                                   \
+  } while (0)
+
+constexpr size_t kN = (1ull << 20) * 1024;  // floats per buffer (4 GiB)
+
+
+// The production sweep body with a zero-input option: ZIN sums out = 0.0f +
+// b0 (+ b1 ...) (pass 0 adds its loads to +0.0f, so -0 -> +0 as after the
+// memset the planned init replaces); otherwise out = in + b0 + ...
+// vmcnt(N) alone (expcnt / lgkmcnt at their maxima: no wait on them)
+constexpr int vmcnt_imm(int n) { return (n & 0xF) | (((n >> 4) & 3) << 14) | 0x70 | 0xF00; }
+
+template <int NB, int RT, int TG, bool ZIN, bool FL = false, int WT = 0>
+__global__ __launch_bounds__(kBlock) void sweep_lb(f4 *__restrict__ out, const f4 *__restrict__ in,
+                                                   BucketPtrs b, size_t n4_tiles, size_t chunk) {
+  constexpr int U = kPhaseU;
+  constexpr int kT = kPhaseLdsTiles + RT;
+  constexpr int S = ZIN ? NB : NB + 1;  // streams
+  static_assert(kT % TG == 0, "whole bursts");
+  __shared__ f4 res[kPhaseLdsF4];
+  f4 keep[RT > 0 ? RT : 1][U];
+  const f4 *src[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+    src[k] = (!ZIN && k == 0) ? in : reinterpret_cast<const f4 *>(b.p[ZIN ? k : k - 1]);
+  const size_t G = gridDim.x;
+  const size_t lo = chunk * G * (size_t)kT * kPhaseTile;
+  if (lo >= n4_tiles) return;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+#pragma unroll
+    for (int t0 = 0; t0 < kT; t0 += TG) {
+      f4 v[TG][U];
+#pragma unroll
+      for (int j = 0; j < TG; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[j][u] = ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kPhaseTile +
+                              threadIdx.x + u * kBlock);
+#pragma unroll
+      for (int j = 0; j < TG; ++j) {
+        const int t = t0 + j;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const f4 first = ZIN ? f4(0.0f) + v[j][u] : v[j][u];
+          if (FL && k == S - 1) {  // last pass: straight out
+            const f4 s = k == 0 ? first
+                                : (t < kPhaseLdsTiles ? res[t * kPhaseTile + u * kBlock + threadIdx.x]
+                                                      : keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u]) +
+                                      v[j][u];
+            __builtin_nontemporal_store(s, out + lo + ((size_t)t * G + blockIdx.x) * kPhaseTile +
+                                               threadIdx.x + u * kBlock);
+          } else if (t < kPhaseLdsTiles) {
+            f4 &r = res[t * kPhaseTile + u * kBlock + threadIdx.x];
+            r = k == 0 ? first : r + v[j][u];
+          } else {
+            f4 &r = keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u];
+            r = k == 0 ? first : r + v[j][u];
+          }
+        }
+      }
+    }
+  }
+  if (FL) return;
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kT; ++t) {
+    const size_t base = lo + ((size_t)t * G + blockIdx.x) * kPhaseTile + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      __builtin_nontemporal_store(t < kPhaseLdsTiles ? res[t * kPhaseTile + u * kBlock + threadIdx.x]
+                                                     : keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u],
+                                  out + base + u * kBlock);
+    if (WT > 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(WT));  // at most WT stores in flight
+  }
+}
+
+template <int NB, int RT, int TG, bool ZIN, bool FL = false, int WT = 0>
+size_t launch_lb(float *out, const float *in, const BucketPtrs &b, bool run) {
+  const size_t n4 = kN / 4;
+  const size_t G = (size_t)num_cus();
+  const size_t chunk_f4 = G * (size_t)(kPhaseLdsTiles + RT) * kPhaseTile;
+  const size_t chunks = n4 / chunk_f4;
+  if (run)
+    for (size_t c = 0; c < chunks; ++c)
+      hipLaunchKernelGGL((sweep_lb<NB, RT, TG, ZIN, FL, WT>), dim3((unsigned)G), dim3(kBlock), 0, 0,
+                         reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b, n4, c);
+  return chunks * chunk_f4 * 4;
+}
+
+template <int NB, int RT, int TG, bool ZIN, bool FL = false>
+void report(const char *name) {
+  hipFuncAttributes a;
+  CK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&sweep_lb<NB, RT, TG, ZIN, FL>)));
+  std::printf("%-22s regs %d  scratch %zu B/lane\n", name, a.numRegs, a.localSizeBytes);
+}
+
+__global__ void fill_k(float *p, size_t n, unsigned seed) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    unsigned x = (unsigned)(i * 2654435761u) ^ seed;
+    x ^= x >> 13;
+    x *= 0x5bd1e995u;
+    x ^= x >> 15;
+    p[i] = (float)(x & 0xffffff) / 16777216.0f - 0.5f;
+  }
+}
+
+__global__ void diff_k(const unsigned *a, const unsigned *b, size_t n, unsigned long long *bad) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  unsigned long long c = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) c += a[i] != b[i];
+  if (c) atomicAdd(bad, c);
+}
+
+int main(int argc, char **argv) {
+  const int rounds = argc > 1 ? std::atoi(argv[1]) : 5;
+  const int n_arenas = argc > 2 ? std::atoi(argv[2]) : 2;
+  struct Set {
+    std::string name;
+    BucketPtrs b;
+    float *master;
+  };
+  std::vector<Set> sets;
+  for (int i = 0; i < n_arenas; ++i) {
+    char *a = nullptr;
+    const size_t stride = kN * 4;
+    CK(hipMalloc(&a, 9 * stride));
+    Set s{"arena #" + std::to_string(i + 1), {}, nullptr};
+    for (int k = 0; k < 8; ++k) {
+      s.b.p[k] = reinterpret_cast<const float *>(a + (size_t)k * stride);
+      fill_k<<<4096, 256>>>(reinterpret_cast<float *>(a + (size_t)k * stride), kN, 1000 + k);
+    }
+    s.master = reinterpret_cast<float *>(a + (size_t)8 * stride);
+    fill_k<<<4096, 256>>>(s.master, kN, 77);
+    sets.push_back(s);
+  }
+  CK(hipDeviceSynchronize());
+  report<8, 14, 2, false>("add8 RT14 TG2");
+  struct V {
+    std::string name;
+    int nb;
+    std::function<size_t(float *, const BucketPtrs &, bool)> run;
+  };
+  auto prod_sum = [](int nb) {
+    return [nb](float *m, const BucketPtrs &b, bool run) {
+      std::vector<const float *> bv(b.p, b.p + nb);
+      if (run) gp_bucket_sum_apply(m, bv.data(), nb, kN, nullptr);
+      return kN;
+    };
+  };
+#define LB(NB, RT, TG, FL) [](float *m, const BucketPtrs &b, bool r) { return launch_lb<NB, RT, TG, false, FL>(m, m, b, r); }
+  auto prod_zin = [](float *m, const BucketPtrs &b, bool run) {
+    if (run) launch_bucket_sum_nb<1, true>(m, nullptr, b, kN, nullptr);
+    return kN;
+  };
+#define LBW(NB, RT, TG, WT) [](float *m, const BucketPtrs &b, bool r) { return launch_lb<NB, RT, TG, false, false, WT>(m, m, b, r); }
+#define LBZ(RT, TG, WT) [](float *m, const BucketPtrs &b, bool r) { return launch_lb<1, RT, TG, true, false, WT>(m, m, b, r); }
+  std::vector<V> kinds = {
+      {"prod (RT14 TG8 + 64 MiB)", 8, prod_sum(8)},
+      {"sweep RT14 TG8 (96 MiB)", 8, LBW(8, 14, 8, 0)},
+      {"sweep RT14 TG2", 8, LBW(8, 14, 2, 0)},
+      {"sweep RT14 TG2 WT4", 8, LBW(8, 14, 2, 4)},
+      {"sweep RT14 TG2 WT8", 8, LBW(8, 14, 2, 8)},
+      {"sweep RT14 TG2 WT16", 8, LBW(8, 14, 2, 16)},
+      {"prod (RT14 TG8 + tile-major)", 2, prod_sum(2)},
+      {"sweep RT14 TG8", 2, LBW(2, 14, 8, 0)},
+      {"sweep RT14 TG8 WT8", 2, LBW(2, 14, 8, 8)},
+      {"sweep RT14 TG2 WT8", 2, LBW(2, 14, 2, 8)},
+      {"prod (RT14 TG8 + tile-major)", 1, prod_sum(1)},
+      {"sweep RT14 TG8", 1, LBW(1, 14, 8, 0)},
+      {"sweep RT14 TG8 WT8", 1, LBW(1, 14, 8, 8)},
+      {"sweep RT14 TG8 WT4", 1, LBW(1, 14, 8, 4)},
+      {"prod ZIN (RT6 TG4, 64 MiB)", 0, prod_zin},
+      {"ZIN RT6 TG4 WT8", 0, LBZ(6, 4, 8)},
+      {"ZIN RT6 TG4 WT4", 0, LBZ(6, 4, 4)},
+  };
+#undef LBW
+#undef LBZ
+#undef LB
+  {
+    const Set &s = sets[0];
+    float *ref = nullptr, *m2 = nullptr;
+    unsigned long long *bad = nullptr;
+    CK(hipMalloc(&ref, kN * 4));
+    CK(hipMalloc(&m2, kN * 4));
+    CK(hipMalloc(&bad, 8));
+    for (auto &v : kinds) {
+      if (v.name.rfind("prod", 0) == 0) {
+        CK(hipMemcpy(ref, s.master, kN * 4, hipMemcpyDeviceToDevice));
+        v.run(ref, s.b, true);
+        continue;
+      }
+      CK(hipMemcpy(m2, s.master, kN * 4, hipMemcpyDeviceToDevice));
+      const size_t covered = v.run(m2, s.b, true);
+      CK(hipMemset(bad, 0, 8));
+      diff_k<<<4096, 256>>>(reinterpret_cast<const unsigned *>(ref), reinterpret_cast<const unsigned *>(m2),
+                            covered, bad);
+      unsigned long long hb = 0;
+      CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+      std::printf("NB%d %-26s vs prod, %zu covered floats: %llu mismatches\n", v.nb, v.name.c_str(),
+                  covered, hb);
+    }
+    CK(hipFree(ref));
+    CK(hipFree(m2));
+    CK(hipFree(bad));
+  }
+  struct R {
+    std::string name;
+    std::function<void()> run;
+    double bytes;
+    std::vector<float> ms;
+  };
+  std::vector<R> rs;
+  for (auto &s : sets)
+    for (auto &v : kinds) {
+      float *m = s.master;
+      BucketPtrs bp = s.b;
+      auto f = v.run;
+      const size_t covered = f(m, bp, false);
+      rs.push_back(R{s.name + " NB" + std::to_string(v.nb) + " " + v.name, [=]() { f(m, bp, true); },
+                     (v.nb == 0 ? 2.0 : v.nb + 2.0) * covered * 4, {}});
+    }
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (auto &r : rs) r.run();
+  CK(hipDeviceSynchronize());
+  for (int k = 0; k < rounds; ++k)
+    for (auto &r : rs) {
+      CK(hipEventRecord(a));
+      r.run();
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      r.ms.push_back(ms);
+    }
+  std::printf("%-46s %10s %10s %10s %8s\n", "arena / kernel", "med_ms", "min_ms", "GB/s", "frac8T");
+  for (auto &r : rs) {
+    std::sort(r.ms.begin(), r.ms.end());
+    const double med = r.ms[r.ms.size() / 2];
+    const double gbs = r.bytes / (med * 1e-3) / 1e9;
+    std::printf("%-46s %10.4f %10.4f %10.1f %8.4f\n", r.name.c_str(), med, r.ms[0], gbs, gbs / 8000.0);
+  }
+  return 0;
+}
