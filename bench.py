@@ -59,15 +59,16 @@ def sum_launch_plan(num_vals: int, num_buckets: int) -> dict:
     """The dominant kernel of one N-way sum of num_vals floats and how many
     launches of it one sum issues, from the library's own launch plan
     (gp_bucket_sum_launch_plan).  Shards of at least 3 whole 96-MiB chunks go
-    to bucket_sum_sweep_kernel<NB, 14, 8> (the 4 GiB headline shard: 42 of
-    them), then whole 64-MiB chunks to bucket_sum_sweep_kernel<NB, 6, 4> (the
+    to bucket_sum_sweep_kernel<NB, 14, TG> (TG = 2 at 3-8 buckets, 8 at 1-2;
+    the 4 GiB headline shard: 42 of them), then whole 64-MiB chunks to
+    bucket_sum_sweep_kernel<NB, 6, 4> (the
     4 GiB shard: 1), the rest to the tile-major bucket_sum_phased_kernel and
     the mixed / scalar forms; smaller shards start at the 64-MiB sweep or the
     phased kernel.  `launches` counts the dominant kernel only and `share` is
     its part of the shard, so a per-launch time or byte figure (call time x
     share / launches) compares with rocprofv3's average for that kernel;
-    `kernel_id` names the instantiation (as rocprofv3 prints it, up to the
-    burst depth)."""
+    `kernel_id` names the instantiation as rocprofv3 prints it (buckets,
+    register tiles, burst depth)."""
     import ctypes
     from geeps_amd import native
     p = native.SumPlan()
@@ -75,17 +76,18 @@ def sum_launch_plan(num_vals: int, num_buckets: int) -> dict:
                  "gp_bucket_sum_launch_plan")
     cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
     tile_floats = cus * 16384 // 4  # one 16-KiB tile per CU
-    forms = [("bucket_sum_sweep_kernel", p.sweep_launches, p.sweep_reg_tiles),
-             ("bucket_sum_sweep_kernel", p.small_sweep_launches, 6),
-             ("bucket_sum_phased_kernel", p.phased_launches, p.phased_reg_tiles)]
+    forms = [("bucket_sum_sweep_kernel", p.sweep_launches, p.sweep_reg_tiles, p.sweep_burst_tiles),
+             ("bucket_sum_sweep_kernel", p.small_sweep_launches, 6, p.small_sweep_burst_tiles),
+             ("bucket_sum_phased_kernel", p.phased_launches, p.phased_reg_tiles, None)]
     total = p.sweep_launches + p.small_sweep_launches + p.phased_launches + p.other_launches
-    for kernel, n, rt in forms:
+    for kernel, n, rt, tg in forms:
         if n > 0:
             share = 1.0
             if kernel == "bucket_sum_sweep_kernel":
                 share = min(1.0, n * (10 + rt) * tile_floats / num_vals)
-            return {"kernel": kernel, "kernel_id": f"{kernel}<{num_buckets}, {rt},", "launches": n,
-                    "other_launches": total - n, "reg_tiles": rt, "share": share}
+            kid = f"{kernel}<{num_buckets}, {rt}, {tg}," if tg else f"{kernel}<{num_buckets}, {rt},"
+            return {"kernel": kernel, "kernel_id": kid, "launches": n,
+                    "other_launches": total - n, "reg_tiles": rt, "burst_tiles": tg, "share": share}
     return {"kernel": "bucket_sum_vec_kernel", "kernel_id": f"bucket_sum_vec_kernel<{num_buckets},",
             "launches": 1, "other_launches": total - 1, "reg_tiles": None, "share": 1.0}
 

@@ -351,11 +351,22 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
 // against the tile-major form's 78.6-79.4 %, so there the rest goes straight
 // to tile-major).  Whole chunks only (no guards: the waitcnt counts stay
 // exact).  The zero-input form has one shape, 64-MiB chunks.
+// Burst depth (round 2, scripts/tune/big_tune.hip, profiles/r02/tune/
+// big_tune{2,3,4}.txt: 4 boxes x 3 arenas): at 3-8 buckets, bursts of 2 tiles
+// ran +2.3-3.5 % per byte at 8 buckets (6.11-6.14 ms against 6.28-6.36 ms for
+// the 96-MiB chunks, 86.1-86.5 % of 8 TB/s) and +1.3-1.9 % at 3-4.  The assembly
+// keeps one burst (8 loads) in flight per wave, so the chip has ~8 MiB of one
+// stream in flight instead of ~32 MiB: the HBM row buffers see a narrower
+// address window.  Bursts of 1 (4 loads) starve the pipe (-14 %), of 3 sit in
+// between.  At 1-2 buckets and in the zero-input form, whose write phase is a
+// larger part of the chunk, bursts of 2 tied or lost 1 % and bursts of 8 stay.
+// Capping the write phase's stores in flight (s_waitcnt vmcnt(4-16) per tile)
+// changed nothing at any bucket count.
 template <int NB, bool ZIN>
 struct SweepShape {  // register tiles, tiles per burst of loads: the big chunks
   // one stream (the zero-input form, the NB = 0 copy): 64-MiB chunks, bursts of 4
   static constexpr int RT = (ZIN || NB == 0) ? 6 : 14;
-  static constexpr int TG = (ZIN || NB == 0) ? 4 : 8;
+  static constexpr int TG = (ZIN || NB == 0) ? 4 : (NB >= 3 ? 2 : 8);
 };
 constexpr int kSweepRT = 6;  // the small (64-MiB) chunks and the zero-input form
 constexpr int kSweepTG = 4;
@@ -585,7 +596,9 @@ void sum_plan_nb(size_t n, gp_sum_plan *out) {
   const SumLaunches l = sum_launches<NB>(n);
   out->sweep_launches = (int)l.sweep;
   out->sweep_reg_tiles = l.sweep ? SweepShape<NB, false>::RT : -1;
+  out->sweep_burst_tiles = l.sweep ? SweepShape<NB, false>::TG : -1;
   out->small_sweep_launches = (int)l.sweep_small;
+  out->small_sweep_burst_tiles = l.sweep_small ? kSweepTG : -1;
   out->phased_launches = (int)l.phased;
   out->phased_reg_tiles = l.phased_reg_tiles;
   out->other_launches = (int)l.other;

@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 8  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 9  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -50,7 +50,8 @@ class SumPlan(ctypes.Structure):
     _fields_ = [("sweep_launches", ctypes.c_int), ("sweep_reg_tiles", ctypes.c_int),
                 ("small_sweep_launches", ctypes.c_int),
                 ("phased_launches", ctypes.c_int), ("phased_reg_tiles", ctypes.c_int),
-                ("other_launches", ctypes.c_int)]
+                ("other_launches", ctypes.c_int),
+                ("sweep_burst_tiles", ctypes.c_int), ("small_sweep_burst_tiles", ctypes.c_int)]
 
 
 _c = ctypes

@@ -41,7 +41,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 8
+#define GP_ABI_VERSION 9
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -265,18 +265,24 @@ int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launc
 /* Every launch of one pass of num_buckets (1..8) over num_vals floats in
  * 16-B-aligned buffers, by kernel form, in launch order; launches nothing:
  *   sweep_launches       the stream-by-stream kernel's big chunks (96 MiB on
- *                        256 CUs: 14 register tiles beside the 10 LDS ones),
- *   small_sweep_launches then its 64-MiB chunks (6 register tiles),
+ *                        256 CUs: 14 register tiles beside the 10 LDS ones;
+ *                        sweep_burst_tiles: tiles per burst of loads, 2 at
+ *                        3-8 buckets, 8 at 1-2),
+ *   small_sweep_launches then its 64-MiB chunks (6 register tiles, bursts of
+ *                        small_sweep_burst_tiles = 4),
  *   phased_launches      then the tile-major phase-separated form
  *                        (phased_reg_tiles: 20 at 1-2 buckets, 12 at 3-4, 4 at 5-8),
  *   other_launches       then the mixed dwordx4 and scalar forms (0-2).
- * A reg_tiles field is -1 when its form has no launch.  For measurement
- * tools: bench.py prices each kernel per launch, as rocprofv3 reports it. */
+ * A reg_tiles / burst_tiles field is -1 when its form has no launch.  For
+ * measurement tools: bench.py names and prices each kernel instantiation per
+ * launch (bucket_sum_sweep_kernel<NB, reg_tiles, burst_tiles, ...>), as
+ * rocprofv3 reports it. */
 typedef struct gp_sum_plan {
   int sweep_launches, sweep_reg_tiles;
   int small_sweep_launches;
   int phased_launches, phased_reg_tiles;
   int other_launches;
+  int sweep_burst_tiles, small_sweep_burst_tiles; /* ABI 9 */
 } gp_sum_plan;
 int gp_bucket_sum_launch_plan(size_t num_vals, int num_buckets, gp_sum_plan *plan);
 

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 8
+    assert L.gp_abi_version() == native.ABI_VERSION == 9
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -167,6 +167,10 @@ def test_bucket_sum_plan_without_device():
     assert L.gp_bucket_sum_launch_plan(1 << 30, 8, ctypes.byref(sp)) == 0
     assert (sp.sweep_launches, sp.sweep_reg_tiles, sp.small_sweep_launches, sp.phased_launches,
             sp.phased_reg_tiles, sp.other_launches) == (42, 14, 1, 0, -1, 0)
+    assert (sp.sweep_burst_tiles, sp.small_sweep_burst_tiles) == (2, 4)  # 3-8 buckets: bursts of 2
+    assert L.gp_bucket_sum_launch_plan(1 << 30, 2, ctypes.byref(sp)) == 0
+    assert (sp.sweep_launches, sp.sweep_reg_tiles, sp.sweep_burst_tiles, sp.small_sweep_launches,
+            sp.small_sweep_burst_tiles) == (42, 14, 8, 0, -1)  # 1-2 buckets: bursts of 8, no 64-MiB chunks
     n = (1 << 27) + 4 + 3  # 512 MiB + one dwordx4 + 3 floats
     assert L.gp_bucket_sum_launch_plan(n, 5, ctypes.byref(sp)) == 0
     assert (sp.sweep_launches, sp.small_sweep_launches, sp.phased_launches, sp.phased_reg_tiles,

@@ -38,8 +38,8 @@ def _kernel(asm, pattern):
 # (buckets, register tiles, tiles per burst, zero-input): every production
 # instantiation (gp_reduce.hip: SweepShape's 96-MiB chunks, the 64-MiB
 # chunks after them, the zero-input form)
-SWEEP_SHAPES = ([(nb, 14, 8, 0) for nb in range(1, 9)] + [(nb, 6, 4, 0) for nb in range(3, 9)]
-                + [(1, 6, 4, 1)])
+SWEEP_SHAPES = ([(nb, 14, 8, 0) for nb in range(1, 3)] + [(nb, 14, 2, 0) for nb in range(3, 9)]
+                + [(nb, 6, 4, 0) for nb in range(3, 9)] + [(1, 6, 4, 1)])
 
 
 @pytest.mark.parametrize("nb,rt,tg,zin", SWEEP_SHAPES)
@@ -54,6 +54,10 @@ def test_sweep_kernel_keeps_burst_schedule(asm, nb, rt, tg, zin):
     # regressed schedule drained once per tile or more (117-224 at 8 buckets)
     bursts = streams * (10 + rt) // tg
     assert full_drains <= bursts, f"{full_drains} full vmcnt(0) drains: the burst schedule regressed"
+    # each burst's loads are issued together: some wait leaves the rest of a
+    # burst (4 * tg - 1 loads) in flight
+    counts = [int(n) for n in re.findall(r"s_waitcnt vmcnt\((\d+)\)", body)]
+    assert max(counts) >= 4 * tg - 1, f"at most {max(counts)} loads in flight: bursts split"
     assert "scratch_" not in body and "buffer_store_dword" not in body  # no spills
 
 
