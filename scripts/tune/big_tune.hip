@@ -16,7 +16,10 @@
 // (profiles/r02/tune/big_tune3.txt): bursts of 2 +1.3-3.0 % at 3-8 buckets, tie
 // at 2, -1 % at 1 and for the zero-input form.  Pass 4 (this version): the
 // write phase throttled to WT stores in flight per wave (s_waitcnt vmcnt(WT)
-// after each tile), since the read side gained from a narrower address window.
+// after each tile), since the read side gained from a narrower address window
+// (profiles/r02/tune/big_tune4.txt: no effect).  Pass 5 (this version): burst
+// depth and chunk size at 1-2 buckets, the zero-input form and the NB = 0 copy
+// (a gather plan's dense runs; out = b0 here, so the copy reads another buffer).
 // Usage: big_tune [rounds] [arenas]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -171,7 +174,10 @@ int main(int argc, char **argv) {
     sets.push_back(s);
   }
   CK(hipDeviceSynchronize());
-  report<8, 14, 2, false>("add8 RT14 TG2");
+  report<2, 14, 12, false>("add2 RT14 TG12");
+  report<1, 14, 12, false>("add1 RT14 TG12");
+  report<1, 6, 8, true>("zin1 RT6 TG8");
+  report<1, 6, 16, true>("zin1 RT6 TG16");
   struct V {
     std::string name;
     int nb;
@@ -191,25 +197,31 @@ int main(int argc, char **argv) {
   };
 #define LBW(NB, RT, TG, WT) [](float *m, const BucketPtrs &b, bool r) { return launch_lb<NB, RT, TG, false, false, WT>(m, m, b, r); }
 #define LBZ(RT, TG, WT) [](float *m, const BucketPtrs &b, bool r) { return launch_lb<1, RT, TG, true, false, WT>(m, m, b, r); }
+#define LB0(RT, TG) [](float *m, const BucketPtrs &b, bool r) { return launch_lb<0, RT, TG, false, false, 0>(m, b.p[0], b, r); }
+  auto prod_copy = [](float *m, const BucketPtrs &b, bool run) {
+    if (run) launch_bucket_sum_nb<0>(m, b.p[0], b, kN, nullptr);
+    return kN;
+  };
   std::vector<V> kinds = {
-      {"prod (RT14 TG8 + 64 MiB)", 8, prod_sum(8)},
-      {"sweep RT14 TG8 (96 MiB)", 8, LBW(8, 14, 8, 0)},
-      {"sweep RT14 TG2", 8, LBW(8, 14, 2, 0)},
-      {"sweep RT14 TG2 WT4", 8, LBW(8, 14, 2, 4)},
-      {"sweep RT14 TG2 WT8", 8, LBW(8, 14, 2, 8)},
-      {"sweep RT14 TG2 WT16", 8, LBW(8, 14, 2, 16)},
       {"prod (RT14 TG8 + tile-major)", 2, prod_sum(2)},
       {"sweep RT14 TG8", 2, LBW(2, 14, 8, 0)},
-      {"sweep RT14 TG8 WT8", 2, LBW(2, 14, 8, 8)},
-      {"sweep RT14 TG2 WT8", 2, LBW(2, 14, 2, 8)},
+      {"sweep RT14 TG6", 2, LBW(2, 14, 6, 0)},
+      {"sweep RT14 TG12", 2, LBW(2, 14, 12, 0)},
+      {"sweep RT10 TG4 (80 MiB)", 2, LBW(2, 10, 4, 0)},
       {"prod (RT14 TG8 + tile-major)", 1, prod_sum(1)},
       {"sweep RT14 TG8", 1, LBW(1, 14, 8, 0)},
-      {"sweep RT14 TG8 WT8", 1, LBW(1, 14, 8, 8)},
-      {"sweep RT14 TG8 WT4", 1, LBW(1, 14, 8, 4)},
+      {"sweep RT14 TG6", 1, LBW(1, 14, 6, 0)},
+      {"sweep RT14 TG12", 1, LBW(1, 14, 12, 0)},
       {"prod ZIN (RT6 TG4, 64 MiB)", 0, prod_zin},
-      {"ZIN RT6 TG4 WT8", 0, LBZ(6, 4, 8)},
-      {"ZIN RT6 TG4 WT4", 0, LBZ(6, 4, 4)},
+      {"ZIN RT6 TG8", 0, LBZ(6, 8, 0)},
+      {"ZIN RT6 TG16", 0, LBZ(6, 16, 0)},
+      {"ZIN RT10 TG4 (80 MiB)", 0, LBZ(10, 4, 0)},
+      {"prod copy (RT6 TG4, 64 MiB)", 0, prod_copy},
+      {"copy RT6 TG2", 0, LB0(6, 2)},
+      {"copy RT6 TG8", 0, LB0(6, 8)},
+      {"copy RT14 TG8 (96 MiB)", 0, LB0(14, 8)},
   };
+#undef LB0
 #undef LBW
 #undef LBZ
 #undef LB
