@@ -1,0 +1,182 @@
+// wave_tune.hip — rows in flight for the wave-map row kernel on a row plan's
+// residual (tuning harness, not product code; it #includes the product
+// kernels).  The 8-way sweep sum gained 2-3.5 % from fewer loads in flight per
+// wave (bursts of 2 tiles: a narrower window of outstanding addresses,
+// big_tune.hip).  Here the same question for row_wave_kernel, which production
+// launches as one resident round of blocks (CUs x blocks resident per CU) with
+// 8 rows per 32-lane group in flight: 8 M rows of 128 floats, a random
+// permutation index in destination order (what a scatter plan's residual and
+// a gather plan's residual hold), scatter-add, fused init and gather, with 4 or
+// 8 rows per group and 1, 2 or the resident count of blocks per CU.  Each
+// variant is bit-checked against the production planned call.  Pass 1
+// (profiles/r02/tune/wave_tune.txt): the scatter forms want every resident
+// block (fewer lose 10-50 %); the gather ran +2.7 % at 2 blocks per CU against
+// production's 4.  Pass 2 (this version): the gather at 2-4 blocks per CU,
+// random and identity (the unplanned call's) indexes.
+// Usage: wave_tune [rounds]
+#include "../../geeps_amd/csrc/gp_reduce.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                           \
+  do {                                                                                  \
+    hipError_t e = (x);                                                                 \
+    if (e != hipSuccess) {                                                              \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      std::exit(2);                                                                     \
+    }                                                                                   \
+  } while (0)
+
+constexpr size_t R = 8u << 20, W = 128, N = R * W;
+
+__global__ void fill_k(float *p, size_t n, unsigned seed) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    unsigned v = (unsigned)(i * 2654435761u) ^ seed;
+    v ^= v >> 13;
+    v *= 0x5bd1e995u;
+    v ^= v >> 15;
+    p[i] = (float)(v & 0xffffff) / 16777216.0f - 0.5f;
+  }
+}
+
+__global__ void diff_k(const unsigned *a, const unsigned *b, size_t n, unsigned long long *bad) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  unsigned long long c = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) c += a[i] != b[i];
+  if (c) atomicAdd(bad, c);
+}
+
+template <int OP, int RPG>
+int occupancy() {
+  int occ = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &occ, reinterpret_cast<const void *>(&row_wave_kernel<f4, OP, 32, RPG, kFlat>), kBlock, 0));
+  return occ;
+}
+
+// y (+)= x / y = x over the sorted index: rows [0, R) through row_wave_kernel
+template <int OP, int RPG>
+void wave(float *y, const float *x, const gp_double_index *ix, int per_cu) {
+  const size_t grid = std::min((R + kBlock - 1) / kBlock, (size_t)num_cus() * per_cu);
+  const SegArg<kFlat> flat{};
+  hipLaunchKernelGGL((row_wave_kernel<f4, OP, 32, RPG, kFlat>), dim3((unsigned)grid), dim3(kBlock), 0, 0, y,
+                     x, ix, R, 0, 0, W, W / 4, ~size_t(0), flat);
+}
+
+int main(int argc, char **argv) {
+  const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
+  float *x, *y, *y0, *ref;
+  unsigned long long *bad;
+  CK(hipMalloc(&x, N * 4));
+  CK(hipMalloc(&y, N * 4));
+  CK(hipMalloc(&y0, N * 4));
+  CK(hipMalloc(&ref, N * 4));
+  CK(hipMalloc(&bad, 8));
+  fill_k<<<4096, 256>>>(x, N, 11);
+  fill_k<<<4096, 256>>>(y0, N, 22);
+  // random permutation: scatter index (id0 = op row, id1 = cache row) sorted by
+  // id1; gather index (id0 = op row, id1 = cache row) sorted by id0 (= op order)
+  std::vector<uint64_t> perm(R);
+  std::iota(perm.begin(), perm.end(), 0);
+  std::mt19937_64 rng(7);
+  std::shuffle(perm.begin(), perm.end(), rng);
+  std::vector<gp_double_index> sidx(R), gidx(R);
+  for (size_t r = 0; r < R; ++r) {
+    sidx[perm[r]] = gp_double_index{r, perm[r]};  // position perm[r]: ascending id1
+    gidx[r] = gp_double_index{r, perm[r]};
+  }
+  gp_double_index *ds, *dg;
+  CK(hipMalloc(&ds, R * 16));
+  CK(hipMalloc(&dg, R * 16));
+  CK(hipMemcpy(ds, sidx.data(), R * 16, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dg, gidx.data(), R * 16, hipMemcpyHostToDevice));
+  gp_double_index *di;  // identity
+  CK(hipMalloc(&di, R * 16));
+  for (size_t r = 0; r < R; ++r) gidx[r] = gp_double_index{r, r};
+  CK(hipMemcpy(di, gidx.data(), R * 16, hipMemcpyHostToDevice));
+  for (size_t r = 0; r < R; ++r) gidx[r] = gp_double_index{r, perm[r]};
+  gp_row_plan sp = nullptr, gp = nullptr;
+  CK(gp_row_plan_create(&sp, sidx.data(), R, gp_double_index{0, 0}, W, ~size_t(0)) == 0 ? hipSuccess
+                                                                                         : hipErrorUnknown);
+  CK(gp_gather_plan_create(&gp, gidx.data(), R, gp_double_index{0, 0}, W, ~size_t(0)) == 0
+         ? hipSuccess
+         : hipErrorUnknown);
+  std::printf("occupancy (blocks per CU): add R8 %d R4 %d, init R8 %d R4 %d, gather R8 %d R4 %d\n",
+              occupancy<kAddFrom, 8>(), occupancy<kAddFrom, 4>(), occupancy<kInitFrom, 8>(),
+              occupancy<kInitFrom, 4>(), occupancy<kAssignTo, 8>(), occupancy<kAssignTo, 4>());
+
+  struct V {
+    std::string name;
+    int op;  // 0 add, 3 init, 1 gather
+    std::function<void()> f;
+    double bytes;
+  };
+  const double add_b = 3.0 * N * 4, two_b = 2.0 * N * 4;
+  // gather: y[id0] = x[id1] -> x is the cache (read randomly), y the op buffer
+  std::vector<V> vs;
+  auto add_v = [&](const char *nm, std::function<void()> f) { vs.push_back({nm, 0, f, add_b}); };
+  auto ini_v = [&](const char *nm, std::function<void()> f) { vs.push_back({nm, 3, f, two_b}); };
+  auto gat_v = [&](const char *nm, std::function<void()> f) { vs.push_back({nm, 1, f, two_b}); };
+  gat_v("gath prod planned", [=] { gp_gather_rows_planned(y, x, gp, nullptr); });
+  gat_v("gath R8 /2", [=] { wave<kAssignTo, 8>(y, x, dg, 2); });
+  gat_v("gath R8 /3", [=] { wave<kAssignTo, 8>(y, x, dg, 3); });
+  gat_v("gath R8 /4", [=] { wave<kAssignTo, 8>(y, x, dg, 4); });
+  gat_v("gath prod unplanned", [=] { gp_gather_rows(y, x, dg, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  gat_v("gath ident prod unplanned", [=] { gp_gather_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  gat_v("gath ident R8 /2", [=] { wave<kAssignTo, 8>(y, x, di, 2); });
+  gat_v("gath ident R8 /3", [=] { wave<kAssignTo, 8>(y, x, di, 3); });
+  ini_v("init prod planned", [=] { gp_scatter_init_rows_planned(y, x, sp, nullptr); });
+  ini_v("init R8 /3", [=] { wave<kInitFrom, 8>(y, x, ds, 3); });
+  ini_v("init R8 /4", [=] { wave<kInitFrom, 8>(y, x, ds, 4); });
+  add_v("add  prod planned", [=] { gp_scatter_add_rows_planned(y, x, sp, nullptr); });
+  add_v("add  R8 /3", [=] { wave<kAddFrom, 8>(y, x, ds, 3); });
+  // bit check against the production planned call of the same op
+  for (size_t i = 0; i < vs.size(); ++i) {
+    CK(hipMemcpy(y, y0, N * 4, hipMemcpyDeviceToDevice));
+    vs[i].f();
+    CK(hipDeviceSynchronize());
+    if (vs[i].name.find("prod") != std::string::npos) {
+      CK(hipMemcpy(ref, y, N * 4, hipMemcpyDeviceToDevice));
+      continue;
+    }
+    CK(hipMemset(bad, 0, 8));
+    diff_k<<<4096, 256>>>(reinterpret_cast<const unsigned *>(ref), reinterpret_cast<const unsigned *>(y), N, bad);
+    unsigned long long hb = 0;
+    CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+    std::printf("%-22s vs prod: %llu mismatches\n", vs[i].name.c_str(), hb);
+  }
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  std::vector<std::vector<float>> ms(vs.size());
+  for (int r = 0; r < rounds; ++r)
+    for (size_t i = 0; i < vs.size(); ++i) {
+      CK(hipEventRecord(a, 0));
+      vs[i].f();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float t = 0;
+      CK(hipEventElapsedTime(&t, a, b));
+      ms[i].push_back(t);
+    }
+  CK(hipGetLastError());
+  std::printf("%-22s %9s %9s %9s %8s\n", "variant", "med_ms", "min_ms", "TB/s", "%8TB/s");
+  for (size_t i = 0; i < vs.size(); ++i) {
+    auto m = ms[i];
+    std::sort(m.begin(), m.end());
+    const double med = m[m.size() / 2];
+    const double tbs = vs[i].bytes / (med * 1e-3) / 1e12;
+    std::printf("%-22s %9.4f %9.4f %9.3f %7.1f%%\n", vs[i].name.c_str(), med, m[0], tbs, 100.0 * tbs / 8.0);
+  }
+  gp_row_plan_destroy(sp);
+  gp_row_plan_destroy(gp);
+  return 0;
+}
