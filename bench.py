@@ -59,8 +59,9 @@ def sum_launch_plan(num_vals: int, num_buckets: int) -> dict:
     """The dominant kernel of one N-way sum of num_vals floats and how many
     launches of it one sum issues, from the library's own launch plan
     (gp_bucket_sum_launch_plan).  Shards of at least 3 whole 96-MiB chunks go
-    to bucket_sum_sweep_kernel<NB, 14, TG> (TG = 2 at 3-8 buckets, 8 at 1-2;
-    the 4 GiB headline shard: 42 of them), then whole 64-MiB chunks to
+    to bucket_sum_sweep_kernel<NB, 7, 1, false, 8> at 2-8 buckets (7 register
+    tiles of 32 KiB, bursts of 1), <1, 14, 8, false, 4> at 1 (the 4 GiB
+    headline shard: 42 of them), then whole 64-MiB chunks to
     bucket_sum_sweep_kernel<NB, 6, 4> (the
     4 GiB shard: 1), the rest to the tile-major bucket_sum_phased_kernel and
     the mixed / scalar forms; smaller shards start at the 64-MiB sweep or the
@@ -75,16 +76,17 @@ def sum_launch_plan(num_vals: int, num_buckets: int) -> dict:
     native.check(native.lib().gp_bucket_sum_launch_plan(num_vals, num_buckets, ctypes.byref(p)),
                  "gp_bucket_sum_launch_plan")
     cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
-    tile_floats = cus * 16384 // 4  # one 16-KiB tile per CU
-    forms = [("bucket_sum_sweep_kernel", p.sweep_launches, p.sweep_reg_tiles, p.sweep_burst_tiles),
-             ("bucket_sum_sweep_kernel", p.small_sweep_launches, 6, p.small_sweep_burst_tiles),
-             ("bucket_sum_phased_kernel", p.phased_launches, p.phased_reg_tiles, None)]
+    # (kernel, launches, register tiles, tiles per burst, KiB per tile)
+    forms = [("bucket_sum_sweep_kernel", p.sweep_launches, p.sweep_reg_tiles, p.sweep_burst_tiles,
+              p.sweep_tile_kib),
+             ("bucket_sum_sweep_kernel", p.small_sweep_launches, 6, p.small_sweep_burst_tiles, 16),
+             ("bucket_sum_phased_kernel", p.phased_launches, p.phased_reg_tiles, None, 16)]
     total = p.sweep_launches + p.small_sweep_launches + p.phased_launches + p.other_launches
-    for kernel, n, rt, tg in forms:
+    for kernel, n, rt, tg, kib in forms:
         if n > 0:
             share = 1.0
-            if kernel == "bucket_sum_sweep_kernel":
-                share = min(1.0, n * (10 + rt) * tile_floats / num_vals)
+            if kernel == "bucket_sum_sweep_kernel":  # 160 KiB of LDS + rt register tiles per CU
+                share = min(1.0, n * (160 + rt * kib) * 1024 // 4 * cus / num_vals)
             kid = f"{kernel}<{num_buckets}, {rt}, {tg}," if tg else f"{kernel}<{num_buckets}, {rt},"
             return {"kernel": kernel, "kernel_id": kid, "launches": n,
                     "other_launches": total - n, "reg_tiles": rt, "burst_tiles": tg, "share": share}

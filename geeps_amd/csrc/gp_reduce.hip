@@ -351,35 +351,46 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
 // against the tile-major form's 78.6-79.4 %, so there the rest goes straight
 // to tile-major).  Whole chunks only (no guards: the waitcnt counts stay
 // exact).  The zero-input form has one shape, 64-MiB chunks.
-// Burst depth (round 2, scripts/tune/big_tune.hip, profiles/r02/tune/
-// big_tune{2,3,4}.txt: 4 boxes x 3 arenas): at 3-8 buckets, bursts of 2 tiles
-// ran +2.3-3.5 % per byte at 8 buckets (6.11-6.14 ms against 6.28-6.36 ms for
-// the 96-MiB chunks, 86.1-86.5 % of 8 TB/s) and +1.3-1.9 % at 3-4.  The assembly
-// keeps one burst (8 loads) in flight per wave, so the chip has ~8 MiB of one
-// stream in flight instead of ~32 MiB: the HBM row buffers see a narrower
-// address window.  Bursts of 1 (4 loads) starve the pipe (-14 %), of 3 sit in
-// between.  At 1-2 buckets and in the zero-input form, whose write phase is a
-// larger part of the chunk, bursts of 2 tied or lost 1 % and bursts of 8 stay.
-// Capping the write phase's stores in flight (s_waitcnt vmcnt(4-16) per tile)
-// changed nothing at any bucket count.
+// Burst depth and tile width (round 2, scripts/tune/big_tune.hip, profiles/
+// r02/tune/big_tune{2,...,7}.txt: 6 boxes x 3 arenas).  With 16-KiB tiles and
+// bursts of 8 tiles a wave keeps 32 loads in flight and the chip ~32 MiB of
+// one stream.  Bursts of 2 tiles (8 loads per wave, ~8 MiB on the chip) ran
+// +2.3-3.5 % per byte at 8 buckets and +1.3-1.9 % at 3-4: the HBM row buffers
+// see a narrower address window.  Bursts of 1 (4 loads) starve the pipe
+// (-14 %), of 3 sit in between.  The same 8 loads per wave as ONE tile of 8
+// block-strides (U = 8: a CU's burst is one contiguous 32-KiB run instead of
+// two 16-KiB tiles 4 MiB apart) gained again: +0.4-0.9 % at 8 buckets, +1.4-
+// 2.2 % at 3-4 and +1.1-2.7 % at 2 buckets, where 16-KiB bursts of 2 had
+// tied.  Same chunk, same registers: 5 LDS tiles + 7 register tiles of 32
+// KiB = 96 MiB on 256 CUs.  At 1 bucket the wide tiles tie or lose 0.7 % and
+// the zero-input form and the copy vary by +-3 % between arenas, so they keep
+// their shapes.  Capping the write phase's stores in flight (s_waitcnt
+// vmcnt(4-16) per tile) changed nothing at any bucket count.
 template <int NB, bool ZIN>
-struct SweepShape {  // register tiles, tiles per burst of loads: the big chunks
-  // one stream (the zero-input form, the NB = 0 copy): 64-MiB chunks, bursts of 4
-  static constexpr int RT = (ZIN || NB == 0) ? 6 : 14;
-  static constexpr int TG = (ZIN || NB == 0) ? 4 : (NB >= 3 ? 2 : 8);
+struct SweepShape {  // the big chunks: register tiles, tiles per burst, block-strides per tile
+  // one stream (the zero-input form, the NB = 0 copy): 64-MiB chunks, bursts of 4 16-KiB tiles
+  static constexpr bool kOne = ZIN || NB == 0;
+  static constexpr int RT = kOne ? 6 : NB == 1 ? 14 : 7;
+  static constexpr int TG = kOne ? 4 : NB == 1 ? 8 : 1;
+  static constexpr int U = kOne || NB == 1 ? kPhaseU : 8;
+  // f4 per block per chunk: the LDS tiles' 160 KiB + the register tiles
+  static constexpr size_t kBlockF4 = kPhaseLdsF4 + (size_t)RT * kBlock * U;
 };
 constexpr int kSweepRT = 6;  // the small (64-MiB) chunks and the zero-input form
 constexpr int kSweepTG = 4;
 [[maybe_unused]] constexpr int kSweepT = kPhaseLdsTiles + kSweepRT;  // tuning harnesses
 
-// RT register tiles, bursts of TG tiles (template arguments so the tuning
-// harnesses can instantiate other shapes; production uses SweepShape).
-template <int NB, int RT = kSweepRT, int TG = kSweepTG, bool ZIN = false>
+// RT register tiles, bursts of TG tiles of U block-strides (4 KiB each)
+// (template arguments so the tuning harnesses can instantiate other shapes;
+// production uses SweepShape).
+template <int NB, int RT = kSweepRT, int TG = kSweepTG, bool ZIN = false, int U = kPhaseU>
 __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
     size_t chunk) {
-  constexpr int U = kPhaseU;
-  constexpr int kT = kPhaseLdsTiles + RT;
+  constexpr int kTile = kBlock * U;            // f4 per tile
+  constexpr int kLds = kPhaseLdsF4 / kTile;    // tiles parked in LDS
+  static_assert(kLds * kTile == kPhaseLdsF4, "whole LDS tiles");
+  constexpr int kT = kLds + RT;
   constexpr int S = ZIN ? NB : NB + 1;  // streams read
   static_assert(kT % TG == 0, "whole bursts");
   __shared__ f4 res[kPhaseLdsF4];
@@ -389,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
   for (int k = 0; k < S; ++k)
     src[k] = (!ZIN && k == 0) ? in : reinterpret_cast<const f4 *>(b.p[ZIN ? k : (k > 0 ? k - 1 : 0)]);
   const size_t G = gridDim.x;
-  const size_t lo = chunk * G * (size_t)kT * kPhaseTile;
+  const size_t lo = chunk * G * (size_t)kT * kTile;
   // Never taken (the host launches whole chunks only), but keep it: with this
   // exit the compiler schedules each burst's loads together at 6-8 buckets;
   // without it, short of registers, it regrouped the register tiles' adds
@@ -406,7 +417,7 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
       for (int j = 0; j < TG; ++j)
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          v[j][u] = ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kPhaseTile +
+          v[j][u] = ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kTile +
                               threadIdx.x + u * kBlock);
 #pragma unroll
       for (int j = 0; j < TG; ++j) {
@@ -415,11 +426,11 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
         for (int u = 0; u < U; ++u) {
           // each lane owns its slots: no barrier between passes; bucket order 0..NB-1
           const f4 first = ZIN ? f4(0.0f) + v[j][u] : v[j][u];
-          if (t < kPhaseLdsTiles) {
-            f4 &r = res[t * kPhaseTile + u * kBlock + threadIdx.x];
+          if (t < kLds) {
+            f4 &r = res[t * kTile + u * kBlock + threadIdx.x];
             r = k == 0 ? first : r + v[j][u];
           } else {
-            f4 &r = keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u];
+            f4 &r = keep[t >= kLds ? t - kLds : 0][u];
             r = k == 0 ? first : r + v[j][u];
           }
         }
@@ -429,12 +440,12 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
   __syncthreads();
 #pragma unroll
   for (int t = 0; t < kT; ++t) {
-    const size_t base = lo + ((size_t)t * G + blockIdx.x) * kPhaseTile + threadIdx.x;
+    const size_t base = lo + ((size_t)t * G + blockIdx.x) * kTile + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      __builtin_nontemporal_store(t < kPhaseLdsTiles
-                                      ? res[t * kPhaseTile + u * kBlock + threadIdx.x]
-                                      : keep[t >= kPhaseLdsTiles ? t - kPhaseLdsTiles : 0][u],
+      __builtin_nontemporal_store(t < kLds
+                                      ? res[t * kTile + u * kBlock + threadIdx.x]
+                                      : keep[t >= kLds ? t - kLds : 0][u],
                                   out + base + u * kBlock);
   }
 }
@@ -451,14 +462,14 @@ struct SweepSplit {
 
 template <int NB, bool ZIN = false>
 SweepSplit sweep_split(size_t n4_tiles) {
-  constexpr int RT = SweepShape<NB, ZIN>::RT;
+  using SS = SweepShape<NB, ZIN>;
   const size_t G = (size_t)num_cus();
   SweepSplit sp;
-  sp.big_f4 = G * (size_t)(kPhaseLdsTiles + RT) * kPhaseTile;
+  sp.big_f4 = G * SS::kBlockF4;
   sp.small_f4 = G * (size_t)(kPhaseLdsTiles + kSweepRT) * kPhaseTile;
   sp.big = n4_tiles / sp.big_f4;
   if (sp.big < (size_t)kPhaseMinChunks) sp.big = 0;
-  if (RT != kSweepRT && NB >= 3) {  // at 1-2 buckets the 64-MiB sweep lost to tile-major
+  if (!SS::kOne && NB >= 3) {  // at 1-2 buckets the 64-MiB sweep lost to tile-major
     // One big chunk fewer when that lets whole small chunks take more of the
     // rest: a 512-MiB shard is 4 x 96 + 2 x 64 MiB, not 5 x 96 + 32 MiB
     // through the tile-major form.
@@ -496,11 +507,11 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     using SS = SweepShape<NB, ZIN>;
     const SweepSplit sp = sweep_split<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
     for (size_t c = 0; c < sp.big; ++c)
-      hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN>), dim3((unsigned)G),
+      hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN, SS::U>), dim3((unsigned)G),
                          dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out),
                          reinterpret_cast<const f4 *>(in), b, n / 4, c);
     done = sp.big * sp.big_f4 * 4;
-    if constexpr (SS::RT != kSweepRT) {
+    if constexpr (!SS::kOne) {
       const BucketPtrs bo = offset_buckets<NB>(b, done);
       for (size_t c = 0; c < sp.small; ++c)
         hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN>), dim3((unsigned)G),
@@ -597,6 +608,7 @@ void sum_plan_nb(size_t n, gp_sum_plan *out) {
   out->sweep_launches = (int)l.sweep;
   out->sweep_reg_tiles = l.sweep ? SweepShape<NB, false>::RT : -1;
   out->sweep_burst_tiles = l.sweep ? SweepShape<NB, false>::TG : -1;
+  out->sweep_tile_kib = l.sweep ? SweepShape<NB, false>::U * 4 : -1;
   out->small_sweep_launches = (int)l.sweep_small;
   out->small_sweep_burst_tiles = l.sweep_small ? kSweepTG : -1;
   out->phased_launches = (int)l.phased;

@@ -51,7 +51,8 @@ class SumPlan(ctypes.Structure):
                 ("small_sweep_launches", ctypes.c_int),
                 ("phased_launches", ctypes.c_int), ("phased_reg_tiles", ctypes.c_int),
                 ("other_launches", ctypes.c_int),
-                ("sweep_burst_tiles", ctypes.c_int), ("small_sweep_burst_tiles", ctypes.c_int)]
+                ("sweep_burst_tiles", ctypes.c_int), ("small_sweep_burst_tiles", ctypes.c_int),
+                ("sweep_tile_kib", ctypes.c_int)]
 
 
 _c = ctypes

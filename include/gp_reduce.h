@@ -247,10 +247,12 @@ int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
  * *phased_launches = launches of the phase-separated kernels, sweep and
  * tile-major together (0 when the shard is too small for them and the mixed
  * form sums it in one launch);
- * *reg_tiles = 16-KiB tiles per block held in registers beside the 10 in LDS
- * by the first phased form (sweep: 14 with 96-MiB chunks, 6 with 64-MiB;
- * tile-major: 20 at 1-2 buckets, 12 at 3-4, 4 at 5-8; -1: not phased).  For measurement tools: bench.py prices the
- * dominant kernel per launch with it, as rocprofv3 reports it.
+ * *reg_tiles = tiles per block held in registers beside the 160 KiB in LDS
+ * by the first phased form (sweep, 96-MiB chunks: 7 tiles of 32 KiB at 2-8
+ * buckets, 14 of 16 KiB at 1; 64-MiB chunks: 6 of 16 KiB; tile-major: 20 at
+ * 1-2 buckets, 12 at 3-4, 4 at 5-8, of 16 KiB; -1: not phased).  For
+ * measurement tools: bench.py prices the dominant kernel per launch with it,
+ * as rocprofv3 reports it.
  * Returns GP_ERR_INVALID for num_buckets outside 1..8. */
 int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
                        int *reg_tiles);
@@ -258,16 +260,18 @@ int gp_bucket_sum_plan(size_t num_vals, int num_buckets, int *phased_launches,
 /* The same plan, plus *sweep_launches = how many of the phased launches are
  * the stream-by-stream sweep kernel, big and small chunks together
  * (gp_bucket_sum_launch_plan splits them); *reg_tiles is then the first sweep
- * form's: 14 (96-MiB chunks) or 6 (64-MiB chunks). */
+ * form's: 7 or 14 (96-MiB chunks) or 6 (64-MiB chunks). */
 int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launches,
                              int *reg_tiles, int *sweep_launches);
 
 /* Every launch of one pass of num_buckets (1..8) over num_vals floats in
  * 16-B-aligned buffers, by kernel form, in launch order; launches nothing:
  *   sweep_launches       the stream-by-stream kernel's big chunks (96 MiB on
- *                        256 CUs: 14 register tiles beside the 10 LDS ones;
- *                        sweep_burst_tiles: tiles per burst of loads, 2 at
- *                        3-8 buckets, 8 at 1-2),
+ *                        256 CUs: 384 KiB per block, 160 KiB of it in LDS;
+ *                        sweep_reg_tiles tiles of sweep_tile_kib KiB in
+ *                        registers, bursts of sweep_burst_tiles tiles: 7 x 32
+ *                        KiB, bursts of 1, at 2-8 buckets; 14 x 16 KiB, bursts
+ *                        of 8, at 1),
  *   small_sweep_launches then its 64-MiB chunks (6 register tiles, bursts of
  *                        small_sweep_burst_tiles = 4),
  *   phased_launches      then the tile-major phase-separated form
@@ -275,7 +279,7 @@ int gp_bucket_sum_sweep_plan(size_t num_vals, int num_buckets, int *phased_launc
  *   other_launches       then the mixed dwordx4 and scalar forms (0-2).
  * A reg_tiles / burst_tiles field is -1 when its form has no launch.  For
  * measurement tools: bench.py names and prices each kernel instantiation per
- * launch (bucket_sum_sweep_kernel<NB, reg_tiles, burst_tiles, ...>), as
+ * launch (bucket_sum_sweep_kernel<NB, reg_tiles, burst_tiles, zin, strides>), as
  * rocprofv3 reports it. */
 typedef struct gp_sum_plan {
   int sweep_launches, sweep_reg_tiles;
@@ -283,6 +287,7 @@ typedef struct gp_sum_plan {
   int phased_launches, phased_reg_tiles;
   int other_launches;
   int sweep_burst_tiles, small_sweep_burst_tiles; /* ABI 9 */
+  int sweep_tile_kib;                              /* ABI 9: 16 or 32 */
 } gp_sum_plan;
 int gp_bucket_sum_launch_plan(size_t num_vals, int num_buckets, gp_sum_plan *plan);
 

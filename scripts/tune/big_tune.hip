@@ -19,7 +19,13 @@
 // after each tile), since the read side gained from a narrower address window
 // (profiles/r02/tune/big_tune4.txt: no effect).  Pass 5 (this version): burst
 // depth and chunk size at 1-2 buckets, the zero-input form and the NB = 0 copy
-// (a gather plan's dense runs; out = b0 here, so the copy reads another buffer).
+// (a gather plan's dense runs; out = b0 here, so the copy reads another buffer)
+// (profiles/r02/tune/big_tune5.txt: production best or tied).  Pass 6 (this
+// version): tile width (sweep_u): 8 loads per wave as one contiguous 32-KiB
+// run per CU (UU = 8, TG = 1) or four 8-KiB tiles (UU = 2, TG = 4)
+// (profiles/r02/tune/big_tune6.txt): UU = 8, TG = 1 +0.4 % at 8 buckets, +2.2 %
+// at 4 and +2 % at 2.  Pass 7 (this version): UU = 8 at 1-8 buckets, the
+// zero-input form and the copy.
 // Usage: big_tune [rounds] [arenas]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -126,6 +132,80 @@ size_t launch_lb(float *out, const float *in, const BucketPtrs &b, bool run) {
   return chunks * chunk_f4 * 4;
 }
 
+
+// Tile width as a parameter (UU block-strides of 4 KiB per tile; production
+// UU = kPhaseU = 4): the same chunk and registers with wider tiles and fewer
+// per burst, so a CU's burst is one contiguous 8 * 4-KiB run (UU = 8, TG = 1)
+// instead of two 16-KiB tiles 4 MiB apart.
+template <int NB, int RT, int TG, int UU, bool ZIN = false>
+__global__ __launch_bounds__(kBlock) void sweep_u(f4 *__restrict__ out, const f4 *__restrict__ in,
+                                                  BucketPtrs b, size_t n4_tiles, size_t chunk) {
+  constexpr int kTile = kBlock * UU;
+  constexpr int kLds = kPhaseLdsF4 / kTile;
+  static_assert(kLds * kTile == kPhaseLdsF4, "whole LDS tiles");
+  constexpr int kT = kLds + RT;
+  constexpr int S = ZIN ? NB : NB + 1;
+  static_assert(kT % TG == 0, "whole bursts");
+  __shared__ f4 res[kPhaseLdsF4];
+  f4 keep[RT][UU];
+  const f4 *src[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+    src[k] = (!ZIN && k == 0) ? in : reinterpret_cast<const f4 *>(b.p[ZIN ? k : (k > 0 ? k - 1 : 0)]);
+  const size_t G = gridDim.x;
+  const size_t lo = chunk * G * (size_t)kT * kTile;
+  if (lo >= n4_tiles) return;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+#pragma unroll
+    for (int t0 = 0; t0 < kT; t0 += TG) {
+      f4 v[TG][UU];
+#pragma unroll
+      for (int j = 0; j < TG; ++j)
+#pragma unroll
+        for (int u = 0; u < UU; ++u)
+          v[j][u] = ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kTile + threadIdx.x + u * kBlock);
+#pragma unroll
+      for (int j = 0; j < TG; ++j) {
+        const int t = t0 + j;
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+          const f4 first = ZIN ? f4(0.0f) + v[j][u] : v[j][u];
+          if (t < kLds) {
+            f4 &r = res[t * kTile + u * kBlock + threadIdx.x];
+            r = k == 0 ? first : r + v[j][u];
+          } else {
+            f4 &r = keep[t >= kLds ? t - kLds : 0][u];
+            r = k == 0 ? first : r + v[j][u];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kT; ++t) {
+    const size_t base = lo + ((size_t)t * G + blockIdx.x) * kTile + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < UU; ++u)
+      __builtin_nontemporal_store(t < kLds ? res[t * kTile + u * kBlock + threadIdx.x] : keep[t >= kLds ? t - kLds : 0][u],
+                                  out + base + u * kBlock);
+  }
+}
+
+template <int NB, int RT, int TG, int UU, bool ZIN = false>
+size_t launch_u(float *out, const float *in, const BucketPtrs &b, bool run) {
+  const size_t n4 = kN / 4;
+  const size_t G = (size_t)num_cus();
+  const size_t chunk_f4 = G * (size_t)(kPhaseLdsF4 / (kBlock * UU) + RT) * kBlock * UU;
+  const size_t chunks = n4 / chunk_f4;
+  if (run)
+    for (size_t c = 0; c < chunks; ++c)
+      hipLaunchKernelGGL((sweep_u<NB, RT, TG, UU, ZIN>), dim3((unsigned)G), dim3(kBlock), 0, 0,
+                         reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b, n4, c);
+  return chunks * chunk_f4 * 4;
+}
+
 template <int NB, int RT, int TG, bool ZIN, bool FL = false>
 void report(const char *name) {
   hipFuncAttributes a;
@@ -174,10 +254,6 @@ int main(int argc, char **argv) {
     sets.push_back(s);
   }
   CK(hipDeviceSynchronize());
-  report<2, 14, 12, false>("add2 RT14 TG12");
-  report<1, 14, 12, false>("add1 RT14 TG12");
-  report<1, 6, 8, true>("zin1 RT6 TG8");
-  report<1, 6, 16, true>("zin1 RT6 TG16");
   struct V {
     std::string name;
     int nb;
@@ -202,25 +278,33 @@ int main(int argc, char **argv) {
     if (run) launch_bucket_sum_nb<0>(m, b.p[0], b, kN, nullptr);
     return kN;
   };
+#define LU(NB, RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<NB, RT, TG, UU>(m, m, b, r); }
+#define LUZ(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<1, RT, TG, UU, true>(m, m, b, r); }
+#define LU0(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<0, RT, TG, UU>(m, b.p[0], b, r); }
   std::vector<V> kinds = {
+      {"prod (RT14 TG2 + 64 MiB)", 8, prod_sum(8)},
+      {"sweep U4 RT14 TG2 (prod shape)", 8, LBW(8, 14, 2, 0)},
+      {"sweep U8 RT7 TG1", 8, LU(8, 7, 1, 8)},
+      {"sweep U5 RT11 TG1 (95 MiB)", 8, LU(8, 11, 1, 5)},
+      {"prod (RT14 TG2 + 64 MiB)", 3, prod_sum(3)},
+      {"sweep U8 RT7 TG1", 3, LU(3, 7, 1, 8)},
       {"prod (RT14 TG8 + tile-major)", 2, prod_sum(2)},
-      {"sweep RT14 TG8", 2, LBW(2, 14, 8, 0)},
-      {"sweep RT14 TG6", 2, LBW(2, 14, 6, 0)},
-      {"sweep RT14 TG12", 2, LBW(2, 14, 12, 0)},
-      {"sweep RT10 TG4 (80 MiB)", 2, LBW(2, 10, 4, 0)},
+      {"sweep U4 RT14 TG8 (prod shape)", 2, LBW(2, 14, 8, 0)},
+      {"sweep U8 RT7 TG1", 2, LU(2, 7, 1, 8)},
       {"prod (RT14 TG8 + tile-major)", 1, prod_sum(1)},
-      {"sweep RT14 TG8", 1, LBW(1, 14, 8, 0)},
-      {"sweep RT14 TG6", 1, LBW(1, 14, 6, 0)},
-      {"sweep RT14 TG12", 1, LBW(1, 14, 12, 0)},
+      {"sweep U4 RT14 TG8 (prod shape)", 1, LBW(1, 14, 8, 0)},
+      {"sweep U8 RT7 TG1", 1, LU(1, 7, 1, 8)},
+      {"sweep U8 RT7 TG2", 1, LU(1, 7, 2, 8)},
       {"prod ZIN (RT6 TG4, 64 MiB)", 0, prod_zin},
-      {"ZIN RT6 TG8", 0, LBZ(6, 8, 0)},
-      {"ZIN RT6 TG16", 0, LBZ(6, 16, 0)},
-      {"ZIN RT10 TG4 (80 MiB)", 0, LBZ(10, 4, 0)},
+      {"ZIN U8 RT3 TG1", 0, LUZ(3, 1, 8)},
+      {"ZIN U8 RT3 TG2", 0, LUZ(3, 2, 8)},
       {"prod copy (RT6 TG4, 64 MiB)", 0, prod_copy},
-      {"copy RT6 TG2", 0, LB0(6, 2)},
-      {"copy RT6 TG8", 0, LB0(6, 8)},
-      {"copy RT14 TG8 (96 MiB)", 0, LB0(14, 8)},
+      {"copy U8 RT3 TG1", 0, LU0(3, 1, 8)},
+      {"copy U8 RT3 TG2", 0, LU0(3, 2, 8)},
   };
+#undef LUZ
+#undef LU0
+#undef LU
 #undef LB0
 #undef LBW
 #undef LBZ

@@ -115,10 +115,11 @@ def test_product_does_not_import_oracle():
 
 def test_bucket_sum_plan_without_device():
     """gp_bucket_sum_plan launches nothing.  Without a device the library
-    assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 64 MiB
-    for the sweep form at 3-8 buckets (6 register tiles beside 10 LDS tiles
-    per block), 96 MiB at 1-2 (14 register tiles), on shards of at least 3
-    such chunks; tile-major 56 / 88 / 120 MiB
+    assumes MI355X's 256 CUs, as on the GPU box; chunk sizes there: 96 MiB
+    for the sweep form (7 register tiles of 32 KiB at 2-8 buckets, 14 of 16
+    KiB at 1, beside 160 KiB of LDS per block), then 64 MiB at 3-8 buckets (6
+    register tiles of 16 KiB), on shards of at least 3 such chunks;
+    tile-major 56 / 88 / 120 MiB
     with 4 / 12 / 20 register tiles for the rest; balanced chunks from 4 MiB
     (one 16-KiB tile per block) up."""
     L = native.lib()
@@ -136,17 +137,17 @@ def test_bucket_sum_plan_without_device():
         return launches.value, rt.value, sweeps.value
 
     # the 4 GiB headline shard: 42 sweep chunks of 96 MiB, then one of 64 MiB
-    assert sweep_plan(1 << 30, 8) == (43, 14, 43)
-    assert plan(1 << 30, 8) == (43, 14)
+    assert sweep_plan(1 << 30, 8) == (43, 7, 43)
+    assert plan(1 << 30, 8) == (43, 7)
     # 1-2 buckets: the rest after the 96-MiB chunks goes to the tile-major form
-    assert sweep_plan(1 << 30, 2) == (43, 14, 42)
+    assert sweep_plan(1 << 30, 2) == (43, 7, 42)
     assert sweep_plan(1 << 30, 1) == (43, 14, 42)
-    assert sweep_plan(1 << 30, 4) == (43, 14, 43)
-    assert sweep_plan(288 << 18, 2) == (3, 14, 3)
+    assert sweep_plan(1 << 30, 4) == (43, 7, 43)
+    assert sweep_plan(288 << 18, 2) == (3, 7, 3)
     # the 8-GPU shard (512 MiB): 4 x 96 + 2 x 64 MiB (not 5 x 96 + a 32-MiB tile-major rest)
-    assert sweep_plan(1 << 27, 8) == (6, 14, 6)
-    assert sweep_plan(1 << 29, 8) == (22, 14, 22)  # the 2-GPU shard: 20 x 96 + 2 x 64 MiB
-    assert sweep_plan(1 << 28, 3) == (11, 14, 11)  # the 4-GPU shard (1 GiB): 10 x 96 + 64 MiB
+    assert sweep_plan(1 << 27, 8) == (6, 7, 6)
+    assert sweep_plan(1 << 29, 8) == (22, 7, 22)  # the 2-GPU shard: 20 x 96 + 2 x 64 MiB
+    assert sweep_plan(1 << 28, 3) == (11, 7, 11)  # the 4-GPU shard (1 GiB): 10 x 96 + 64 MiB
     # 200 MiB: under 3 big chunks, so 3 64-MiB sweep chunks, then the 8-MiB
     # rest in 1 balanced tile-major chunk
     assert sweep_plan(200 << 18, 8) == (4, 6, 3)
@@ -166,11 +167,15 @@ def test_bucket_sum_plan_without_device():
     sp = native.SumPlan()
     assert L.gp_bucket_sum_launch_plan(1 << 30, 8, ctypes.byref(sp)) == 0
     assert (sp.sweep_launches, sp.sweep_reg_tiles, sp.small_sweep_launches, sp.phased_launches,
-            sp.phased_reg_tiles, sp.other_launches) == (42, 14, 1, 0, -1, 0)
-    assert (sp.sweep_burst_tiles, sp.small_sweep_burst_tiles) == (2, 4)  # 3-8 buckets: bursts of 2
+            sp.phased_reg_tiles, sp.other_launches) == (42, 7, 1, 0, -1, 0)
+    # 2-8 buckets: 32-KiB tiles, bursts of 1; the 64-MiB chunks: 16-KiB tiles, bursts of 4
+    assert (sp.sweep_burst_tiles, sp.sweep_tile_kib, sp.small_sweep_burst_tiles) == (1, 32, 4)
     assert L.gp_bucket_sum_launch_plan(1 << 30, 2, ctypes.byref(sp)) == 0
-    assert (sp.sweep_launches, sp.sweep_reg_tiles, sp.sweep_burst_tiles, sp.small_sweep_launches,
-            sp.small_sweep_burst_tiles) == (42, 14, 8, 0, -1)  # 1-2 buckets: bursts of 8, no 64-MiB chunks
+    assert (sp.sweep_launches, sp.sweep_reg_tiles, sp.sweep_burst_tiles, sp.sweep_tile_kib,
+            sp.small_sweep_launches, sp.small_sweep_burst_tiles) == (42, 7, 1, 32, 0, -1)  # no 64-MiB chunks
+    assert L.gp_bucket_sum_launch_plan(1 << 30, 1, ctypes.byref(sp)) == 0
+    assert (sp.sweep_launches, sp.sweep_reg_tiles, sp.sweep_burst_tiles, sp.sweep_tile_kib,
+            sp.small_sweep_launches) == (42, 14, 8, 16, 0)  # 1 bucket: 16-KiB tiles, bursts of 8
     n = (1 << 27) + 4 + 3  # 512 MiB + one dwordx4 + 3 floats
     assert L.gp_bucket_sum_launch_plan(n, 5, ctypes.byref(sp)) == 0
     assert (sp.sweep_launches, sp.small_sweep_launches, sp.phased_launches, sp.phased_reg_tiles,

@@ -35,29 +35,30 @@ def _kernel(asm, pattern):
     return body
 
 
-# (buckets, register tiles, tiles per burst, zero-input): every production
-# instantiation (gp_reduce.hip: SweepShape's 96-MiB chunks, the 64-MiB
-# chunks after them, the zero-input form)
-SWEEP_SHAPES = ([(nb, 14, 8, 0) for nb in range(1, 3)] + [(nb, 14, 2, 0) for nb in range(3, 9)]
-                + [(nb, 6, 4, 0) for nb in range(3, 9)] + [(1, 6, 4, 1)])
+# (buckets, register tiles, tiles per burst, zero-input, 4-KiB block-strides
+# per tile): every production instantiation (gp_reduce.hip: SweepShape's
+# 96-MiB chunks, the 64-MiB chunks after them, the zero-input form)
+SWEEP_SHAPES = ([(1, 14, 8, 0, 4)] + [(nb, 7, 1, 0, 8) for nb in range(2, 9)]
+                + [(nb, 6, 4, 0, 4) for nb in range(3, 9)] + [(1, 6, 4, 1, 4)])
 
 
-@pytest.mark.parametrize("nb,rt,tg,zin", SWEEP_SHAPES)
-def test_sweep_kernel_keeps_burst_schedule(asm, nb, rt, tg, zin):
-    body = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi{nb}ELi{rt}ELi{tg}ELb{zin}EE")
+@pytest.mark.parametrize("nb,rt,tg,zin,u", SWEEP_SHAPES)
+def test_sweep_kernel_keeps_burst_schedule(asm, nb, rt, tg, zin, u):
+    body = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi{nb}ELi{rt}ELi{tg}ELb{zin}ELi{u}EE")
     loads = len(re.findall(r"global_load_dwordx4", body))
     full_drains = len(re.findall(r"s_waitcnt vmcnt\(0\)", body))
     streams = nb if zin else nb + 1
-    # streams x (10 LDS + rt register) tiles x 4 block-strides, all dwordx4
-    assert loads == streams * (10 + rt) * 4
-    # production: at most one full drain per burst (0-14 per chunk); the
-    # regressed schedule drained once per tile or more (117-224 at 8 buckets)
-    bursts = streams * (10 + rt) // tg
+    lds_tiles = 40 // u  # 160 KiB of LDS in tiles of u * 4 KiB
+    # streams x (LDS + register) tiles x u block-strides, all dwordx4
+    assert loads == streams * (lds_tiles + rt) * u
+    # production: at most one full drain per burst; the regressed schedule
+    # drained once per 16-KiB tile or more (117-224 at 8 buckets)
+    bursts = streams * (lds_tiles + rt) // tg
     assert full_drains <= bursts, f"{full_drains} full vmcnt(0) drains: the burst schedule regressed"
     # each burst's loads are issued together: some wait leaves the rest of a
-    # burst (4 * tg - 1 loads) in flight
+    # burst (u * tg - 1 loads) in flight
     counts = [int(n) for n in re.findall(r"s_waitcnt vmcnt\((\d+)\)", body)]
-    assert max(counts) >= 4 * tg - 1, f"at most {max(counts)} loads in flight: bursts split"
+    assert max(counts) >= u * tg - 1, f"at most {max(counts)} loads in flight: bursts split"
     assert "scratch_" not in body and "buffer_store_dword" not in body  # no spills
 
 
