@@ -24,8 +24,11 @@
 // version): tile width (sweep_u): 8 loads per wave as one contiguous 32-KiB
 // run per CU (UU = 8, TG = 1) or four 8-KiB tiles (UU = 2, TG = 4)
 // (profiles/r02/tune/big_tune6.txt): UU = 8, TG = 1 +0.4 % at 8 buckets, +2.2 %
-// at 4 and +2 % at 2.  Pass 7 (this version): UU = 8 at 1-8 buckets, the
-// zero-input form and the copy.
+// at 4 and +2 % at 2.  Pass 7: UU = 8 at 1-8 buckets, the zero-input form and
+// the copy (big_tune7.txt: adopted at 2-8 buckets; 1 bucket tied or lost, the
+// one-stream forms +-3 % by arena).  Pass 8 (this version, 4 arenas): the
+// 64-MiB chunks after the big ones, 1 bucket with deeper 32-KiB bursts, and
+// the one-stream forms again.
 // Usage: big_tune [rounds] [arenas]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -282,19 +285,16 @@ int main(int argc, char **argv) {
 #define LUZ(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<1, RT, TG, UU, true>(m, m, b, r); }
 #define LU0(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<0, RT, TG, UU>(m, b.p[0], b, r); }
   std::vector<V> kinds = {
-      {"prod (RT14 TG2 + 64 MiB)", 8, prod_sum(8)},
-      {"sweep U4 RT14 TG2 (prod shape)", 8, LBW(8, 14, 2, 0)},
-      {"sweep U8 RT7 TG1", 8, LU(8, 7, 1, 8)},
-      {"sweep U5 RT11 TG1 (95 MiB)", 8, LU(8, 11, 1, 5)},
-      {"prod (RT14 TG2 + 64 MiB)", 3, prod_sum(3)},
-      {"sweep U8 RT7 TG1", 3, LU(3, 7, 1, 8)},
-      {"prod (RT14 TG8 + tile-major)", 2, prod_sum(2)},
-      {"sweep U4 RT14 TG8 (prod shape)", 2, LBW(2, 14, 8, 0)},
-      {"sweep U8 RT7 TG1", 2, LU(2, 7, 1, 8)},
+      {"prod (32-KiB tiles + 64 MiB)", 8, prod_sum(8)},
+      {"small U4 RT6 TG4 (prod, 64 MiB)", 8, LBW(8, 6, 4, 0)},
+      {"small U8 RT3 TG1 (64 MiB)", 8, LU(8, 3, 1, 8)},
+      {"prod (32-KiB tiles + 64 MiB)", 4, prod_sum(4)},
+      {"small U4 RT6 TG4 (prod, 64 MiB)", 4, LBW(4, 6, 4, 0)},
+      {"small U8 RT3 TG1 (64 MiB)", 4, LU(4, 3, 1, 8)},
       {"prod (RT14 TG8 + tile-major)", 1, prod_sum(1)},
       {"sweep U4 RT14 TG8 (prod shape)", 1, LBW(1, 14, 8, 0)},
-      {"sweep U8 RT7 TG1", 1, LU(1, 7, 1, 8)},
       {"sweep U8 RT7 TG2", 1, LU(1, 7, 2, 8)},
+      {"sweep U8 RT7 TG4", 1, LU(1, 7, 4, 8)},
       {"prod ZIN (RT6 TG4, 64 MiB)", 0, prod_zin},
       {"ZIN U8 RT3 TG1", 0, LUZ(3, 1, 8)},
       {"ZIN U8 RT3 TG2", 0, LUZ(3, 2, 8)},
