@@ -1082,7 +1082,19 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
   constexpr int kGroups = kBlock / LPR;
   const size_t groups = (n + RPG - 1) / RPG;
   size_t grid = (groups + kGroups - 1) / kGroups;
-  if (grid > grid_cap()) grid = grid_cap();
+  // The op-order scatter-add of RowData-sized rows with fewer blocks per CU
+  // than 8: fewer rows in flight, a narrower window of the read-modify-write
+  // side's addresses (as for the sweep sums' bursts).  Flat, 2 per CU: +3.9-
+  // 4.2 % on an identity index, +0.2-0.5 % on a random one (1 or 4 lost);
+  // segmented (read-my-writes), whose registers leave fewer waves per block
+  // resident, 4 per CU: +6.6-7.2 % identity, +5.0 % random (2 lost); the
+  // segmented gather keeps 8 (2 or 4 lost 6-25 %).  Three boxes, bit-exact
+  // (scripts/tune/wave_tune.hip, profiles/r02/tune/wave_tune{3,3b,4,4b}.txt).
+  constexpr bool kRowAdd = OP == kAddFrom && VEC == 4 && LPR == 32;
+  const size_t cap = (kRowAdd && SEG == kFlat)   ? (size_t)num_cus() * 2
+                     : (kRowAdd && SEG == kSegY) ? (size_t)num_cus() * 4
+                                                 : grid_cap();
+  if (grid > cap) grid = cap;
   if constexpr (SEG == kFlat)
     hipLaunchKernelGGL((row_op_kernel<T, VEC, OP, LPR, RPG>), dim3((unsigned)grid),
                        dim3(kBlock), 0, s, y, x, idx, n, off0, off1, row_size,

@@ -11,8 +11,16 @@
 // variant is bit-checked against the production planned call.  Pass 1
 // (profiles/r02/tune/wave_tune.txt): the scatter forms want every resident
 // block (fewer lose 10-50 %); the gather ran +2.7 % at 2 blocks per CU against
-// production's 4.  Pass 2 (this version): the gather at 2-4 blocks per CU,
-// random and identity (the unplanned call's) indexes.
+// production's 4.  Pass 2: the gather at 2-4 blocks per CU, random and
+// identity (the unplanned call's) indexes (wave_tune2.txt: within noise).
+// Pass 3: the unplanned scatter-add (row_op_kernel, op order) at grid caps of
+// 1-8 blocks per CU (wave_tune3{,b}.txt: 2 per CU +4 % identity, +0.3 %
+// random; adopted).  Pass 4 (this version): the segmented forms at 2-8
+// (wave_tune4{,b}.txt: the segmented add +5-7 % at 4 per CU, adopted; the
+// segmented gather keeps 8).  Pass 5 (this version): rows per group x blocks
+// per CU around the adopted flat scatter-add (4 rows, 2 per CU)
+// (wave_tune5.txt: the adopted shape is best; 2 or 8 rows per group at 1-4
+// blocks per CU lose 1.6-11 %).
 // Usage: wave_tune [rounds]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -52,6 +60,31 @@ __global__ void diff_k(const unsigned *a, const unsigned *b, size_t n, unsigned 
   unsigned long long c = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) c += a[i] != b[i];
   if (c) atomicAdd(bad, c);
+}
+
+// the unplanned scatter-add's kernel (row_op_kernel, op order) at a grid cap of
+// per_cu blocks per CU (production: kBlocksPerCU = 8)
+template <int OP, int RPG>
+void rowop(float *y, const float *x, const gp_double_index *ix, int per_cu) {
+  const size_t groups = (R + RPG - 1) / RPG;
+  const size_t grid = std::min((groups + kBlock / 32 - 1) / (kBlock / 32), (size_t)num_cus() * per_cu);
+  hipLaunchKernelGGL((row_op_kernel<f4, 4, OP, 32, RPG>), dim3((unsigned)grid), dim3(kBlock), 0, 0, y, x, ix, R,
+                     0, 0, W, W / 4, ~size_t(0));
+}
+
+// the segmented forms (row_op_seg_kernel: Read's segmented gather residual,
+// read-my-writes' segmented add) at a grid cap of per_cu blocks per CU
+template <int OP, int SEG>
+void rowseg(float *flat, const gp_row_segments &t, const gp_double_index *ix, int per_cu) {
+  constexpr int RPG = OP == kAddFrom ? 4 : 8;
+  const size_t groups = (R + RPG - 1) / RPG;
+  const size_t grid = std::min((groups + kBlock / 32 - 1) / (kBlock / 32), (size_t)num_cus() * per_cu);
+  SegArg<SEG> seg;
+  seg.t = t;
+  float *y = SEG == kSegX ? flat : nullptr;
+  const float *x = SEG == kSegY ? flat : nullptr;
+  hipLaunchKernelGGL((row_op_seg_kernel<f4, 4, OP, 32, RPG, SEG>), dim3((unsigned)grid), dim3(kBlock), 0, 0, y, x,
+                     ix, R, 0, 0, W, W / 4, ~size_t(0), seg);
 }
 
 template <int OP, int RPG>
@@ -125,19 +158,24 @@ int main(int argc, char **argv) {
   auto add_v = [&](const char *nm, std::function<void()> f) { vs.push_back({nm, 0, f, add_b}); };
   auto ini_v = [&](const char *nm, std::function<void()> f) { vs.push_back({nm, 3, f, two_b}); };
   auto gat_v = [&](const char *nm, std::function<void()> f) { vs.push_back({nm, 1, f, two_b}); };
-  gat_v("gath prod planned", [=] { gp_gather_rows_planned(y, x, gp, nullptr); });
-  gat_v("gath R8 /2", [=] { wave<kAssignTo, 8>(y, x, dg, 2); });
-  gat_v("gath R8 /3", [=] { wave<kAssignTo, 8>(y, x, dg, 3); });
-  gat_v("gath R8 /4", [=] { wave<kAssignTo, 8>(y, x, dg, 4); });
-  gat_v("gath prod unplanned", [=] { gp_gather_rows(y, x, dg, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  gat_v("gath ident prod unplanned", [=] { gp_gather_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  gat_v("gath ident R8 /2", [=] { wave<kAssignTo, 8>(y, x, di, 2); });
-  gat_v("gath ident R8 /3", [=] { wave<kAssignTo, 8>(y, x, di, 3); });
-  ini_v("init prod planned", [=] { gp_scatter_init_rows_planned(y, x, sp, nullptr); });
-  ini_v("init R8 /3", [=] { wave<kInitFrom, 8>(y, x, ds, 3); });
-  ini_v("init R8 /4", [=] { wave<kInitFrom, 8>(y, x, ds, 4); });
-  add_v("add  prod planned", [=] { gp_scatter_add_rows_planned(y, x, sp, nullptr); });
-  add_v("add  R8 /3", [=] { wave<kAddFrom, 8>(y, x, ds, 3); });
+  // op order: random (x sequential, y random) and identity
+  std::vector<gp_double_index> ridx(R);
+  for (size_t r = 0; r < R; ++r) ridx[r] = gp_double_index{r, perm[r]};
+  gp_double_index *dr;
+  CK(hipMalloc(&dr, R * 16));
+  CK(hipMemcpy(dr, ridx.data(), R * 16, hipMemcpyHostToDevice));
+  add_v("add rand prod (RPG4 /2)", [=] { gp_scatter_add_rows(y, x, dr, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  add_v("add rand RPG2 /3", [=] { rowop<kAddFrom, 2>(y, x, dr, 3); });
+  add_v("add rand RPG2 /4", [=] { rowop<kAddFrom, 2>(y, x, dr, 4); });
+  add_v("add rand RPG4 /3", [=] { rowop<kAddFrom, 4>(y, x, dr, 3); });
+  add_v("add rand RPG8 /1", [=] { rowop<kAddFrom, 8>(y, x, dr, 1); });
+  add_v("add rand RPG8 /2", [=] { rowop<kAddFrom, 8>(y, x, dr, 2); });
+  add_v("add ident prod (RPG4 /2)", [=] { gp_scatter_add_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  add_v("add ident RPG2 /3", [=] { rowop<kAddFrom, 2>(y, x, di, 3); });
+  add_v("add ident RPG2 /4", [=] { rowop<kAddFrom, 2>(y, x, di, 4); });
+  add_v("add ident RPG4 /3", [=] { rowop<kAddFrom, 4>(y, x, di, 3); });
+  add_v("add ident RPG8 /1", [=] { rowop<kAddFrom, 8>(y, x, di, 1); });
+  add_v("add ident RPG8 /2", [=] { rowop<kAddFrom, 8>(y, x, di, 2); });
   // bit check against the production planned call of the same op
   for (size_t i = 0; i < vs.size(); ++i) {
     CK(hipMemcpy(y, y0, N * 4, hipMemcpyDeviceToDevice));
