@@ -909,11 +909,11 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // row_op_kernel (scripts/tune/rowmap_tune.hip, profiles/r01b/rowmap_focus_*.txt):
 // 11-12 % faster for the gather at 128-float rows (1.39-1.44 ms for 8 M rows,
 // 76-78 % of 8 TB/s), 8-10 % at 64-float rows and 6-7 % at 16-float rows
-// (profiles/r01b/rowmap_short_{a,b}.txt).  The scatter ops keep row_op_kernel:
-// through this kernel (the add / init forms below exist for that A/B only;
-// the product instantiates the gather) the scatter-add was 3-8 % slower and
-// the fused init 13-18 % slower (profiles/r01b/rowmap_scatter_{a,b}.txt), and
-// so were 1024-float rows (13 %, one row per wave instruction).
+// (profiles/r01b/rowmap_short_{a,b}.txt).  In op order the scatter-add keeps
+// row_op_kernel: through this kernel it was 3-8 % slower (profiles/r01b/
+// rowmap_scatter_{a,b}.txt), and so were 1024-float rows (13 %, one row per
+// wave instruction).  The fused init runs here, and a row plan's destination-
+// sorted residual runs its add here too (launch_row_op_lpr).
 template <typename T, int OP, int LPR, int RPG, int SEG>
 __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
@@ -1062,6 +1062,12 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
     // read-modify-write side runs 3-8 % slower here than in row_op_kernel).  Rows in flight per group: 8 at
     // 32 lanes per row (16 spilled past 256 VGPRs: 9 % slower), 16 at 16 lanes.
     constexpr int RPG = LPR == 32 ? 8 : 16;
+    // The fused init in op order stays here too: row_op_kernel at 2 blocks
+    // per CU ran 68.5-68.7 % against 60.1-60.2 % on an identity index but
+    // 64.0-64.2 % against 66.4-66.5 % on a random one in the probe
+    // (profiles/r02/tune/wave_tune6{,b}.txt), and in the bench line the
+    // random leg fell from 68.4-69.2 % to 61.2 % while identity rose only to
+    // 66.2 % (profiles/r02/rowinit/): a net loss, not adopted.
     if (kWaveGather || OP == kInitFrom || sorted) {
       auto *kern = &row_wave_kernel<T, OP, LPR, RPG, SEG>;
       size_t grid = (n + kBlock - 1) / kBlock;  // one 64-row tile per wave

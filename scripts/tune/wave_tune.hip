@@ -20,7 +20,11 @@
 // segmented gather keeps 8).  Pass 5 (this version): rows per group x blocks
 // per CU around the adopted flat scatter-add (4 rows, 2 per CU)
 // (wave_tune5.txt: the adopted shape is best; 2 or 8 rows per group at 1-4
-// blocks per CU lose 1.6-11 %).
+// blocks per CU lose 1.6-11 %).  Pass 6 (this version): the unplanned init
+// and gather in op order, wave-map kernel against row_op_kernel at 1-8 per CU
+// (wave_tune6{,b}.txt: the init +14 % identity / -3 % random at 2 per CU, but
+// a net loss in the bench line, profiles/r02/rowinit/; the gather keeps the
+// wave map).
 // Usage: wave_tune [rounds]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -164,18 +168,27 @@ int main(int argc, char **argv) {
   gp_double_index *dr;
   CK(hipMalloc(&dr, R * 16));
   CK(hipMemcpy(dr, ridx.data(), R * 16, hipMemcpyHostToDevice));
-  add_v("add rand prod (RPG4 /2)", [=] { gp_scatter_add_rows(y, x, dr, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  add_v("add rand RPG2 /3", [=] { rowop<kAddFrom, 2>(y, x, dr, 3); });
-  add_v("add rand RPG2 /4", [=] { rowop<kAddFrom, 2>(y, x, dr, 4); });
-  add_v("add rand RPG4 /3", [=] { rowop<kAddFrom, 4>(y, x, dr, 3); });
-  add_v("add rand RPG8 /1", [=] { rowop<kAddFrom, 8>(y, x, dr, 1); });
-  add_v("add rand RPG8 /2", [=] { rowop<kAddFrom, 8>(y, x, dr, 2); });
-  add_v("add ident prod (RPG4 /2)", [=] { gp_scatter_add_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  add_v("add ident RPG2 /3", [=] { rowop<kAddFrom, 2>(y, x, di, 3); });
-  add_v("add ident RPG2 /4", [=] { rowop<kAddFrom, 2>(y, x, di, 4); });
-  add_v("add ident RPG4 /3", [=] { rowop<kAddFrom, 4>(y, x, di, 3); });
-  add_v("add ident RPG8 /1", [=] { rowop<kAddFrom, 8>(y, x, di, 1); });
-  add_v("add ident RPG8 /2", [=] { rowop<kAddFrom, 8>(y, x, di, 2); });
+  // unplanned init / gather in op order (random and identity): production
+  // (row_wave_kernel, one resident round) against fewer blocks and against
+  // row_op_kernel at 1-8 blocks per CU
+  ini_v("init rand prod unplanned", [=] { gp_scatter_init_rows(y, x, dr, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  ini_v("init rand wave /2", [=] { wave<kInitFrom, 8>(y, x, dr, 2); });
+  ini_v("init rand row_op /2", [=] { rowop<kInitFrom, 8>(y, x, dr, 2); });
+  ini_v("init rand row_op /4", [=] { rowop<kInitFrom, 8>(y, x, dr, 4); });
+  ini_v("init rand row_op /8", [=] { rowop<kInitFrom, 8>(y, x, dr, 8); });
+  ini_v("init ident prod unplanned", [=] { gp_scatter_init_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  ini_v("init ident wave /2", [=] { wave<kInitFrom, 8>(y, x, di, 2); });
+  ini_v("init ident wave /3", [=] { wave<kInitFrom, 8>(y, x, di, 3); });
+  ini_v("init ident row_op /1", [=] { rowop<kInitFrom, 8>(y, x, di, 1); });
+  ini_v("init ident row_op /2", [=] { rowop<kInitFrom, 8>(y, x, di, 2); });
+  ini_v("init ident row_op /4", [=] { rowop<kInitFrom, 8>(y, x, di, 4); });
+  gat_v("gath ident prod unplanned", [=] { gp_gather_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  gat_v("gath ident row_op /2", [=] { rowop<kAssignTo, 8>(y, x, di, 2); });
+  gat_v("gath ident row_op /4", [=] { rowop<kAssignTo, 8>(y, x, di, 4); });
+  gat_v("gath ident row_op /8", [=] { rowop<kAssignTo, 8>(y, x, di, 8); });
+  gat_v("gath rand prod unplanned", [=] { gp_gather_rows(y, x, dg, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  gat_v("gath rand row_op /2", [=] { rowop<kAssignTo, 8>(y, x, dg, 2); });
+  gat_v("gath rand row_op /4", [=] { rowop<kAssignTo, 8>(y, x, dg, 4); });
   // bit check against the production planned call of the same op
   for (size_t i = 0; i < vs.size(); ++i) {
     CK(hipMemcpy(y, y0, N * 4, hipMemcpyDeviceToDevice));
