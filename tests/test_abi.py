@@ -373,3 +373,29 @@ def test_c_abi_consumer_builds_as_c99(tmp_path):
         assert r.returncode == 1 and "gp_device_count" in r.stderr, r.stdout + r.stderr
     else:
         assert "c_abi_check ok" in r.stdout
+
+
+def test_sweep_shapes_and_plan_cover_every_headline_shard():
+    """For 1-8 buckets and the 1/2/4/8-GPU shards of the 1M x 1024 table, the
+    launch plan uses the documented sweep shapes (gp_reduce.hip SweepShape:
+    32-KiB tiles, bursts of 1 at 2-8 buckets; 16-KiB tiles, bursts of 8 at 1)
+    and its chunks never overrun the shard (96-MiB chunks, then 64-MiB ones at
+    3-8 buckets, on 256 CUs without a device)."""
+    L = native.lib()
+    sp = native.SumPlan()
+    for shards in (1, 2, 4, 8):
+        n = (1 << 30) // shards  # floats per shard
+        for nb in range(1, 9):
+            assert L.gp_bucket_sum_launch_plan(n, nb, ctypes.byref(sp)) == 0
+            assert sp.sweep_launches >= 3, (shards, nb)
+            if nb == 1:
+                assert (sp.sweep_reg_tiles, sp.sweep_burst_tiles, sp.sweep_tile_kib) == (14, 8, 16)
+            else:
+                assert (sp.sweep_reg_tiles, sp.sweep_burst_tiles, sp.sweep_tile_kib) == (7, 1, 32)
+            big = (160 + sp.sweep_reg_tiles * sp.sweep_tile_kib) * 1024 * 256  # bytes per 96-MiB chunk
+            assert big == 96 << 20
+            small = (160 + 6 * 16) * 1024 * 256 if sp.small_sweep_launches else 0
+            if nb <= 2:
+                assert sp.small_sweep_launches == 0
+            covered = sp.sweep_launches * big + sp.small_sweep_launches * small
+            assert covered <= 4 * n and 4 * n - covered < big, (shards, nb, covered)
