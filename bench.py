@@ -452,7 +452,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                 if ginfo["dense_rows"] == R:  # one dense run: the no-bucket sweep copy
                     pl = gplan.launches()
                     kernel = "bucket_sum_sweep_kernel" if pl["sweep"] else "bucket_sum_phased_kernel"
-                    kernel_id = "bucket_sum_sweep_kernel<0, 6, 4, false>" if pl["sweep"] else None
+                    kernel_id = "bucket_sum_sweep_kernel<0, 6, 4, false," if pl["sweep"] else None
                     launches = pl["sweep"] or pl["phased"]
                     other = pl["phased"] + pl["other"] if pl["sweep"] else pl["other"]
                     cus = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -466,7 +466,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                     if init:  # one sweep shape (64-MiB chunks), then the tile-major rest
                         pl = plan.launches(True)
                         kernel = "bucket_sum_sweep_kernel" if pl["sweep"] else "bucket_sum_phased_kernel"
-                        kernel_id = "bucket_sum_sweep_kernel<1, 6, 4, true>" if pl["sweep"] else None
+                        kernel_id = "bucket_sum_sweep_kernel<1, 6, 4, true," if pl["sweep"] else None
                         launches = pl["sweep"] or pl["phased"]
                         other = pl["phased"] + pl["other"] if pl["sweep"] else pl["other"]
                         cus = torch.cuda.get_device_properties(dev).multi_processor_count
