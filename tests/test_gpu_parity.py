@@ -943,3 +943,43 @@ def test_c_abi_consumer_on_gpu(dev):
     for what in ("gp_bucket_sum_apply 8 buckets", "gp_scatter_add_rows", "gp_scatter_add_rows_planned",
                  "gp_scatter_init_rows_planned", "gp_gather_rows", "gp_gather_rows_planned"):
         assert f"{what}: " in r.stdout and "bit-exact" in r.stdout
+
+
+# Sizes around the plan's boundaries on 256 CUs (floats): 3 whole 96-MiB chunks
+# (the big sweep's threshold), 3 whole 64-MiB chunks, whole multiples of both,
+# each +- one 16-KiB tile per block, one dwordx4 and single floats.
+_MiB = 1 << 18  # floats per MiB
+_FUZZ_SIZES = [3 * 96 * _MiB, 3 * 96 * _MiB - 4, 3 * 96 * _MiB + 4 * 1024 * 256 + 5,
+               3 * 64 * _MiB, 3 * 64 * _MiB - 1, 2 * 96 * _MiB + 64 * _MiB + 3,
+               5 * 96 * _MiB + 2 * 64 * _MiB + 7, 4 * 96 * _MiB + 17 * _MiB + 1]
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_bucket_sum_plan_boundaries_fuzz(dev, case):
+    """Random bucket counts (1-8, and 9-11 for chained passes) and in-place /
+    out-of-place sums at sizes around the launch plan's boundaries: every
+    element bit for bit against a plain torch fp32 reference adding the buckets
+    in client order, and the input left untouched out of place."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(9000 + case)
+    n = int(_FUZZ_SIZES[case % len(_FUZZ_SIZES)])
+    N = int(rng.integers(1, 12)) if case % 4 == 3 else int(rng.integers(1, 9))
+    out_of_place = bool(case % 2)
+    g = torch.Generator(device=dev)
+    g.manual_seed(9000 + case)
+    buckets = [torch.rand(n, generator=g, device=dev) - 0.5 for _ in range(N)]
+    master = torch.rand(n, generator=g, device=dev) - 0.5
+    expect = master.clone()
+    for b in buckets:
+        expect += b
+    if out_of_place:
+        m0 = master.clone()
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+        rowops.bucket_sum_into(out, master, buckets)
+        torch.cuda.synchronize()
+        assert torch.equal(master.view(torch.int32), m0.view(torch.int32))
+    else:
+        rowops.bucket_sum_apply(master, buckets)
+        out = master
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), expect.view(torch.int32)), (n, N, out_of_place)
