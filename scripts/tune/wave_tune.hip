@@ -24,7 +24,8 @@
 // and gather in op order, wave-map kernel against row_op_kernel at 1-8 per CU
 // (wave_tune6{,b}.txt: the init +14 % identity / -3 % random at 2 per CU, but
 // a net loss in the bench line, profiles/r02/rowinit/; the gather keeps the
-// wave map).
+// wave map).  Pass 7 (this version): the oplog side's cache policy for the
+// op-order scatter-add at its new 2 blocks per CU.
 // Usage: wave_tune [rounds]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -89,6 +90,60 @@ void rowseg(float *flat, const gp_row_segments &t, const gp_double_index *ix, in
   const float *x = SEG == kSegY ? flat : nullptr;
   hipLaunchKernelGGL((row_op_seg_kernel<f4, 4, OP, 32, RPG, SEG>), dim3((unsigned)grid), dim3(kBlock), 0, 0, y, x,
                      ix, R, 0, 0, W, W / 4, ~size_t(0), seg);
+}
+
+
+// row_op_kernel's whole-row path with the oplog (y) side's cache policy as a
+// parameter: YL non-temporal y loads, YS non-temporal y stores (production:
+// plain both; the op buffer x is read non-temporally either way)
+template <int RPG, bool YL, bool YS>
+__global__ __launch_bounds__(kBlock) void add_var_kernel(float *__restrict__ y, const float *__restrict__ x,
+                                                         const gp_double_index *__restrict__ index,
+                                                         size_t num_rows, size_t vw) {
+  constexpr int LPR = 32, kGroups = kBlock / LPR;
+  const int lane = threadIdx.x % LPR;
+  const size_t group = (size_t)blockIdx.x * kGroups + threadIdx.x / LPR;
+  const size_t gstride = (size_t)gridDim.x * kGroups * RPG;
+  f4 *yv = reinterpret_cast<f4 *>(y);
+  const f4 *xv = reinterpret_cast<const f4 *>(x);
+  for (size_t r0 = group * RPG; r0 < num_rows; r0 += gstride) {
+    uint64_t from[RPG], to[RPG];
+    bool live[RPG];
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+      live[k] = r0 + k < num_rows;
+      from[k] = to[k] = 0;
+      if (live[k]) {
+        const gp_double_index ix = index[r0 + k];
+        from[k] = ix.id0;
+        to[k] = ix.id1;
+      }
+    }
+    for (size_t j = lane; j < vw; j += LPR) {
+      f4 xs[RPG], ys[RPG];
+#pragma unroll
+      for (int k = 0; k < RPG; ++k)
+        if (live[k]) xs[k] = __builtin_nontemporal_load(xv + from[k] * vw + j);
+#pragma unroll
+      for (int k = 0; k < RPG; ++k)
+        if (live[k]) ys[k] = YL ? __builtin_nontemporal_load(yv + to[k] * vw + j) : yv[to[k] * vw + j];
+#pragma unroll
+      for (int k = 0; k < RPG; ++k)
+        if (live[k]) {
+          if (YS)
+            __builtin_nontemporal_store(ys[k] + xs[k], yv + to[k] * vw + j);
+          else
+            yv[to[k] * vw + j] = ys[k] + xs[k];
+        }
+    }
+  }
+}
+
+template <bool YL, bool YS>
+void addvar(float *y, const float *x, const gp_double_index *ix, int per_cu) {
+  const size_t groups = (R + 3) / 4;
+  const size_t grid = std::min((groups + kBlock / 32 - 1) / (kBlock / 32), (size_t)num_cus() * per_cu);
+  hipLaunchKernelGGL((add_var_kernel<4, YL, YS>), dim3((unsigned)grid), dim3(kBlock), 0, 0, y, x, ix, R, W / 4);
 }
 
 template <int OP, int RPG>
@@ -168,27 +223,16 @@ int main(int argc, char **argv) {
   gp_double_index *dr;
   CK(hipMalloc(&dr, R * 16));
   CK(hipMemcpy(dr, ridx.data(), R * 16, hipMemcpyHostToDevice));
-  // unplanned init / gather in op order (random and identity): production
-  // (row_wave_kernel, one resident round) against fewer blocks and against
-  // row_op_kernel at 1-8 blocks per CU
-  ini_v("init rand prod unplanned", [=] { gp_scatter_init_rows(y, x, dr, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  ini_v("init rand wave /2", [=] { wave<kInitFrom, 8>(y, x, dr, 2); });
-  ini_v("init rand row_op /2", [=] { rowop<kInitFrom, 8>(y, x, dr, 2); });
-  ini_v("init rand row_op /4", [=] { rowop<kInitFrom, 8>(y, x, dr, 4); });
-  ini_v("init rand row_op /8", [=] { rowop<kInitFrom, 8>(y, x, dr, 8); });
-  ini_v("init ident prod unplanned", [=] { gp_scatter_init_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  ini_v("init ident wave /2", [=] { wave<kInitFrom, 8>(y, x, di, 2); });
-  ini_v("init ident wave /3", [=] { wave<kInitFrom, 8>(y, x, di, 3); });
-  ini_v("init ident row_op /1", [=] { rowop<kInitFrom, 8>(y, x, di, 1); });
-  ini_v("init ident row_op /2", [=] { rowop<kInitFrom, 8>(y, x, di, 2); });
-  ini_v("init ident row_op /4", [=] { rowop<kInitFrom, 8>(y, x, di, 4); });
-  gat_v("gath ident prod unplanned", [=] { gp_gather_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  gat_v("gath ident row_op /2", [=] { rowop<kAssignTo, 8>(y, x, di, 2); });
-  gat_v("gath ident row_op /4", [=] { rowop<kAssignTo, 8>(y, x, di, 4); });
-  gat_v("gath ident row_op /8", [=] { rowop<kAssignTo, 8>(y, x, di, 8); });
-  gat_v("gath rand prod unplanned", [=] { gp_gather_rows(y, x, dg, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
-  gat_v("gath rand row_op /2", [=] { rowop<kAssignTo, 8>(y, x, dg, 2); });
-  gat_v("gath rand row_op /4", [=] { rowop<kAssignTo, 8>(y, x, dg, 4); });
+  add_v("add rand prod (plain y, /2)", [=] { gp_scatter_add_rows(y, x, dr, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  add_v("add rand var plain /2", [=] { addvar<false, false>(y, x, dr, 2); });
+  add_v("add rand var nt ld+st /2", [=] { addvar<true, true>(y, x, dr, 2); });
+  add_v("add rand var nt st /2", [=] { addvar<false, true>(y, x, dr, 2); });
+  add_v("add rand var nt ld /2", [=] { addvar<true, false>(y, x, dr, 2); });
+  add_v("add ident prod (plain y, /2)", [=] { gp_scatter_add_rows(y, x, di, R, gp_double_index{0, 0}, W, ~size_t(0), nullptr); });
+  add_v("add ident var plain /2", [=] { addvar<false, false>(y, x, di, 2); });
+  add_v("add ident var nt ld+st /2", [=] { addvar<true, true>(y, x, di, 2); });
+  add_v("add ident var nt st /2", [=] { addvar<false, true>(y, x, di, 2); });
+  add_v("add ident var nt ld /2", [=] { addvar<true, false>(y, x, di, 2); });
   // bit check against the production planned call of the same op
   for (size_t i = 0; i < vs.size(); ++i) {
     CK(hipMemcpy(y, y0, N * 4, hipMemcpyDeviceToDevice));
