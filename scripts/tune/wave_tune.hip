@@ -25,7 +25,10 @@
 // (wave_tune6{,b}.txt: the init +14 % identity / -3 % random at 2 per CU, but
 // a net loss in the bench line, profiles/r02/rowinit/; the gather keeps the
 // wave map).  Pass 7 (this version): the oplog side's cache policy for the
-// op-order scatter-add at its new 2 blocks per CU.
+// op-order scatter-add at its new 2 blocks per CU (wave_tune7{,b}.txt: nt
+// stores +0.7-1.2 % random / +1.5-2.2 % identity on two boxes, but the
+// bench line's random leg lost 4-5 % with them (profiles/r02/ntst/): not
+// adopted; nt loads lose on a random index).
 // Usage: wave_tune [rounds]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
