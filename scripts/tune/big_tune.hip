@@ -28,7 +28,10 @@
 // the copy (big_tune7.txt: adopted at 2-8 buckets; 1 bucket tied or lost, the
 // one-stream forms +-3 % by arena).  Pass 8 (this version, 4 arenas): the
 // 64-MiB chunks after the big ones, 1 bucket with deeper 32-KiB bursts, and
-// the one-stream forms again.
+// the one-stream forms again (big_tune8.txt: none adopted).  Pass 9 (this
+// version): around the adopted 32-KiB shape -- write order, 88-104 MiB
+// chunks, 40-KiB runs (10 block-strides per tile) (big_tune9.txt: the
+// adopted shape is best or tied everywhere).
 // Usage: big_tune [rounds] [arenas]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -140,7 +143,7 @@ size_t launch_lb(float *out, const float *in, const BucketPtrs &b, bool run) {
 // UU = kPhaseU = 4): the same chunk and registers with wider tiles and fewer
 // per burst, so a CU's burst is one contiguous 8 * 4-KiB run (UU = 8, TG = 1)
 // instead of two 16-KiB tiles 4 MiB apart.
-template <int NB, int RT, int TG, int UU, bool ZIN = false>
+template <int NB, int RT, int TG, int UU, bool ZIN = false, bool REV = false>
 __global__ __launch_bounds__(kBlock) void sweep_u(f4 *__restrict__ out, const f4 *__restrict__ in,
                                                   BucketPtrs b, size_t n4_tiles, size_t chunk) {
   constexpr int kTile = kBlock * UU;
@@ -187,7 +190,8 @@ __global__ __launch_bounds__(kBlock) void sweep_u(f4 *__restrict__ out, const f4
   }
   __syncthreads();
 #pragma unroll
-  for (int t = 0; t < kT; ++t) {
+  for (int t_ = 0; t_ < kT; ++t_) {
+    const int t = REV ? kT - 1 - t_ : t_;  // REV: register tiles out first
     const size_t base = lo + ((size_t)t * G + blockIdx.x) * kTile + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < UU; ++u)
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void sweep_u(f4 *__restrict__ out, const f4
   }
 }
 
-template <int NB, int RT, int TG, int UU, bool ZIN = false>
+template <int NB, int RT, int TG, int UU, bool ZIN = false, bool REV = false>
 size_t launch_u(float *out, const float *in, const BucketPtrs &b, bool run) {
   const size_t n4 = kN / 4;
   const size_t G = (size_t)num_cus();
@@ -204,7 +208,7 @@ size_t launch_u(float *out, const float *in, const BucketPtrs &b, bool run) {
   const size_t chunks = n4 / chunk_f4;
   if (run)
     for (size_t c = 0; c < chunks; ++c)
-      hipLaunchKernelGGL((sweep_u<NB, RT, TG, UU, ZIN>), dim3((unsigned)G), dim3(kBlock), 0, 0,
+      hipLaunchKernelGGL((sweep_u<NB, RT, TG, UU, ZIN, REV>), dim3((unsigned)G), dim3(kBlock), 0, 0,
                          reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b, n4, c);
   return chunks * chunk_f4 * 4;
 }
@@ -284,24 +288,20 @@ int main(int argc, char **argv) {
 #define LU(NB, RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<NB, RT, TG, UU>(m, m, b, r); }
 #define LUZ(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<1, RT, TG, UU, true>(m, m, b, r); }
 #define LU0(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<0, RT, TG, UU>(m, b.p[0], b, r); }
+#define LUR(NB, RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<NB, RT, TG, UU, false, true>(m, m, b, r); }
   std::vector<V> kinds = {
       {"prod (32-KiB tiles + 64 MiB)", 8, prod_sum(8)},
-      {"small U4 RT6 TG4 (prod, 64 MiB)", 8, LBW(8, 6, 4, 0)},
-      {"small U8 RT3 TG1 (64 MiB)", 8, LU(8, 3, 1, 8)},
-      {"prod (32-KiB tiles + 64 MiB)", 4, prod_sum(4)},
-      {"small U4 RT6 TG4 (prod, 64 MiB)", 4, LBW(4, 6, 4, 0)},
-      {"small U8 RT3 TG1 (64 MiB)", 4, LU(4, 3, 1, 8)},
-      {"prod (RT14 TG8 + tile-major)", 1, prod_sum(1)},
-      {"sweep U4 RT14 TG8 (prod shape)", 1, LBW(1, 14, 8, 0)},
-      {"sweep U8 RT7 TG2", 1, LU(1, 7, 2, 8)},
-      {"sweep U8 RT7 TG4", 1, LU(1, 7, 4, 8)},
-      {"prod ZIN (RT6 TG4, 64 MiB)", 0, prod_zin},
-      {"ZIN U8 RT3 TG1", 0, LUZ(3, 1, 8)},
-      {"ZIN U8 RT3 TG2", 0, LUZ(3, 2, 8)},
-      {"prod copy (RT6 TG4, 64 MiB)", 0, prod_copy},
-      {"copy U8 RT3 TG1", 0, LU0(3, 1, 8)},
-      {"copy U8 RT3 TG2", 0, LU0(3, 2, 8)},
+      {"U8 RT7 TG1 (prod shape, 96 MiB)", 8, LU(8, 7, 1, 8)},
+      {"U8 RT7 TG1 reversed writes", 8, LUR(8, 7, 1, 8)},
+      {"U8 RT6 TG1 (88 MiB)", 8, LU(8, 6, 1, 8)},
+      {"U8 RT8 TG1 (104 MiB)", 8, LU(8, 8, 1, 8)},
+      {"U10 RT5 TG1 (90 MiB, 40-KiB runs)", 8, LU(8, 5, 1, 10)},
+      {"prod (32-KiB tiles + tile-major)", 2, prod_sum(2)},
+      {"U8 RT7 TG1 (prod shape)", 2, LU(2, 7, 1, 8)},
+      {"U8 RT7 TG1 reversed writes", 2, LUR(2, 7, 1, 8)},
+      {"U10 RT5 TG1 (90 MiB)", 2, LU(2, 5, 1, 10)},
   };
+#undef LUR
 #undef LUZ
 #undef LU0
 #undef LU
