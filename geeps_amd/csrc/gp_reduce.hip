@@ -718,9 +718,10 @@ __device__ __forceinline__ float *seg_row(const gp_row_segments &t, uint64_t row
 //    non-temporal loads, 2-3 % faster.  The oplog side stays plain (nt on its
 //    loads or stores lost or tied; the server's sum reads it next and may find
 //    it in the Infinity Cache when the table is small).  At round 2's 2 blocks
-//    per CU for the op-order add, nt oplog stores gained 0.7-2.2 % in the probe
-//    (profiles/r02/tune/wave_tune7{,b}.txt) but the bench line's random leg
-//    fell from 64.6-65.4 % to 60.5 % (profiles/r02/ntst/): not adopted.
+//    per CU for the op-order add, nt oplog stores gained 0.7-2.2 % in the
+//    paired probe (profiles/r02/tune/wave_tune7{,b}.txt), but the bench line
+//    with them ran the random leg at 60.5 % (profiles/r02/ntst/), below the
+//    62.8-65.4 % plain stores reached on five other boxes: not adopted.
 //  * gather (Read): non-temporal loads of the cache rows AND stores into the
 //    op buffer, 3-5 % faster; either one alone tied or lost.
 template <int OP, typename T>
