@@ -31,7 +31,10 @@
 // the one-stream forms again (big_tune8.txt: none adopted).  Pass 9 (this
 // version): around the adopted 32-KiB shape -- write order, 88-104 MiB
 // chunks, 40-KiB runs (10 block-strides per tile) (big_tune9.txt: the
-// adopted shape is best or tied everywhere).
+// adopted shape is best or tied everywhere).  Pass 10 (this version): the
+// one-stream forms (zero-input, copy) with 32-KiB tiles over 5 arenas, to
+// settle big_tune7/8's +-3 % by arena (big_tune10.txt: zero-input +0.3 %,
+// copy -0.8 % on average; production kept).
 // Usage: big_tune [rounds] [arenas]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -290,16 +293,12 @@ int main(int argc, char **argv) {
 #define LU0(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<0, RT, TG, UU>(m, b.p[0], b, r); }
 #define LUR(NB, RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<NB, RT, TG, UU, false, true>(m, m, b, r); }
   std::vector<V> kinds = {
-      {"prod (32-KiB tiles + 64 MiB)", 8, prod_sum(8)},
-      {"U8 RT7 TG1 (prod shape, 96 MiB)", 8, LU(8, 7, 1, 8)},
-      {"U8 RT7 TG1 reversed writes", 8, LUR(8, 7, 1, 8)},
-      {"U8 RT6 TG1 (88 MiB)", 8, LU(8, 6, 1, 8)},
-      {"U8 RT8 TG1 (104 MiB)", 8, LU(8, 8, 1, 8)},
-      {"U10 RT5 TG1 (90 MiB, 40-KiB runs)", 8, LU(8, 5, 1, 10)},
-      {"prod (32-KiB tiles + tile-major)", 2, prod_sum(2)},
-      {"U8 RT7 TG1 (prod shape)", 2, LU(2, 7, 1, 8)},
-      {"U8 RT7 TG1 reversed writes", 2, LUR(2, 7, 1, 8)},
-      {"U10 RT5 TG1 (90 MiB)", 2, LU(2, 5, 1, 10)},
+      {"prod ZIN (U4 RT6 TG4, 64 MiB)", 0, prod_zin},
+      {"ZIN U8 RT3 TG2", 0, LUZ(3, 2, 8)},
+      {"ZIN U8 RT3 TG1", 0, LUZ(3, 1, 8)},
+      {"prod copy (U4 RT6 TG4, 64 MiB)", 0, prod_copy},
+      {"copy U8 RT3 TG2", 0, LU0(3, 2, 8)},
+      {"copy U8 RT3 TG1", 0, LU0(3, 1, 8)},
   };
 #undef LUR
 #undef LUZ
