@@ -318,6 +318,9 @@ int gp_zero(float *y, size_t num_vals, gp_stream s);
 int gp_device_count(int *count);
 int gp_set_device(int device);
 int gp_get_device(int *device);
+/* Device memory; buffers of 64 MiB and up are requested physically
+ * contiguous first (steadier HBM rates for the streaming sums), plain
+ * otherwise or when no contiguous range is left. */
 int gp_malloc_device(void **ptr, size_t bytes);
 int gp_free_device(void *ptr);
 int gp_malloc_host(void **ptr, size_t bytes); /* pinned (mallocHost) */
