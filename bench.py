@@ -689,11 +689,19 @@ def main(argv=None, backend="nccl", apply_fn=None):
     from geeps_amd.shard import ShardLayout, hosted_clients
     hosted = hosted_clients(rank, world, C)
     # At N = 1 the buckets are the hosted clients' own buffers: the master shard
-    # goes in the same arena, after them.
-    master_floats = ShardLayout(R, W, world, rank).max_rows * W if world == 1 else 0
-    deltas, master = make_deltas(hosted, R * W, dev, args.layout, master_floats)
-    red = ShardedReducer(R, W, C, dev, exchange=args.exchange, apply_fn=apply_fn,
-                         master=master, layout=args.layout)
+    # goes in the same arena, after them.  At N > 1 the timed sum streams the
+    # reducer's arena (receive buckets + master), so it is allocated first: a
+    # process's first large allocation ran the sum at the top of the spread
+    # that later ones land in (allocation spread).
+    if world == 1:
+        master_floats = ShardLayout(R, W, world, rank).max_rows * W
+        deltas, master = make_deltas(hosted, R * W, dev, args.layout, master_floats)
+        red = ShardedReducer(R, W, C, dev, exchange=args.exchange, apply_fn=apply_fn,
+                             master=master, layout=args.layout)
+    else:
+        red = ShardedReducer(R, W, C, dev, exchange=args.exchange, apply_fn=apply_fn,
+                             layout=args.layout)
+        deltas, master = make_deltas(hosted, R * W, dev, args.layout, 0)
     L = red.layout
     log(f"[rank {rank}] shard rows [{L.row_start}, {L.row_start + L.local_rows}) "
         f"hosting clients {red.hosted}, HBM layout {args.layout}")
