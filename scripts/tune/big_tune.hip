@@ -34,7 +34,10 @@
 // adopted shape is best or tied everywhere).  Pass 10 (this version): the
 // one-stream forms (zero-input, copy) with 32-KiB tiles over 5 arenas, to
 // settle big_tune7/8's +-3 % by arena (big_tune10.txt: zero-input +0.3 %,
-// copy -0.8 % on average; production kept).
+// copy -0.8 % on average; production kept).  Pass 11 (this version): fewer
+// LDS tiles and more register tiles in the same 96-MiB chunk (sweep_l)
+// (big_tune11.txt: 4 LDS + 8 register tiles tie, 3 + 9 spill and lose 3-5 %,
+// 2 + 10 lose 1 %: the LDS read-modify-write is not what bounds a pass).
 // Usage: big_tune [rounds] [arenas]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -216,6 +219,82 @@ size_t launch_u(float *out, const float *in, const BucketPtrs &b, bool run) {
   return chunks * chunk_f4 * 4;
 }
 
+
+// LDS tiles as a parameter (NL of UU * 4 KiB; production: 160 KiB = 5 x 32 KiB
+// beside 7 register tiles): the same 96-MiB chunk with fewer tiles parked in
+// LDS and more in registers, so each pass does less LDS read-modify-write.
+template <int NB, int RT, int TG, int UU, int NL>
+__global__ __launch_bounds__(kBlock) void sweep_l(f4 *__restrict__ out, const f4 *__restrict__ in,
+                                                  BucketPtrs b, size_t n4_tiles, size_t chunk) {
+  constexpr int kTile = kBlock * UU;
+  constexpr int kT = NL + RT;
+  constexpr int S = NB + 1;
+  static_assert(kT % TG == 0, "whole bursts");
+  __shared__ f4 res[NL > 0 ? NL * kTile : 1];
+  f4 keep[RT][UU];
+  const f4 *src[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) src[k] = k == 0 ? in : reinterpret_cast<const f4 *>(b.p[k - 1]);
+  const size_t G = gridDim.x;
+  const size_t lo = chunk * G * (size_t)kT * kTile;
+  if (lo >= n4_tiles) return;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+#pragma unroll
+    for (int t0 = 0; t0 < kT; t0 += TG) {
+      f4 v[TG][UU];
+#pragma unroll
+      for (int j = 0; j < TG; ++j)
+#pragma unroll
+        for (int u = 0; u < UU; ++u)
+          v[j][u] = ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kTile + threadIdx.x + u * kBlock);
+#pragma unroll
+      for (int j = 0; j < TG; ++j) {
+        const int t = t0 + j;
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+          if (t < NL) {
+            f4 &r = res[t * kTile + u * kBlock + threadIdx.x];
+            r = k == 0 ? v[j][u] : r + v[j][u];
+          } else {
+            f4 &r = keep[t >= NL ? t - NL : 0][u];
+            r = k == 0 ? v[j][u] : r + v[j][u];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kT; ++t) {
+    const size_t base = lo + ((size_t)t * G + blockIdx.x) * kTile + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < UU; ++u)
+      __builtin_nontemporal_store(t < NL ? res[t * kTile + u * kBlock + threadIdx.x] : keep[t >= NL ? t - NL : 0][u],
+                                  out + base + u * kBlock);
+  }
+}
+
+template <int NB, int RT, int TG, int UU, int NL>
+size_t launch_l(float *out, const float *in, const BucketPtrs &b, bool run) {
+  const size_t n4 = kN / 4;
+  const size_t G = (size_t)num_cus();
+  const size_t chunk_f4 = G * (size_t)(NL + RT) * kBlock * UU;
+  const size_t chunks = n4 / chunk_f4;
+  if (run)
+    for (size_t c = 0; c < chunks; ++c)
+      hipLaunchKernelGGL((sweep_l<NB, RT, TG, UU, NL>), dim3((unsigned)G), dim3(kBlock), 0, 0,
+                         reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b, n4, c);
+  return chunks * chunk_f4 * 4;
+}
+
+template <int NB, int RT, int TG, int UU, int NL>
+void report_l(const char *name) {
+  hipFuncAttributes a;
+  CK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&sweep_l<NB, RT, TG, UU, NL>)));
+  std::printf("%-26s regs %d  scratch %zu B/lane  lds %zu B\n", name, a.numRegs, a.localSizeBytes, a.sharedSizeBytes);
+}
+
 template <int NB, int RT, int TG, bool ZIN, bool FL = false>
 void report(const char *name) {
   hipFuncAttributes a;
@@ -264,6 +343,10 @@ int main(int argc, char **argv) {
     sets.push_back(s);
   }
   CK(hipDeviceSynchronize());
+  report_l<8, 7, 1, 8, 5>("add8 L5 R7 (prod shape)");
+  report_l<8, 8, 1, 8, 4>("add8 L4 R8");
+  report_l<8, 9, 1, 8, 3>("add8 L3 R9");
+  report_l<8, 10, 1, 8, 2>("add8 L2 R10");
   struct V {
     std::string name;
     int nb;
@@ -292,14 +375,18 @@ int main(int argc, char **argv) {
 #define LUZ(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<1, RT, TG, UU, true>(m, m, b, r); }
 #define LU0(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<0, RT, TG, UU>(m, b.p[0], b, r); }
 #define LUR(NB, RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<NB, RT, TG, UU, false, true>(m, m, b, r); }
+#define LL(NB, RT, NL) [](float *m, const BucketPtrs &b, bool r) { return launch_l<NB, RT, 1, 8, NL>(m, m, b, r); }
   std::vector<V> kinds = {
-      {"prod ZIN (U4 RT6 TG4, 64 MiB)", 0, prod_zin},
-      {"ZIN U8 RT3 TG2", 0, LUZ(3, 2, 8)},
-      {"ZIN U8 RT3 TG1", 0, LUZ(3, 1, 8)},
-      {"prod copy (U4 RT6 TG4, 64 MiB)", 0, prod_copy},
-      {"copy U8 RT3 TG2", 0, LU0(3, 2, 8)},
-      {"copy U8 RT3 TG1", 0, LU0(3, 1, 8)},
+      {"prod (32-KiB tiles + 64 MiB)", 8, prod_sum(8)},
+      {"L5 R7 (prod shape)", 8, LL(8, 7, 5)},
+      {"L4 R8", 8, LL(8, 8, 4)},
+      {"L3 R9", 8, LL(8, 9, 3)},
+      {"L2 R10", 8, LL(8, 10, 2)},
+      {"prod (32-KiB tiles + tile-major)", 2, prod_sum(2)},
+      {"L5 R7 (prod shape)", 2, LL(2, 7, 5)},
+      {"L3 R9", 2, LL(2, 9, 3)},
   };
+#undef LL
 #undef LUR
 #undef LUZ
 #undef LU0
