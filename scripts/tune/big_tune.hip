@@ -38,6 +38,8 @@
 // LDS tiles and more register tiles in the same 96-MiB chunk (sweep_l)
 // (big_tune11.txt: 4 LDS + 8 register tiles tie, 3 + 9 spill and lose 3-5 %,
 // 2 + 10 lose 1 %: the LDS read-modify-write is not what bounds a pass).
+// Pass 12 (this version): plain instead of non-temporal loads in that shape
+// (big_tune12.txt: plain loads lose 5-10 %).
 // Usage: big_tune [rounds] [arenas]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -223,7 +225,7 @@ size_t launch_u(float *out, const float *in, const BucketPtrs &b, bool run) {
 // LDS tiles as a parameter (NL of UU * 4 KiB; production: 160 KiB = 5 x 32 KiB
 // beside 7 register tiles): the same 96-MiB chunk with fewer tiles parked in
 // LDS and more in registers, so each pass does less LDS read-modify-write.
-template <int NB, int RT, int TG, int UU, int NL>
+template <int NB, int RT, int TG, int UU, int NL, bool PL = false>
 __global__ __launch_bounds__(kBlock) void sweep_l(f4 *__restrict__ out, const f4 *__restrict__ in,
                                                   BucketPtrs b, size_t n4_tiles, size_t chunk) {
   constexpr int kTile = kBlock * UU;
@@ -247,7 +249,8 @@ __global__ __launch_bounds__(kBlock) void sweep_l(f4 *__restrict__ out, const f4
       for (int j = 0; j < TG; ++j)
 #pragma unroll
         for (int u = 0; u < UU; ++u)
-          v[j][u] = ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kTile + threadIdx.x + u * kBlock);
+          v[j][u] = PL ? src[k][lo + ((size_t)(t0 + j) * G + blockIdx.x) * kTile + threadIdx.x + u * kBlock]
+                       : ld_stream(src[k] + lo + ((size_t)(t0 + j) * G + blockIdx.x) * kTile + threadIdx.x + u * kBlock);
 #pragma unroll
       for (int j = 0; j < TG; ++j) {
         const int t = t0 + j;
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void sweep_l(f4 *__restrict__ out, const f4
   }
 }
 
-template <int NB, int RT, int TG, int UU, int NL>
+template <int NB, int RT, int TG, int UU, int NL, bool PL = false>
 size_t launch_l(float *out, const float *in, const BucketPtrs &b, bool run) {
   const size_t n4 = kN / 4;
   const size_t G = (size_t)num_cus();
@@ -283,7 +286,7 @@ size_t launch_l(float *out, const float *in, const BucketPtrs &b, bool run) {
   const size_t chunks = n4 / chunk_f4;
   if (run)
     for (size_t c = 0; c < chunks; ++c)
-      hipLaunchKernelGGL((sweep_l<NB, RT, TG, UU, NL>), dim3((unsigned)G), dim3(kBlock), 0, 0,
+      hipLaunchKernelGGL((sweep_l<NB, RT, TG, UU, NL, PL>), dim3((unsigned)G), dim3(kBlock), 0, 0,
                          reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b, n4, c);
   return chunks * chunk_f4 * 4;
 }
@@ -343,10 +346,6 @@ int main(int argc, char **argv) {
     sets.push_back(s);
   }
   CK(hipDeviceSynchronize());
-  report_l<8, 7, 1, 8, 5>("add8 L5 R7 (prod shape)");
-  report_l<8, 8, 1, 8, 4>("add8 L4 R8");
-  report_l<8, 9, 1, 8, 3>("add8 L3 R9");
-  report_l<8, 10, 1, 8, 2>("add8 L2 R10");
   struct V {
     std::string name;
     int nb;
@@ -376,16 +375,16 @@ int main(int argc, char **argv) {
 #define LU0(RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<0, RT, TG, UU>(m, b.p[0], b, r); }
 #define LUR(NB, RT, TG, UU) [](float *m, const BucketPtrs &b, bool r) { return launch_u<NB, RT, TG, UU, false, true>(m, m, b, r); }
 #define LL(NB, RT, NL) [](float *m, const BucketPtrs &b, bool r) { return launch_l<NB, RT, 1, 8, NL>(m, m, b, r); }
+#define LLP(NB, RT, NL) [](float *m, const BucketPtrs &b, bool r) { return launch_l<NB, RT, 1, 8, NL, true>(m, m, b, r); }
   std::vector<V> kinds = {
       {"prod (32-KiB tiles + 64 MiB)", 8, prod_sum(8)},
-      {"L5 R7 (prod shape)", 8, LL(8, 7, 5)},
-      {"L4 R8", 8, LL(8, 8, 4)},
-      {"L3 R9", 8, LL(8, 9, 3)},
-      {"L2 R10", 8, LL(8, 10, 2)},
+      {"L5 R7 nt loads (prod shape)", 8, LL(8, 7, 5)},
+      {"L5 R7 plain loads", 8, LLP(8, 7, 5)},
       {"prod (32-KiB tiles + tile-major)", 2, prod_sum(2)},
-      {"L5 R7 (prod shape)", 2, LL(2, 7, 5)},
-      {"L3 R9", 2, LL(2, 9, 3)},
+      {"L5 R7 nt loads (prod shape)", 2, LL(2, 7, 5)},
+      {"L5 R7 plain loads", 2, LLP(2, 7, 5)},
   };
+#undef LLP
 #undef LL
 #undef LUR
 #undef LUZ
