@@ -22,6 +22,10 @@ exchange + apply + all-gather refresh is timed separately and reported as
 
 value = gradient (delta) bytes reduced per second, whole job:
         clients * rows * width * 4 B / max-over-ranks step time.
+roofline.traffic = HBM bytes per launch of the dominant kernel from two
+        rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over this bench's
+        headline step in child processes, measured in this run at N = 1
+        (profiles/pmc_traffic.json's committed value otherwise, and beside it).
 roofline.achieved = algorithmic HBM bytes of one step ((clients + 2) * shard
         bytes: 8 bucket reads + master read + master write) / the step's
         average kernel time from HIP events around its launches on their
@@ -123,6 +127,9 @@ def parse(argv=None):
     p.add_argument("--no-e2e", action="store_true",
                    help="skip the libgeeps end-to-end clock leg")
     p.add_argument("--no-hbm-probe", action="store_true")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the in-run PMC traffic passes (roofline.traffic then comes from "
+                        "profiles/pmc_traffic.json)")
     p.add_argument("--layout", choices=["arena", "separate"], default="arena",
                    help="HBM layout of buckets + master: one arena (master last) or one "
                         "allocation per buffer")
@@ -596,6 +603,58 @@ def load_traffic(workload_key, kernel):
         return None
 
 
+def measure_traffic(rows, W, clients, kernel_id, timeout_s=150):
+    """HBM traffic per launch of the headline kernel, measured in this run: two
+    child processes, each this bench (headline step only, 2 steps + 1 warm-up)
+    under `rocprofv3 --pmc <counter> --kernel-trace`, one counter per pass
+    (FETCH_SIZE, then WRITE_SIZE), each under a hard time limit.  Per launch:
+    2 * FETCH_SIZE + WRITE_SIZE (KiB), the gfx950 correction of
+    MI355X_MICROARCH.md's HBM section, averaged over the dispatches of the
+    instantiation `kernel_id` names.  Returns (result, None) or (None, reason);
+    the caller falls back to profiles/pmc_traffic.json."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    child = [sys.executable, os.path.join(REPO, "bench.py"), "--rows", str(rows), "--width", str(W),
+             "--clients", str(clients), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+             "--no-host-inclusive", "--no-hbm-probe", "--no-config2", "--no-e2e", "--no-rowops",
+             "--no-per-rank", "--no-pmc"]
+    kib = {}
+    dispatches = {}
+    with tempfile.TemporaryDirectory(prefix="geeps_pmc_") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", counter, "--kernel-trace",
+                   "--output-format", "csv", "-d", out, "-o", "run", "--"] + child
+            r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True,
+                               env=dict(os.environ, TMPDIR=tmp))
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {counter} exited {r.returncode}: {r.stderr[-300:]}"
+            vals = []
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if kernel_id in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None, f"no {counter} rows for {kernel_id!r}"
+            kib[counter] = statistics.fmean(vals)
+            dispatches[counter] = len(vals)
+    hbm = 2 * kib["FETCH_SIZE"] * 1024 + kib["WRITE_SIZE"] * 1024
+    return {"bytes_per_launch": hbm, "kernel": kernel_id, "dispatches": dispatches,
+            "FETCH_SIZE_KiB_mean": round(kib["FETCH_SIZE"], 1),
+            "WRITE_SIZE_KiB_mean": round(kib["WRITE_SIZE"], 1),
+            "source": "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                      "this bench's headline step in child processes (2 * FETCH + WRITE)",
+            "emulated": False}, None
+
+
 def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
     """The drop-in path end to end: scripts/apps/geeps_clock_bench (built by
     __graft_entry__.build() against libgeeps.so and include/geeps.hpp, as an
@@ -744,6 +803,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
 
     host_inc = None
     cpu = None
+    pmc, pmc_error = None, None
     rowops_res = None
     probe = None
     config2 = None
@@ -784,9 +844,14 @@ def main(argv=None, backend="nccl", apply_fn=None):
         if not args.no_cpu_baseline:
             log("[rank 0] cpu baseline leg")
             cpu = cpu_baseline(min(args.cpu_rows, R), W, C, args.cpu_seconds)
+        # not when this process itself runs under rocprofv3 (it sets ROCPROF_*)
+        if not args.no_pmc and not any(k.startswith("ROCPROF") for k in os.environ):
+            log("[rank 0] PMC traffic passes (rocprofv3 child processes)")
+            pmc, pmc_error = measure_traffic(R, W, C, plan["kernel_id"])
 
     if rank == 0:
-        traffic = load_traffic(workload_key, plan["kernel_id"])
+        committed = load_traffic(workload_key, plan["kernel_id"])
+        traffic = pmc or committed
         share = plan["share"]
         line = {
             "metric": METRIC,
@@ -832,6 +897,10 @@ def main(argv=None, backend="nccl", apply_fn=None):
             "hbm_GBps_algorithmic": round((C + 2) * R * W * 4 / step_s / 1e9, 1),
             "cpu_baseline": cpu,
         }
+        if pmc and committed:
+            line["roofline"]["traffic_committed"] = committed
+        if pmc_error:
+            line["roofline"]["traffic_measure_error"] = pmc_error
         if result_exchange:
             line["exchange_inclusive"] = result_exchange[0]
             line["exchange_inclusive_alt"] = result_exchange[1]
