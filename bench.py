@@ -127,6 +127,8 @@ def parse(argv=None):
     p.add_argument("--no-e2e", action="store_true",
                    help="skip the libgeeps end-to-end clock leg")
     p.add_argument("--no-hbm-probe", action="store_true")
+    p.add_argument("--no-separate-alloc", action="store_true",
+                   help="skip timing the headline sum on separately allocated buffers")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the in-run PMC traffic passes (roofline.traffic then comes from "
                         "profiles/pmc_traffic.json)")
@@ -438,7 +440,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             planned = name.endswith("_planned")
             pinfo = ginfo if name.startswith("gather") else info
             # dense runs read no index; residual rows (and unplanned calls) do
-            index_rows = pinfo["residual_rows"] if planned else R
+            index_rows = pinfo["rows"] - pinfo["dense_rows"] if planned else R
             nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * index_rows
             writes = R * 512
             launches, other, share, kernel_id = 1, 0, 1.0, None
@@ -511,20 +513,29 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
     return out
 
 
+CPU_SHARE_PER_GPU = 16  # host threads per GPU on the pool's boxes (their per-GPU CPU share)
+
+
 def cpu_threads() -> tuple[int, str]:
-    """Threads for the all-cores CPU figure: the CPU share this process may
-    use (OMP_NUM_THREADS, set to the box's per-GPU share; else the affinity
-    mask), and how it was chosen."""
+    """Threads for the all-cores CPU figure, and how they were chosen: the CPU
+    share this process may use (OMP_NUM_THREADS when it grants more than one);
+    otherwise the affinity mask capped at one GPU's share of the box
+    (CPU_SHARE_PER_GPU: a 256-thread box hosts 8 GPUs and the harness sizes a
+    one-GPU job at 16), so an environment that pins OMP_NUM_THREADS=1 still
+    gets an all-cores figure, with its source stated."""
     nproc = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = nproc
     env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
+    if env and env.isdigit() and int(env) > 1:
         t = min(int(env), aff)
         return t, f"OMP_NUM_THREADS={env} (this process's CPU share; nproc={nproc}, affinity={aff})"
-    return aff, f"affinity mask (nproc={nproc})"
+    t = min(aff, CPU_SHARE_PER_GPU)
+    why = f"OMP_NUM_THREADS={env}" if env else "OMP_NUM_THREADS unset"
+    return t, (f"{why}; affinity mask ({aff} of nproc={nproc}) capped at one GPU's CPU share "
+               f"({CPU_SHARE_PER_GPU})")
 
 
 def cpu_baseline(rows, W, clients, seconds):
@@ -569,6 +580,8 @@ def cpu_baseline(rows, W, clients, seconds):
                             "threads_from": how, "ms_per_round": round(per2 * 1e3, 1),
                             "note": "row range split over threads = num_comm_channels "
                                     "server threads (clientlib.cpp:216-224)"}
+    else:
+        res["all_cores_skipped"] = f"1 thread available ({how})"
     res["setup_s"] = round(setup, 1)
     try:
         with open("/proc/cpuinfo") as f:
@@ -624,7 +637,7 @@ def measure_traffic(rows, W, clients, kernel_id, timeout_s=150):
     child = [sys.executable, os.path.join(REPO, "bench.py"), "--rows", str(rows), "--width", str(W),
              "--clients", str(clients), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
              "--no-host-inclusive", "--no-hbm-probe", "--no-config2", "--no-e2e", "--no-rowops",
-             "--no-per-rank", "--no-pmc"]
+             "--no-per-rank", "--no-pmc", "--no-separate-alloc"]
     kib = {}
     dispatches = {}
     with tempfile.TemporaryDirectory(prefix="geeps_pmc_") as tmp:
@@ -708,6 +721,45 @@ def per_rank_leg(deltas, master, rows, W, dev, ranks=(2, 4, 8), reps=10):
     return {"emulated": True, "ranks": out,
             "note": "one rank's shard sum at N GPUs, on this GPU; the driver's N-GPU runs measure "
                     "the real thing"}
+
+
+def separate_alloc_leg(deltas, reps=10):
+    """The headline 8-way sum on buffers allocated the way libgeeps allocates
+    its oplogs, staging buckets and master versions: one gp_malloc_device per
+    buffer (physically contiguous when the device has the range), instead of
+    the headline's single arena.  Same bytes, same kernel plan; the bucket
+    contents are the headline's deltas copied over.  DESIGN.md §5 (allocation
+    spread) has the measured spread over fresh allocations."""
+    import ctypes
+    from geeps_amd import native
+    lib = native.lib()
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    n = deltas[0].numel()
+    nbytes = n * 4
+    ptrs = []
+    try:
+        for _ in range(len(deltas) + 1):
+            p = ctypes.c_void_p()
+            native.check(lib.gp_malloc_device(ctypes.byref(p), nbytes), "gp_malloc_device")
+            ptrs.append(p.value)
+        for p, d in zip(ptrs, deltas):
+            native.check(lib.gp_memcpy_async(p, d.data_ptr(), nbytes, s), "gp_memcpy_async")
+        master = ptrs[-1]
+        native.check(lib.gp_memset_async(master, 0, nbytes, s), "gp_memset_async")
+        arr = (ctypes.c_void_p * len(deltas))(*ptrs[:-1])
+        fn = lambda: native.check(lib.gp_bucket_sum_apply(master, arr, len(deltas), n, s),
+                                  "gp_bucket_sum_apply")
+        avg = _time_calls(fn, reps, stream)
+    finally:
+        torch.cuda.synchronize()
+        for p in ptrs:
+            lib.gp_free_device(p)
+    gbps = (len(deltas) + 2) * nbytes / (avg / 1e3) / 1e9
+    return {"ms": round(avg, 4), "GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "buffers": len(deltas) + 1, "allocator": "gp_malloc_device per buffer (libgeeps' allocation)",
+            "note": "the headline sum on separately allocated bucket and master buffers; "
+                    "the headline line uses one arena"}
 
 
 def config2_leg(deltas, master, dev, probe=None, reps=5):
@@ -809,6 +861,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
     config2 = None
     e2e = None
     per_rank = None
+    sep_alloc = None
     if rank == 0 and world == 1 and dev.type == "cuda":
         if not args.no_hbm_probe:
             log("[rank 0] HBM probes")
@@ -823,6 +876,12 @@ def main(argv=None, backend="nccl", apply_fn=None):
             per_rank = per_rank_leg(deltas, master, R, W, dev)
             for v in per_rank["ranks"].values():
                 v["predicted_speedup"] = round(avg_kernel_ms / v["ms"], 3)
+        if not args.no_separate_alloc and args.layout == "arena":
+            log("[rank 0] separate-allocation leg")
+            try:
+                sep_alloc = separate_alloc_leg(deltas)
+            except Exception as exc:  # a side leg (needs another 36 GiB): report, keep the line
+                sep_alloc = {"error": f"{type(exc).__name__}: {str(exc)[-300:]}"}
         del deltas
         red = None
         master = None
@@ -910,6 +969,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
             line["roofline"]["same_box_model_ms"] = round(mm, 4)
             line["roofline"]["frac_of_same_box_model"] = round(mm / avg_kernel_ms_max, 4)
             line["hbm_probe"] = probe
+        if sep_alloc:
+            line["roofline"]["separate_alloc"] = sep_alloc
         if config2:
             line["config2"] = config2
         if per_rank:

@@ -646,9 +646,12 @@ void ClientLib::decide_fused_init() {
   }
 }
 
-// One DoubleIndex per op, grouped by channel, each channel's id1 set a
-// contiguous, duplicate-free cache range (vi_create_double_index,
-// clientlib-viter.cpp:817-883; the scatter-add kernel relies on distinct id1).
+// One DoubleIndex per op, grouped by channel, each channel's id1 range equal
+// to its row count (vi_create_double_index, clientlib-viter.cpp:817-883: the
+// CHECK_EQ at :871-873).  Like the reference this admits a repeated row when
+// the range still matches (cache rows {0, 0, 2}); the row plans add its
+// occurrences in op order, as the reference's CPU twin does (row-op-util.hpp:
+// 121-139; its GPU kernel races on such a row).
 void ClientLib::create_double_index(OpInfo &op) {
   std::vector<std::vector<gp_double_index>> per(num_channels_);
   for (size_t j = 0; j < op.rows.size(); ++j) {
@@ -674,14 +677,15 @@ void ClientLib::create_double_index(OpInfo &op) {
         hi = std::max<uint64_t>(hi, d.id1);
         ids.insert(d.id1);
       }
-      GP_CHECK_MSG(ids.size() == per[c].size(), "duplicate rows in one op");
+      op.repeats = op.repeats || ids.size() != per[c].size();
       GP_CHECK_EQ(hi - lo + 1, (uint64_t)per[c].size());
     }
     flat.insert(flat.end(), per[c].begin(), per[c].end());
   }
   // The update ops' oplog accumulate runs through a row plan per channel: the
-  // same rows visited in cache-row order (bit-identical: id1 distinct, checked
-  // above), so the scatter's read-modify-write side walks the oplog in order.
+  // same rows visited in cache-row order (bit-identical: a repeated id1 gets
+  // its adds in op order through the plan's repeat layers), so the scatter's
+  // read-modify-write side walks the oplog in order.
   // The read ops' gather runs through a gather plan per channel: its dense
   // runs (first-access order makes an op's rows one run per channel) are
   // copied by the phase-separated kernels, which hold their rate on every
@@ -837,12 +841,16 @@ void ClientLib::update_batch(int handle) {
       else
         GP_CALL(gp_scatter_add_rows_planned(oplog->data(), pre.buffer.data(), plan,
                                             ch.stream->get()));
-      if (config_.read_my_writes && pc.segmented)
+      if (config_.read_my_writes && pc.segmented) {
+        // (unreachable today: read-my-writes refreshes are private copies, so
+        // its cache is never segmented; the unplanned add has no repeat layers)
+        GP_CHECK_MSG(!pre.repeats, "read-my-writes update of an op listing a row twice into a "
+                                   "segmented cache");
         GP_CALL(gp_scatter_add_rows_segmented(&pc.segs, pre.buffer.data(),
                                               pre.index.data() + pre.ch_start[ch.id], n,
                                               gp_double_index{0, 0}, ROW_DATA_SIZE,
                                               pre.num_vals_limit, ch.stream->get()));
-      else if (config_.read_my_writes)
+      } else if (config_.read_my_writes)
         GP_CALL(gp_scatter_add_rows_planned(pc.data.data(), pre.buffer.data(), plan,
                                             ch.stream->get()));
     }

@@ -62,6 +62,9 @@ struct OpInfo {
   bool table_last_write = false;
   DeviceArray<gp_double_index> index;  // channel-major
   std::vector<size_t> ch_start, ch_size;
+  // a row listed more than once in one channel (its id1 repeats; the reference
+  // admits it when the channel's id1 range still equals the count)
+  bool repeats = false;
   // PRE_WRITE: per channel, the channel's slice of `index` as a row plan
   // (destination-sorted), which the oplog scatter-add / fused init run through
   std::vector<std::unique_ptr<RowPlan>> plans;

@@ -1240,6 +1240,15 @@ struct gp_row_plan_s {
   // device, offsets applied, ascending destination (scatter: id1, gather: id0)
   gp_double_index *residual = nullptr;
   size_t residual_rows = 0;
+  // Repeated destinations: layer k holds each destination's (k+1)-th
+  // occurrence in op order (device, ascending destination), run after the
+  // layers before it, so a repeated row receives its adds in op order.
+  struct Layer {
+    gp_double_index *index = nullptr;
+    size_t rows = 0;
+  };
+  std::vector<Layer> repeats;
+  size_t repeat_rows = 0;
   int device = 0;
 };
 
@@ -1251,19 +1260,47 @@ namespace {
 // and the destination must not repeat.
 int build_row_plan(gp_row_plan_s *p, const gp_double_index *host_index, size_t n,
                    gp_double_index off) {
+  using Layer = gp_row_plan_s::Layer;
   const size_t W = p->row_size;
   const bool g = p->gather;
   std::vector<gp_double_index> rows(n);
   for (size_t r = 0; r < n; ++r)
     rows[r] = gp_double_index{host_index[r].id0 + off.id0, host_index[r].id1 + off.id1};
   auto dst = [g](const gp_double_index &d) { return g ? d.id0 : d.id1; };
-  std::sort(rows.begin(), rows.end(), [&](const gp_double_index &a, const gp_double_index &b) {
+  // stable: a repeated destination keeps its occurrences in op order
+  std::stable_sort(rows.begin(), rows.end(), [&](const gp_double_index &a, const gp_double_index &b) {
     return dst(a) < dst(b);
   });
-  for (size_t r = 1; r < n; ++r)
-    if (dst(rows[r]) == dst(rows[r - 1]))
-      return set_error(GP_ERR_INVALID, "row plan: destination row " + std::to_string(dst(rows[r])) +
-                                           " repeats (destinations must be distinct)");
+  // A destination listed k + 1 times: its first occurrence stays in `rows`
+  // (distinct destinations), the later ones go to repeat layers 1..k.  The
+  // reference's channel check (range == count, clientlib-viter.cpp:869-873)
+  // admits such an index, e.g. cache rows {0, 0, 2}; its CPU twin
+  // (row-op-util.hpp:121-139) adds the repeats in op order, its GPU kernel races
+  // on them (row-op-util.cu:109-125).  The layers reproduce the CPU order: each
+  // layer has distinct destinations and runs after the one before it.
+  std::vector<std::vector<gp_double_index>> layers;
+  {
+    size_t w = 0, k = 0;
+    for (size_t r = 0; r < n; ++r) {
+      k = (r > 0 && dst(rows[r]) == dst(rows[r - 1])) ? k + 1 : 0;
+      if (k == 0) {
+        rows[w++] = rows[r];
+      } else {
+        if (layers.size() < k) layers.resize(k);
+        layers[k - 1].push_back(rows[r]);
+      }
+    }
+    rows.resize(w);
+    n = w;
+  }
+  for (auto &l : layers) {
+    Layer d;
+    d.rows = l.size();
+    GP_HIP_TRY(hipMalloc(&d.index, l.size() * sizeof(gp_double_index)));
+    p->repeats.push_back(d);  // owned by the plan from here (freed on any error)
+    GP_HIP_TRY(hipMemcpy(d.index, l.data(), l.size() * sizeof(gp_double_index), hipMemcpyHostToDevice));
+    p->repeat_rows += l.size();
+  }
   auto whole = [&](const gp_double_index &d) { return (d.id0 + 1) * W <= p->limit; };
   const size_t min_rows = std::max<size_t>(1, kDenseRunBytes / (W * sizeof(float)));
   std::vector<gp_double_index> rest;
@@ -1299,7 +1336,7 @@ int check_plan(const gp_row_plan_s *p, bool gather) {
   if (p->gather != gather)
     return set_error(GP_ERR_INVALID, gather ? "a scatter row plan passed to a gather"
                                             : "a gather row plan passed to a scatter");
-  if (p->residual_rows) {
+  if (p->residual_rows || p->repeat_rows) {
     int dev = -1;
     GP_HIP_TRY(hipGetDevice(&dev));
     if (dev != p->device)
@@ -1322,9 +1359,18 @@ int launch_planned(float *y, const float *x, const gp_row_plan_s *p, hipStream_t
                                   : launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s);
     if (rc != GP_OK) return rc;
   }
-  if (p->residual_rows)
-    return launch_row_op<OP>(y, x, p->residual, p->residual_rows, gp_double_index{0, 0}, W,
-                             p->limit, s, /*sorted=*/true);
+  if (p->residual_rows) {
+    const int rc = launch_row_op<OP>(y, x, p->residual, p->residual_rows, gp_double_index{0, 0}, W,
+                                     p->limit, s, /*sorted=*/true);
+    if (rc != GP_OK) return rc;
+  }
+  // later occurrences of repeated destinations: added in op order (the init's
+  // first occurrence zeroed the row; the rest add to it)
+  for (const auto &l : p->repeats) {
+    const int rc = launch_row_op<kAddFrom>(y, x, l.index, l.rows, gp_double_index{0, 0}, W, p->limit, s,
+                                           /*sorted=*/true);
+    if (rc != GP_OK) return rc;
+  }
   return GP_OK;
 }
 
@@ -1366,11 +1412,17 @@ int launch_gather_planned(float *y, const float *x, const gp_row_segments *xs,
       left -= take;
     }
   }
-  if (p->residual_rows) {
-    if (xs) return launch_row_op_seg<kAssignTo, kSegX>(y, xs, p->residual, p->residual_rows,
-                                                       gp_double_index{0, 0}, W, p->limit, s);
-    return launch_row_op<kAssignTo>(y, x, p->residual, p->residual_rows, gp_double_index{0, 0}, W,
-                                    p->limit, s, /*sorted=*/true);
+  // the residual, then later occurrences of repeated destinations (assigned in
+  // op order: the last one listed wins, as in the CPU twin's loop)
+  std::vector<gp_row_plan_s::Layer> parts;
+  if (p->residual_rows) parts.push_back({p->residual, p->residual_rows});
+  parts.insert(parts.end(), p->repeats.begin(), p->repeats.end());
+  for (const auto &l : parts) {
+    const int rc = xs ? launch_row_op_seg<kAssignTo, kSegX>(y, xs, l.index, l.rows, gp_double_index{0, 0},
+                                                             W, p->limit, s)
+                      : launch_row_op<kAssignTo>(y, x, l.index, l.rows, gp_double_index{0, 0}, W,
+                                                 p->limit, s, /*sorted=*/true);
+    if (rc != GP_OK) return rc;
   }
   return GP_OK;
 }
@@ -1483,9 +1535,20 @@ extern "C" {
 
 int gp_row_plan_destroy(gp_row_plan plan) {
   if (!plan) return GP_OK;
-  const hipError_t e = plan->residual ? hipFree(plan->residual) : hipSuccess;
+  hipError_t e = plan->residual ? hipFree(plan->residual) : hipSuccess;
+  for (const auto &l : plan->repeats) {
+    const hipError_t e2 = hipFree(l.index);
+    if (e == hipSuccess) e = e2;
+  }
   delete plan;
   GP_HIP_TRY(e);
+  return GP_OK;
+}
+
+int gp_row_plan_repeats(gp_row_plan plan, size_t *layers, size_t *repeat_rows) {
+  if (!plan || !layers || !repeat_rows) return set_error(GP_ERR_INVALID, "null pointer");
+  *layers = plan->repeats.size();
+  *repeat_rows = plan->repeat_rows;
   return GP_OK;
 }
 
@@ -1502,7 +1565,7 @@ int gp_row_plan_launches(gp_row_plan plan, int init, int *sweep_launches, int *p
                          int *other_launches) {
   if (!plan || !sweep_launches || !phased_launches || !other_launches)
     return set_error(GP_ERR_INVALID, "null pointer");
-  size_t sw = 0, ph = 0, ot = plan->residual_rows ? 1 : 0;
+  size_t sw = 0, ph = 0, ot = (plan->residual_rows ? 1 : 0) + plan->repeats.size();
   for (const RowRun &r : plan->dense) {
     const size_t n = r.rows * plan->row_size;
     const SumLaunches l = plan->gather ? sum_launches<0>(n)

@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 9  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 10  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -70,6 +70,7 @@ _SIGNATURES = {
     "gp_row_plan_create": (_i, [_c.POINTER(_vp), _vp, _sz, DoubleIndex, _sz, _sz]),
     "gp_row_plan_destroy": (_i, [_vp]),
     "gp_row_plan_info": (_i, [_vp, _c.POINTER(_sz), _c.POINTER(_sz), _c.POINTER(_sz)]),
+    "gp_row_plan_repeats": (_i, [_vp, _c.POINTER(_sz), _c.POINTER(_sz)]),
     "gp_row_plan_launches": (_i, [_vp, _i, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
     "gp_gather_plan_create": (_i, [_c.POINTER(_vp), _vp, _sz, DoubleIndex, _sz, _sz]),
     "gp_gather_rows_planned": (_i, [_vp, _vp, _vp, _vp]),

@@ -184,7 +184,9 @@ class RowPlan:
     add_rows_from_double_index_gpu / init_rows_from_double_index_gpu over the
     same index.  Gather plans: ``gather(y, x)`` / ``gather_segmented(y,
     segments)`` to assign_rows_to_double_index_gpu / gather_rows_segmented.
-    Destinations must be distinct (ValueError otherwise)."""
+    A repeated destination is handled in op order through the plan's repeat
+    layers (its adds in the order listed; for a gather the last one wins), as
+    the reference's CPU twins loop (row-op-util.hpp:81-139)."""
 
     def __init__(self, index, num_rows=None, index_offset=None, row_size=ROW_DATA_SIZE,
                  num_vals_limit=None, kind="scatter"):
@@ -229,8 +231,12 @@ class RowPlan:
         a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         check(native.lib().gp_row_plan_info(self._h, ctypes.byref(a), ctypes.byref(b),
                                             ctypes.byref(c)), "gp_row_plan_info")
+        layers, rep = ctypes.c_size_t(), ctypes.c_size_t()
+        check(native.lib().gp_row_plan_repeats(self._h, ctypes.byref(layers), ctypes.byref(rep)),
+              "gp_row_plan_repeats")
         return {"rows": a.value, "dense_runs": b.value, "dense_rows": c.value,
-                "residual_rows": a.value - c.value}
+                "residual_rows": a.value - c.value - rep.value, "repeat_layers": layers.value,
+                "repeat_rows": rep.value}
 
     def launches(self, init: bool = False) -> dict:
         """Launch plan of one planned add (or fused init) over 16-B-aligned

@@ -41,7 +41,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 9
+#define GP_ABI_VERSION 10
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -121,7 +121,14 @@ int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
  * (libgeeps builds one per op and channel at FinishVirtualIteration, where the
  * reference builds the op's device DoubleIndex: vi_create_double_index,
  * src/client/clientlib-viter.cpp:817-883).  The plan visits the rows in
- * destination (id1) order -- bit-neutral, since destinations are distinct.
+ * destination (id1) order -- bit-neutral, since each row's adds keep their
+ * order: a destination listed more than once (the reference's channel check,
+ * range == count at clientlib-viter.cpp:869-873, admits e.g. cache rows
+ * {0, 0, 2}) gets its later occurrences from "repeat layers" that run after
+ * the first occurrences, one layer per occurrence, so its adds land in op
+ * order as in the CPU twin add_rows_from_double_index_cpu
+ * (src/common/row-op-util.hpp:121-139).  (The reference's GPU kernel races on
+ * such a row; the unplanned gp_scatter_add_rows keeps its precondition.)
  * Runs in which id0 and id1 both step by one (whole rows, at least 4 MiB) are
  * moved as dense ranges by the phase-separated sum kernels (the init by their
  * zero-input form); the other rows
@@ -135,20 +142,24 @@ typedef struct gp_row_plan_s *gp_row_plan;
 /* Build a plan from a HOST copy of `num_rows` DoubleIndex entries; `offset`
  * and `num_vals_limit` are baked in (same meaning as gp_scatter_add_rows).
  * The plan's device index lives on the current device, and the plan runs only
- * there.  GP_ERR_INVALID if a destination row (id1 + offset.id1) repeats. */
+ * there. */
 int gp_row_plan_create(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
                        gp_double_index offset, size_t row_size, size_t num_vals_limit);
 int gp_row_plan_destroy(gp_row_plan plan);
 /* The plan's rows, its dense runs and the rows in them (the rest go to the
  * row kernels). */
 int gp_row_plan_info(gp_row_plan plan, size_t *num_rows, size_t *dense_runs, size_t *dense_rows);
+/* ABI 10: the plan's repeat layers (0 when every destination is distinct) and
+ * the rows in them (each destination's second, third ... occurrence). */
+int gp_row_plan_repeats(gp_row_plan plan, size_t *layers, size_t *repeat_rows);
 /* Launch plan of one planned add (init = 0) or fused init (init = 1) over
  * 16-B-aligned buffers (a gather plan: its gather, `init` ignored, flat
  * cache); launches nothing.  *sweep_launches = launches of the
  * stream-by-stream sum kernel over the dense runs (1 bucket; the init's
  * zero-input form), *phased_launches = tile-major phase-separated launches,
- * *other_launches = everything else (mixed / scalar sum forms, and one row
- * kernel launch for the residual rows).  For measurement tools (bench.py). */
+ * *other_launches = everything else (mixed / scalar sum forms, one row
+ * kernel launch for the residual rows and one per repeat layer).  For
+ * measurement tools (bench.py). */
 int gp_row_plan_launches(gp_row_plan plan, int init, int *sweep_launches, int *phased_launches,
                          int *other_launches);
 /* gp_scatter_add_rows(y, x, index, ...) through the plan (a3:
@@ -196,8 +207,9 @@ int gp_scatter_add_rows_segmented(const gp_row_segments *y_segments, const float
 /* A GATHER plan: the same compilation for gp_gather_rows' index (y[id0] =
  * x[id1], assign_rows_to_double_index_gpu, src/common/row-op-util.cu:39-72:
  * num_vals_limit guards the destination y).  libgeeps builds one per Read op
- * and channel.  Rows are visited in destination (id0) order, so destinations
- * must be distinct (GP_ERR_INVALID otherwise); dense runs are plain copies
+ * and channel.  Rows are visited in destination (id0) order (a repeated
+ * destination through repeat layers in op order: the last one listed wins, as
+ * in the CPU twin's loop); dense runs are plain copies
  * through the phase-separated kernels, the rest goes to the gather row
  * kernels.  A gather plan works only with the gp_gather_rows_*planned calls,
  * a scatter plan only with the scatter ones (GP_ERR_INVALID otherwise). */

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 9
+    assert L.gp_abi_version() == native.ABI_VERSION == 10
     assert isinstance(L.gp_last_error(), bytes)
 
 
@@ -238,8 +238,7 @@ def test_row_plan_launches_without_device():
 
 
 def test_gather_plan_without_device():
-    """Gather plans (gp_gather_plan_create): destinations are id0, which must
-    not repeat; an identity index is one dense run, copied by the no-bucket
+    """Gather plans (gp_gather_plan_create): destinations are id0; an identity index is one dense run, copied by the no-bucket
     sweep in 64-MiB chunks (a 4 GiB table: 64 launches); plans of one kind
     are refused by the other kind's calls before anything launches."""
     import numpy as np
@@ -263,11 +262,16 @@ def test_gather_plan_without_device():
     assert L.gp_gather_rows_planned(fake, fake, hs, None) == 1
     assert b"scatter row plan" in L.gp_last_error()
     assert L.gp_row_plan_destroy(hs) == 0
-    # repeated destination rows (id0) are refused
+    # a repeated destination row (id0) goes to a repeat layer (device memory:
+    # without a device the allocation fails, the index is not refused)
     dup = np.ascontiguousarray([[0, 1], [1, 2], [1, 3]], dtype=np.int64)
-    assert L.gp_gather_plan_create(ctypes.byref(h), dup.ctypes.data, 3, native.DoubleIndex(0, 0), 128,
-                                   (1 << 64) - 1) == 1
-    assert b"repeats" in L.gp_last_error()
+    rc = L.gp_gather_plan_create(ctypes.byref(h), dup.ctypes.data, 3, native.DoubleIndex(0, 0), 128,
+                                 (1 << 64) - 1)
+    assert b"repeat" not in L.gp_last_error()
+    if rc == 0:
+        assert L.gp_row_plan_destroy(h) == 0
+    else:
+        assert rc == native.GP_ERR_HIP
 
 
 def test_row_plan_classifies_dense_runs_without_device():
@@ -298,14 +302,27 @@ def test_row_plan_classifies_dense_runs_without_device():
     assert L.gp_row_plan_info(None, None, None, None) == native.GP_ERR_INVALID
 
 
-def test_row_plan_rejects_repeated_destinations():
+def test_row_plan_admits_repeated_destinations():
+    """A repeated destination (cache rows {5, 9, 5, 2}: the reference's range
+    check admits such sets, clientlib-viter.cpp:869-873) is no longer refused:
+    the plan puts the second occurrence in a repeat layer, which needs device
+    memory, so without a device creation fails on the allocation, not on the
+    index.  The GPU test test_row_plan_repeated_destinations checks the sums
+    against the oracle's sequential order."""
     import numpy as np
     idx = np.stack([np.arange(4), np.array([5, 9, 5, 2])], 1)
     rc, h = _plan(idx)
-    assert rc == native.GP_ERR_INVALID and b"repeats" in native.lib().gp_last_error()
-    assert not h.value
-    # distinct before the offset, distinct after: fine; null args rejected
+    msg = native.lib().gp_last_error()
+    assert b"repeat" not in msg
+    if rc == 0:  # a device is present
+        layers, rows = ctypes.c_size_t(), ctypes.c_size_t()
+        assert native.lib().gp_row_plan_repeats(h, ctypes.byref(layers), ctypes.byref(rows)) == 0
+        assert (layers.value, rows.value) == (1, 1)
+        native.lib().gp_row_plan_destroy(h)
+    else:
+        assert rc == native.GP_ERR_HIP and not h.value
     L = native.lib()
+    assert L.gp_row_plan_repeats(None, None, None) == native.GP_ERR_INVALID
     assert L.gp_row_plan_create(None, None, 0, native.DoubleIndex(0, 0), 128, 0) == 1
     h = ctypes.c_void_p()
     assert L.gp_row_plan_create(ctypes.byref(h), None, 4, native.DoubleIndex(0, 0), 128, 0) == 1

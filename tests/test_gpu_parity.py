@@ -618,7 +618,8 @@ def test_row_plan_matches_oracle(dev, kind, W, limit_frac, off):
     info = plan.info()
     assert info["rows"] == n_op
     if kind == "identity" and limit is None:
-        assert info == {"rows": n_op, "dense_runs": 1, "dense_rows": n_op, "residual_rows": 0}
+        assert info == {"rows": n_op, "dense_runs": 1, "dense_rows": n_op, "residual_rows": 0,
+                        "repeat_layers": 0, "repeat_rows": 0}
     if kind == "mixed" and limit is None:
         assert info["dense_runs"] == 3 and info["residual_rows"] > 0
     if kind == "permuted":
@@ -641,6 +642,67 @@ def test_row_plan_matches_oracle(dev, kind, W, limit_frac, off):
     torch.cuda.synchronize()
     assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", kind, W)
     plan.close()
+
+
+@pytest.mark.parametrize("W,limit_frac", [(128, None), (64, 0.7), (130, None)])
+def test_row_plan_repeated_destinations(dev, W, limit_frac):
+    """An index listing destinations more than once (the reference's range
+    check admits e.g. cache rows {0, 0, 2}, clientlib-viter.cpp:869-873):
+    scatter plans add every occurrence in op order, as the CPU twin's loop
+    does (row-op-util.hpp:121-139), so a dense run, a residual and repeat
+    layers 1..3 together equal the oracle bit for bit; the fused init zeroes
+    once, then adds in the same order; a gather plan with a repeated
+    destination (id0) keeps the last assignment, as the CPU twin's loop does."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(W + 17)
+    run = (4 << 20) // (W * 4) + 100  # one dense run of the plan's sweep size
+    n_cache = run + 3000
+    dense = np.stack([np.arange(run), np.arange(run)], 1)
+    # 2000 more rows: destinations drawn from 700 rows (inside and outside the
+    # run), so some appear 2-4 times; order interleaved with the run
+    rep = rng.choice(np.concatenate([rng.choice(run, 300, replace=False), run + np.arange(400)]),
+                     2000)
+    extra = np.stack([run + np.arange(2000), rep], 1)
+    idx = np.concatenate([dense, extra])
+    idx = idx[rng.permutation(len(idx))]
+    n_op = len(idx)
+    limit = None if limit_frac is None else int(n_op * W * limit_frac) + 5
+    x = rng.standard_normal(n_op * W).astype(np.float32)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    plan = rowops.RowPlan(idx, n_op, (0, 0), W, limit)
+    info = plan.info()
+    counts = np.bincount(idx[:, 1], minlength=n_cache)
+    assert info["repeat_rows"] == int((counts - 1).clip(0).sum())
+    assert info["repeat_layers"] == int(counts.max()) - 1 >= 1
+    assert info["dense_runs"] == (1 if limit is None else info["dense_runs"])
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, (0, 0), W, limit)
+    ty = T(y, dev)
+    plan.add(ty, T(x, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", W)
+    e = y.copy()
+    e.reshape(n_cache, W)[counts > 0] = 0.0
+    oracle.add_rows_from_double_index(e, x, idx, (0, 0), W, limit)
+    ty = T(y, dev)
+    plan.init(ty, T(x, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", W)
+    plan.close()
+    # gather: y[id0] = x[id1], destination id0 repeated -> the last one wins
+    g_idx = np.stack([rng.integers(0, 500, 1500), rng.integers(0, n_cache, 1500)], 1)
+    g_lim = None if limit is None else 400 * W + 3
+    src = rng.standard_normal(n_cache * W).astype(np.float32)
+    out = rng.standard_normal(500 * W).astype(np.float32)
+    e = out.copy()
+    oracle.assign_rows_to_double_index(e, src, g_idx, (0, 0), W, g_lim)
+    gplan = rowops.RowPlan(g_idx, len(g_idx), (0, 0), W, g_lim, kind="gather")
+    assert gplan.info()["repeat_layers"] >= 1
+    to = T(out, dev)
+    gplan.gather(to, T(src, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(to.cpu().numpy()), bits(e)), ("gather", W)
+    gplan.close()
 
 
 def test_row_plan_long_run_takes_sweep_forms(dev):
@@ -721,7 +783,8 @@ def test_gather_plan_matches_oracle(dev, kind, W, limit_frac, off, nseg):
     plan = rowops.RowPlan(idx, n_op, off, W, limit, kind="gather")
     info = plan.info()
     if kind == "identity" and limit is None:
-        assert info == {"rows": n_op, "dense_runs": 1, "dense_rows": n_op, "residual_rows": 0}
+        assert info == {"rows": n_op, "dense_runs": 1, "dense_rows": n_op, "residual_rows": 0,
+                        "repeat_layers": 0, "repeat_rows": 0}
     if kind == "mixed" and limit is None:
         assert info["dense_runs"] == 3 and info["residual_rows"] > 0
     ty = T(y, dev)

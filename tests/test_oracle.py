@@ -26,6 +26,26 @@ def test_kat_add_rows_reversed_double_scatter():
     assert y.tolist() == [80, 82, 61, 63, 42, 44, 23, 25]
 
 
+def test_kat_add_rows_repeated_destination_sums_in_op_order():
+    # The reference's channel check admits an op whose cache rows are {0, 0, 2}
+    # (range 3 == count 3, clientlib-viter.cpp:869-873).  Its CPU twin adds the
+    # repeats one after the other in op order (row-op-util.hpp:121-139); the row
+    # plans' repeat layers reproduce exactly this (tests/test_gpu_parity.py::
+    # test_row_plan_repeated_destinations).  fp32 order matters: 1e8 + 1 - 1e8.
+    W = 1
+    y = np.array([1e8, 7, 0], dtype=np.float32)
+    x = np.array([1, -1e8, 5], dtype=np.float32)
+    idx = np.array([[0, 0], [1, 0], [2, 2]], dtype=np.uint64)
+    oracle.add_rows_from_double_index(y, x, idx, (0, 0), W)
+    assert y.tolist() == [np.float32(np.float32(1e8) + 1) - np.float32(1e8), 7, 5]
+    assert y[0] == 0.0  # (1e8 + 1) rounds to 1e8 in fp32; the other order would give 1
+    # a gather listing a destination twice: the last assignment wins
+    g = np.zeros(2, dtype=np.float32)
+    oracle.assign_rows_to_double_index(g, np.array([3, 4, 5], dtype=np.float32),
+                                       np.array([[0, 0], [1, 1], [0, 2]], dtype=np.uint64), (0, 0), W)
+    assert g.tolist() == [5, 4]
+
+
 def test_kat_add_rows_offset_and_limit():
     # offset.id0 = 1 shifts the source, offset.id1 = 2 shifts the destination;
     # num_vals_limit = 5 guards the SOURCE element index (x_idx < 5).
