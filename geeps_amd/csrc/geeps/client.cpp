@@ -52,6 +52,7 @@ std::string ClientStats::to_json() const {
   o << "{\"nr_read\": " << nr_read << ", \"nr_update\": " << nr_update
     << ", \"nr_clock\": " << nr_clock << ", \"nr_push\": " << nr_push
     << ", \"nr_refresh\": " << nr_refresh << ", \"nr_refresh_in_place\": " << nr_refresh_in_place
+    << ", \"nr_refresh_staged\": " << nr_refresh_staged
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -81,12 +82,19 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
                "port_list must have one port per host");
   GP_CALL(gp_get_device(&device_));
   GP_CALL(gp_device_pci_bus_id(device_, pci_bus_id_, sizeof pci_bus_id_));
-  // Test hooks (fault injection; unset in production): GEEPS_STAGE_PEER_UPDATES=1
-  // stages same-node peers' buckets even on one GPU (the cross-GPU path on a
-  // one-GPU box); GEEPS_TEST_READER_DELAY_US=D delays every refresh a reader
-  // thread takes (a lagging client under SSP).
-  const char *stage = std::getenv("GEEPS_STAGE_PEER_UPDATES");
-  force_stage_ = stage && std::string(stage) == "1";
+  // Same-node peers on another GPU: stage their buckets into local HBM before
+  // the server's sum, and their refreshed shards into the local cache, by one
+  // peer copy each (GEEPS_STAGE_PEER_UPDATES / GEEPS_STAGE_PEER_REFRESH: "1"
+  // also on one GPU, which is how the cross-GPU path is tested on a one-GPU
+  // box; "0" never: the kernels read the peer's HBM in place over xGMI).
+  // Test hook (unset in production): GEEPS_TEST_READER_DELAY_US=D delays every
+  // refresh a reader thread takes (a lagging client under SSP).
+  auto mode = [](const char *name) {
+    const char *v = std::getenv(name);
+    return v && std::string(v) == "1" ? 1 : v && std::string(v) == "0" ? 0 : -1;
+  };
+  stage_updates_mode_ = mode("GEEPS_STAGE_PEER_UPDATES");
+  stage_refresh_mode_ = mode("GEEPS_STAGE_PEER_REFRESH");
   const char *delay = std::getenv("GEEPS_TEST_READER_DELAY_US");
   reader_delay_us_ = delay ? std::atoi(delay) : 0;
   // Same-node peers exchange rows device to device through IPC-mapped HBM
@@ -118,7 +126,9 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     ch->client_fd.assign(num_processes_, -1);
     ch->ipc_oplogs.resize(num_processes_);
     ch->ipc_client.assign(num_processes_, 0);
+    ch->other_gpu.assign(num_processes_, 0);
     ch->stage_from.assign(num_processes_, 0);
+    ch->stage_refresh_from.assign(num_processes_, 0);
     ch->version_sent.assign(num_processes_, std::vector<std::set<int>>(config_.num_tables));
     ch->client_done.assign(num_processes_, 0);
     channels_[c] = std::move(ch);
@@ -186,7 +196,12 @@ void ClientLib::server_accept_loop(Channel &ch, int expected) {
     ch.client_fd[cid] = fd;
     ch.ipc_client[cid] = hello.ipc && ipc_to(cid);
     hello.pci_bus_id[sizeof hello.pci_bus_id - 1] = 0;
-    ch.stage_from[cid] = ipc_to(cid) && (force_stage_ || std::strcmp(hello.pci_bus_id, pci_bus_id_) != 0);
+    // process cid hosts client cid and server cid on the same GPU, so one
+    // hello decides both directions
+    ch.other_gpu[cid] = std::strcmp(hello.pci_bus_id, pci_bus_id_) != 0;
+    auto staged = [&](int mode) { return ipc_to(cid) && (mode == 1 || (mode < 0 && ch.other_gpu[cid])); };
+    ch.stage_from[cid] = staged(stage_updates_mode_);
+    ch.stage_refresh_from[cid] = staged(stage_refresh_mode_);
     ch.server_readers.emplace_back([this, &ch, cid, fd] { server_reader(ch, cid, fd); });
   }
 }
@@ -547,12 +562,17 @@ void ClientLib::finish_virtual_iteration() {
       // When every server's shard will be read in place, it is never touched
       // (a Read waits for every server's first refresh) and is not allocated.
       bool copies = config_.read_my_writes;
-      for (uint32_t s = 0; s < num_processes_; ++s) copies = copies || (s != process_id_ && !ipc_to(s));
+      for (uint32_t s = 0; s < num_processes_; ++s)
+        copies = copies || (s != process_id_ && (!ipc_to(s) || ch.stage_refresh_from[s]));
       if (copies) {
         pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
         if (pc.num_rows) GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.stream->get()));
       }
       planned += pc.num_rows * kRowBytes * ((copies ? 1 : 0) + entries);
+      // the server's staging buckets for peers' slices: at most one per
+      // pending bucket (the queue is applied at kMaxPendingBuckets)
+      size_t staged_peers = 0;
+      for (uint32_t s = 0; s < num_processes_; ++s) staged_peers += ch.stage_from[s] ? 1 : 0;
       pc.server_row_start.resize(num_processes_);
       pc.server_num_rows.resize(num_processes_);
       const size_t div = pc.num_rows / num_processes_, res = pc.num_rows % num_processes_;
@@ -560,6 +580,8 @@ void ClientLib::finish_virtual_iteration() {
         pc.server_row_start[i] = div * i + std::min(i, res);
         pc.server_num_rows[i] = div + (i < res ? 1 : 0);
       }
+      planned += pc.server_num_rows[process_id_] * kRowBytes *
+                 std::min<size_t>(staged_peers, TabletServer::kMaxPendingBuckets);
       pc.per_server_data_age.assign(num_processes_, INITIAL_DATA_AGE);
       pc.live_ver.assign(num_processes_, -1);
       pc.live_ptr.assign(num_processes_, nullptr);
@@ -1019,7 +1041,7 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
   const double t0 = now_s();
   Channel &ch = *channels_[channel];
   std::vector<int> released;
-  bool in_place = false;
+  bool in_place = false, staged = false;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     GP_CHECK_LT(table_id, ch.tables.size());
@@ -1051,7 +1073,8 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
     }
     if (num_rows) {
       const int prev = pc.live_ver[server_id];
-      if (version >= 0 && !config_.read_my_writes) {
+      staged = version >= 0 && ch.stage_refresh_from[server_id];
+      if (version >= 0 && !config_.read_my_writes && !staged) {
         // The server's published master version becomes the live copy of
         // this shard, read in place by the segmented gather: no copy.  It is
         // never rewritten while we hold it; the one it replaces goes back.
@@ -1064,7 +1087,9 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
         }
       } else {
         // Copy into the cache (recv_row_batch_gpu, clientlib-data.cpp:110-151):
-        // rows from a socket, or read-my-writes, which re-applies this
+        // rows from a socket; a same-node server on another GPU (staged: one
+        // peer copy over xGMI per refresh, then every Read of the clock
+        // gathers from local HBM); or read-my-writes, which re-applies this
         // client's own not-yet-reflected updates on top of the shard and so
         // needs a private copy (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
         GP_CHECK_MSG(pc.data.size() == pc.num_rows * ROW_DATA_SIZE,
@@ -1096,6 +1121,7 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_refresh++;
   if (in_place) stats_.nr_refresh_in_place++;
+  if (staged) stats_.nr_refresh_staged++;
   stats_.refresh_time += now_s() - t0;
   return released;
 }

@@ -105,6 +105,7 @@ struct ParamCache {
 struct ClientStats {
   uint64_t nr_read = 0, nr_update = 0, nr_clock = 0, nr_push = 0, nr_refresh = 0;
   uint64_t nr_refresh_in_place = 0;  // refreshes read in place from the server's master version
+  uint64_t nr_refresh_staged = 0;    // same-node refreshes peer-copied into the cache (staged)
   uint64_t rows_updated = 0, rows_read = 0, bytes_pushed_remote = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
@@ -160,9 +161,16 @@ struct Channel {
   // IPC handles it already has
   std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
   std::vector<uint8_t> ipc_client;                       // [client]
-  // [client]: its oplog lives on another GPU: stage its slices into local HBM
-  // (a peer copy over xGMI on the server's copy stream) before the sum
+  // [process]: runs on another GPU of this node (its hello's PCI bus id)
+  std::vector<uint8_t> other_gpu;
+  // [client]: stage its oplog slices into local HBM (a peer copy over xGMI on
+  // the server's copy stream) before the sum, instead of the sum reading them
+  // in place (GEEPS_STAGE_PEER_UPDATES; default: when it is on another GPU)
   std::vector<uint8_t> stage_from;
+  // [server]: copy its refreshed shard into this client's cache (one peer copy
+  // per refresh) instead of reading the master version in place on every Read
+  // (GEEPS_STAGE_PEER_REFRESH; default: when it is on another GPU)
+  std::vector<uint8_t> stage_refresh_from;
   std::vector<std::vector<std::set<int>>> version_sent;  // [client][table]
   // [client]: its SHUTDOWN arrived (it reads no more, and its ACKs stop)
   std::vector<uint8_t> client_done;
@@ -230,7 +238,11 @@ class ClientLib {
   const uint32_t num_channels_;
   int device_ = 0;
   char pci_bus_id_[32] = {};  // this process's GPU (gp_device_pci_bus_id)
-  bool force_stage_ = false;  // GEEPS_STAGE_PEER_UPDATES=1 (test hook)
+  // peer staging modes: -1 = on another GPU only (default), 0 = never (read
+  // the peer's HBM in place over xGMI), 1 = always (tests the cross-GPU path
+  // on one GPU): GEEPS_STAGE_PEER_UPDATES (buckets), GEEPS_STAGE_PEER_REFRESH
+  int stage_updates_mode_ = -1;
+  int stage_refresh_mode_ = -1;
   int reader_delay_us_ = 0;   // GEEPS_TEST_READER_DELAY_US (test hook)
   std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)
 

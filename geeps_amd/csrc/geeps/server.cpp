@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <future>
 #include <iostream>
@@ -16,6 +17,17 @@ namespace {
 double now_s() {
   using namespace std::chrono;
   return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+// How long free_version waits with no release at all before it gives up:
+// GEEPS_VERSION_WAIT_S seconds (default 300).
+double version_wait_limit_s() {
+  static const double limit = [] {
+    const char *v = std::getenv("GEEPS_VERSION_WAIT_S");
+    const double d = v ? std::atof(v) : 0.0;
+    return d > 0 ? d : 300.0;
+  }();
+  return limit;
 }
 }  // namespace
 
@@ -93,6 +105,7 @@ void TabletServer::release(uint32_t client_id, uint32_t table_id, int version) {
                "client " << client_id << " releases master version " << version << " of table "
                          << table_id << " it does not hold");
   t.holders[version][client_id] = 0;
+  ++releases_;
   release_cv_.notify_all();
 }
 
@@ -101,6 +114,7 @@ void TabletServer::release_all(uint32_t client_id) {
   GP_CHECK_LT(client_id, num_clients_);
   for (auto &t : tables_)
     for (auto &h : t.holders) h[client_id] = 0;
+  ++releases_;
   release_cv_.notify_all();
 }
 
@@ -190,9 +204,14 @@ void TabletServer::run() {
   }
 }
 
+// A staging bucket no pending bucket references.  At most kMaxPendingBuckets
+// exist per table (the queue is applied when it reaches that many, which
+// frees them all); the client's memory plan counts them (client.cpp,
+// FinishVirtualIteration).
 std::shared_ptr<DeviceArray<float>> TabletServer::stage_buffer(DataTable &t) {
   for (auto &b : t.stage_pool)
     if (b.use_count() == 1) return b;  // not referenced by a pending bucket
+  GP_CHECK_LT(t.stage_pool.size(), kMaxPendingBuckets);
   t.stage_pool.push_back(std::make_shared<DeviceArray<float>>(t.row_count * ROW_DATA_SIZE));
   return t.stage_pool.back();
 }
@@ -259,10 +278,16 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
 
 // A version no client holds, other than the current one; a new one when
 // every version is held and fewer than clients + 2 exist; otherwise wait for
-// a release (see server.hpp: it always comes, from a reader thread).
+// a release (see server.hpp: it comes from a reader thread catching up).  The
+// wait is bounded: every release restarts the clock, and after
+// version_wait_limit_s() with none the server fails loudly with the holders
+// matrix (a reader thread stuck or dead without a SHUTDOWN) instead of
+// stalling the channel forever.
 int TabletServer::free_version(DataTable &t) {
   std::unique_lock<std::mutex> lk(hold_mu_);
   const double t0 = now_s();
+  double progress_t = t0;
+  uint64_t seen = releases_;
   for (;;) {
     for (size_t v = 0; v < t.versions.size(); ++v) {
       if ((int)v == t.cur) continue;
@@ -282,6 +307,21 @@ int TabletServer::free_version(DataTable &t) {
     if (release_cv_.wait_for(lk, std::chrono::milliseconds(12000)) == std::cv_status::timeout)
       std::cerr << "tablet server " << server_id_ << " channel " << channel_id_
                 << ": every master version is held; waiting for a client to release one\n";
+    const double now = now_s();
+    if (releases_ != seen) {
+      seen = releases_;
+      progress_t = now;
+    } else if (now - progress_t > version_wait_limit_s()) {
+      std::ostringstream o;
+      o << "tablet server " << server_id_ << " channel " << channel_id_ << ": no master version "
+        << "released for " << (now - progress_t) << " s (GEEPS_VERSION_WAIT_S); holders "
+        << "[version][client]:";
+      for (size_t v = 0; v < t.holders.size(); ++v) {
+        o << " v" << v << ((int)v == t.cur ? "*" : "") << "=";
+        for (uint8_t h : t.holders[v]) o << (h ? '1' : '0');
+      }
+      GP_CHECK_MSG(false, o.str());
+    }
   }
 }
 

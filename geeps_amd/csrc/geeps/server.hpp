@@ -207,6 +207,7 @@ class TabletServer {
   std::deque<Msg> queue_;
   std::mutex hold_mu_;  // DataTable::holders (and the versions vector's size)
   std::condition_variable release_cv_;  // a hold ended (release / release_all)
+  uint64_t releases_ = 0;               // holds ended so far (hold_mu_): reader progress
   std::unique_ptr<Stream> copy_stream_;  // peer copies of other GPUs' buckets
   uint32_t shutdown_count_ = 0;  // server thread only
   bool shutdown_done_ = false;    // guarded by mu_

@@ -643,9 +643,9 @@ int launch_bucket_sum(float *out, const float *in, const float *const *bk,
 // write_bytes / write_rate.
 // ---------------------------------------------------------------------------
 constexpr int kProbeU = 4;
+__device__ float g_probe_sink[64];  // the read probe's sink: never the probed buffer
 
-__global__ __launch_bounds__(kBlock) void hbm_read_probe_kernel(const f4 *__restrict__ in, size_t n4,
-                                                               float *__restrict__ sink) {
+__global__ __launch_bounds__(kBlock) void hbm_read_probe_kernel(const f4 *__restrict__ in, size_t n4) {
   const size_t tile = (size_t)kBlock * kProbeU;
   const size_t stride = (size_t)gridDim.x * tile;
   f4 acc = f4(0.0f);
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(kBlock) void hbm_read_probe_kernel(const f4 *__rest
   for (int u = 0; u < kProbeU; ++u)
     if (base + u * kBlock < n4) acc += __builtin_nontemporal_load(in + base + u * kBlock);
   // data-dependent, practically never true: keeps every load live
-  if (acc.x + acc.y + acc.z + acc.w == -1234.5f) sink[blockIdx.x % 64] = acc.x;
+  if (acc.x + acc.y + acc.z + acc.w == -1234.5f) g_probe_sink[blockIdx.x % 64] = acc.x;
 }
 
 // ---------------------------------------------------------------------------
@@ -1691,11 +1691,10 @@ int gp_hbm_probe(int kind, float *buffer, size_t num_vals, gp_stream s) {
   if (num_vals == 0) return GP_OK;
   if (!buffer || !aligned16(buffer)) return set_error(GP_ERR_INVALID, "null or unaligned buffer");
   if (kind == GP_PROBE_READ) {
-    // the sink: the first 64 floats of the buffer, written only if the sum of
-    // a thread's loads hits -1234.5 exactly
+    // the buffer is only read (the kernel's sink is a device global of its own)
     const size_t grid = (size_t)num_cus() * 2;
     hipLaunchKernelGGL(hbm_read_probe_kernel, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)s,
-                       reinterpret_cast<const f4 *>(buffer), num_vals / 4, buffer);
+                       reinterpret_cast<const f4 *>(buffer), num_vals / 4);
   } else if (kind == GP_PROBE_WRITE) {
     // the runtime's fill kernel: 6.3-6.7 TB/s, above every store-loop shape
     // tried (5.5-6.3 TB/s; profiles/r02/tune/probe_tune*.txt)

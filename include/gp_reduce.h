@@ -311,9 +311,8 @@ int gp_add(size_t n, const float *a, const float *b, float *y, gp_stream s);
 
 /* HBM probe for measurement tools: stream `num_vals` floats of a 16-B
  * aligned device buffer once, read-only (GP_PROBE_READ: 16-B non-temporal
- * loads; the buffer is left unchanged in practice: its first 64 floats are
- * written only if a thread's running sum lands exactly on -1234.5) or
- * write-only (GP_PROBE_WRITE: zeros, through the runtime's fill kernel).
+ * loads; the buffer is not written) or write-only (GP_PROBE_WRITE: zeros,
+ * through the runtime's fill kernel).
  * bench.py times both to model every kernel's bytes on the same box.  No
  * reference counterpart. */
 #define GP_PROBE_READ 0

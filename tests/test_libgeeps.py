@@ -355,6 +355,25 @@ def test_peer_buckets_staged_into_local_hbm(dev, P, slack, channels):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P,slack,channels,updates", [(2, 0, 1, "1"), (3, 1, 2, "0"), (4, 2, 1, "1")])
+def test_peer_refresh_staged_into_local_cache(dev, P, slack, channels, updates):
+    """The cross-GPU refresh path (the all-gather leg): a same-node server's
+    published master version is peer-copied once per refresh into the
+    client's own cache, so every Read of the clock gathers local HBM (forced on
+    one GPU by GEEPS_STAGE_PEER_REFRESH=1), and the version goes back at once.
+    Combined with bucket staging on ("1") and with the in-place xGMI bucket
+    read ("0", GEEPS_STAGE_PEER_UPDATES=0).  Exact sums / SSP bounds; every
+    process staged refreshes from its peers, and with "0" no server staged
+    buckets."""
+    outs = _run_app(P, rows=900, clocks=10, slack=slack, channels=channels, rmw=0, transport="ipc",
+                    extra_env={"GEEPS_STAGE_PEER_REFRESH": "1", "GEEPS_STAGE_PEER_UPDATES": updates})
+    for s in _stats(outs):
+        assert s["client"]["nr_refresh_staged"] > 0
+        staged = [srv["nr_peer_staged"] for srv in s["servers"]]
+        assert all(n > 0 for n in staged) if updates == "1" else all(n == 0 for n in staged)
+
+
+@pytest.mark.gpu
 def test_one_process_per_gpu(dev):
     """One process per GPU (process p on device p % count), as on an 8-GPU
     node: peers' buckets cross xGMI by the staged peer copy and refreshes are
