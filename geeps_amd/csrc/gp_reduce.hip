@@ -1427,6 +1427,406 @@ int launch_gather_planned(float *y, const float *x, const gp_row_segments *xs,
   return GP_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Device-built plans for the unplanned calls (gp_scatter_add_rows,
+// gp_scatter_init_rows, gp_gather_rows): the reference's own binding passes a
+// device DoubleIndex on every call (add_rows_from_double_index_gpu,
+// row-op-util.cu:127-142, synchronous at :141), with no host copy to compile a
+// gp_row_plan from.  A large call therefore plans itself on the device first:
+//  1. index_scan_kernel reads the index once (16 B per row) and writes, per
+//     64-entry tile, whether it is dense (id0 and id1 both step by one, every
+//     row clear of num_vals_limit), whether it continues the tile before, and
+//     whether its destinations ascend; plus the first entry of every tile that
+//     starts a dense run, and the largest destination row.
+//  2. One D2H of that summary and a stream sync (the reference's call syncs
+//     too); the host turns it into runs, exactly like build_row_plan.
+//  3. Dense runs of at least kDenseRunBytes go to the phase-separated sum
+//     kernels (1 bucket, the zero-input form, the copy), as in a row plan.
+//  4. The other rows: a scatter-add whose destinations are not mostly sorted
+//     is binned by destination on the device first (a counting sort by
+//     destination row >> s into a workspace: histogram, scan, scatter), so
+//     the wave-map kernel walks y nearly front to back as it does for a
+//     plan's sorted residual; otherwise the rows go to the row kernels as they
+//     are.  Binning changes the order rows are visited in, which is bit-neutral
+//     under the call's precondition (distinct destinations).
+// Calls below kAnalyzeMinBytes (gp_set_unplanned_min_bytes) skip all this.
+// ---------------------------------------------------------------------------
+constexpr int kScanGroupTiles = 64;  // tiles of 64 entries per scan word
+constexpr int kMaxRunStarts = 512;   // run-start entries the scan records
+constexpr int kMaxDeviceRuns = 32;   // dense runs a call sweeps (the longest)
+constexpr int kBinShiftRows = 12;    // destination bins of 4096 rows (2 MiB of RowData)
+constexpr size_t kBinMinBytes = 16u << 20;  // smaller residuals are not binned
+
+struct ScanHeader {
+  unsigned long long max_dst;
+  unsigned int n_starts;
+  unsigned int pad;
+};
+struct RunStart {
+  uint64_t tile, from, to;
+};
+// workspace: [ScanHeader][RunStart x kMaxRunStarts][3 words per 64 tiles]
+constexpr size_t kScanWordsOff = sizeof(ScanHeader) + sizeof(RunStart) * kMaxRunStarts;
+
+std::atomic<size_t> g_analyze_min_bytes{64u << 20};
+
+// The endpoints of entry e (offsets applied) and whether its guarded row is
+// whole; dead entries (e >= n) are not whole.
+template <int OP>
+__device__ __forceinline__ bool scan_entry(const gp_double_index *idx, size_t n, size_t e, uint64_t off0,
+                                           uint64_t off1, size_t row_size, size_t limit, uint64_t &from,
+                                           uint64_t &to) {
+  from = to = 0;
+  if (e >= n) return false;
+  row_endpoints<OP>(idx[e], off0, off1, from, to);
+  return ((OP == kAssignTo ? to : from) + 1) * row_size <= limit;
+}
+
+// One wave per group of 64 tiles (4096 entries): three 64-bit words per group
+// (bit k = tile 64 g + k): dense, continues the previous tile, destinations
+// ascend (inside the tile and from the previous tile's last entry).
+template <int OP>
+__global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_index *__restrict__ idx, size_t n,
+                                                            uint64_t off0, uint64_t off1, size_t row_size,
+                                                            size_t limit, char *__restrict__ ws) {
+  ScanHeader *hdr = reinterpret_cast<ScanHeader *>(ws);
+  RunStart *starts = reinterpret_cast<RunStart *>(ws + sizeof(ScanHeader));
+  uint64_t *words = reinterpret_cast<uint64_t *>(ws + kScanWordsOff);
+  const int wl = threadIdx.x & 63;
+  const size_t tiles = (n + 63) / 64;
+  const size_t groups = (tiles + kScanGroupTiles - 1) / kScanGroupTiles;
+  const size_t wave = ((size_t)blockIdx.x * kBlock + threadIdx.x) / 64;
+  const size_t wstride = (size_t)gridDim.x * (kBlock / 64);
+  unsigned long long mx = 0;
+  for (size_t g = wave; g < groups; g += wstride) {
+    const size_t t0 = g * kScanGroupTiles;
+    // the tile before the group: its last entry and whether it is dense
+    uint64_t pf = 0, pt = 0;  // previous entry (lane 63 of the previous tile)
+    bool prev_dense = false;
+    if (t0 > 0) {
+      uint64_t f, t;
+      const bool w = scan_entry<OP>(idx, n, (t0 - 1) * 64 + wl, off0, off1, row_size, limit, f, t);
+      const uint64_t lf = shfl64(f, (wl + 63) & 63), lt = shfl64(t, (wl + 63) & 63);
+      prev_dense = __all(w && (wl == 0 || (f == lf + 1 && t == lt + 1)));
+      pf = shfl64(f, 63);
+      pt = shfl64(t, 63);
+    }
+    uint64_t wd = 0, wc = 0, ws_ = 0;
+    for (int k = 0; k < kScanGroupTiles; ++k) {
+      const size_t t = t0 + k;
+      if (t >= tiles) break;  // wave-uniform
+      const size_t e = t * 64 + wl;
+      uint64_t f, to;
+      const bool whole = scan_entry<OP>(idx, n, e, off0, off1, row_size, limit, f, to);
+      const bool live = e < n;
+      const uint64_t lf = shfl64(f, (wl + 63) & 63), lt = shfl64(to, (wl + 63) & 63);
+      const uint64_t bf = wl == 0 ? pf : lf, bt = wl == 0 ? pt : lt;  // the entry before this one
+      const bool has_before = e > 0;
+      const bool step = has_before && f == bf + 1 && to == bt + 1;
+      const bool dense = __all(whole && (wl == 0 || step));
+      const bool cont = __shfl(step ? 1 : 0, 0, 64) != 0;  // lane 0: continues the previous tile
+      const bool asc = __all(!live || !has_before || to > bt);
+      if (live && to > mx) mx = to;
+      if (dense) wd |= 1ull << k;
+      if (cont) wc |= 1ull << k;
+      if (asc) ws_ |= 1ull << k;
+      if (dense && !(cont && prev_dense) && wl == 0) {
+        const unsigned slot = atomicAdd(&hdr->n_starts, 1u);
+        if (slot < (unsigned)kMaxRunStarts) starts[slot] = RunStart{t, f, to};
+      }
+      prev_dense = dense;
+      pf = shfl64(f, 63);
+      pt = shfl64(to, 63);
+    }
+    if (wl == 0) {
+      words[3 * g] = wd;
+      words[3 * g + 1] = wc;
+      words[3 * g + 2] = ws_;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long v = shfl64(mx, (wl + o) & 63);
+    mx = v > mx ? v : mx;
+  }
+  if (wl == 0) atomicMax(&hdr->max_dst, mx);
+}
+
+// Residual rows of a call: up to kMaxDeviceRuns + 1 entry ranges, passed by
+// value; `pre[i]` = rows in ranges before i.
+struct EntryRanges {
+  uint32_t count;
+  uint64_t lo[kMaxDeviceRuns + 1], hi[kMaxDeviceRuns + 1], pre[kMaxDeviceRuns + 2];
+};
+
+__device__ __forceinline__ size_t range_entry(const EntryRanges &r, size_t k) {
+  uint32_t i = 0;
+  while (i + 1 < r.count && r.pre[i + 1] <= k) ++i;
+  return r.lo[i] + (k - r.pre[i]);
+}
+
+constexpr int kBinLds = 16384;  // bins counted in LDS (64 KiB)
+
+// Counting sort of the residual rows by destination row >> shift: per-bin
+// counts (LDS per block, then global atomics).
+template <int OP>
+__global__ __launch_bounds__(kBlock) void bin_count_kernel(const gp_double_index *__restrict__ idx,
+                                                           EntryRanges rr, uint64_t off0, uint64_t off1,
+                                                           int shift, uint32_t nbins, uint32_t *__restrict__ count,
+                                                           size_t per_block) {
+  __shared__ uint32_t h[kBinLds];
+  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock) h[b] = 0;
+  __syncthreads();
+  const size_t total = rr.pre[rr.count];
+  const size_t lo = (size_t)blockIdx.x * per_block, hi = min(lo + per_block, total);
+  for (size_t k = lo + threadIdx.x; k < hi; k += kBlock) {
+    uint64_t f, t;
+    row_endpoints<OP>(idx[range_entry(rr, k)], off0, off1, f, t);
+    atomicAdd(&h[(uint32_t)(t >> shift)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock)
+    if (h[b]) atomicAdd(&count[b], h[b]);
+}
+
+// One block: exclusive scan of the counts into cursors (nbins <= kBinLds).
+__global__ __launch_bounds__(1024) void bin_scan_kernel(const uint32_t *__restrict__ count, uint32_t nbins,
+                                                        uint32_t *__restrict__ cursor) {
+  __shared__ uint32_t part[1024];
+  const uint32_t per = (nbins + 1023) / 1024;
+  const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nbins);
+  uint32_t s = 0;
+  for (uint32_t b = lo; b < hi; ++b) s += count[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (uint32_t b = lo; b < hi; ++b) {
+    cursor[b] = run;
+    run += count[b];
+  }
+}
+
+// Each block reserves its rows' slots per bin, then places them (order inside
+// a bin is arbitrary).  Entries are written with the offsets applied.
+template <int OP>
+__global__ __launch_bounds__(kBlock) void bin_place_kernel(const gp_double_index *__restrict__ idx,
+                                                           EntryRanges rr, uint64_t off0, uint64_t off1,
+                                                           int shift, uint32_t nbins, uint32_t *__restrict__ cursor,
+                                                           gp_double_index *__restrict__ out, size_t per_block) {
+  __shared__ uint32_t h[kBinLds];
+  __shared__ uint32_t base[kBinLds];
+  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock) h[b] = 0;
+  __syncthreads();
+  const size_t total = rr.pre[rr.count];
+  const size_t lo = (size_t)blockIdx.x * per_block, hi = min(lo + per_block, total);
+  for (size_t k = lo + threadIdx.x; k < hi; k += kBlock) {
+    uint64_t f, t;
+    row_endpoints<OP>(idx[range_entry(rr, k)], off0, off1, f, t);
+    atomicAdd(&h[(uint32_t)(t >> shift)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock) {
+    base[b] = h[b] ? atomicAdd(&cursor[b], h[b]) : 0;
+    h[b] = 0;
+  }
+  __syncthreads();
+  for (size_t k = lo + threadIdx.x; k < hi; k += kBlock) {
+    const gp_double_index ix = idx[range_entry(rr, k)];
+    uint64_t f, t;
+    row_endpoints<OP>(ix, off0, off1, f, t);
+    const uint32_t b = (uint32_t)(t >> shift);
+    out[base[b] + atomicAdd(&h[b], 1u)] = OP == kAssignTo ? gp_double_index{t, f} : gp_double_index{f, t};
+  }
+}
+
+// Thread-local pinned landing buffer for the scan summary (a call's D2H is
+// complete, after its sync, before the same thread issues the next).
+struct PinnedScratch {
+  void *p = nullptr;
+  size_t bytes = 0;
+  ~PinnedScratch() {
+    if (p) (void)hipHostFree(p);
+  }
+  void *get(size_t need) {
+    if (need > bytes) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      bytes = 0;
+      if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return nullptr;
+      bytes = need;
+    }
+    return p;
+  }
+};
+thread_local PinnedScratch g_scan_landing;
+
+// The workspaces come from the device's default stream-ordered pool
+// (hipMallocAsync / hipFreeAsync, safe across streams); keep what it holds
+// instead of returning it to the driver at every sync (release threshold 0
+// by default), so a call's allocations are pool hits after the first.
+std::atomic<bool> g_pool_kept[kMaxDevices];
+
+void keep_pool_memory() {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
+  if (g_pool_kept[dev].exchange(true)) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return;
+  uint64_t keep = UINT64_MAX;
+  (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+}
+
+struct DevRun {
+  uint64_t e0, rows, from, to;  // first entry, rows, endpoints of the first entry
+};
+
+// The analysed form of launch_row_op (see the section comment).
+template <int OP>
+int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx, size_t n, gp_double_index off,
+                           size_t row_size, size_t limit, hipStream_t s) {
+  const size_t W = row_size;
+  const size_t tiles = (n + 63) / 64, groups = (tiles + kScanGroupTiles - 1) / kScanGroupTiles;
+  keep_pool_memory();
+  const size_t scan_bytes = kScanWordsOff + groups * 3 * sizeof(uint64_t);
+  char *ws = nullptr;
+  GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), scan_bytes, s));
+  struct Free {  // the workspace goes back in stream order, whatever happens
+    char *&p;
+    hipStream_t s;
+    ~Free() {
+      if (p) (void)hipFreeAsync(p, s);
+    }
+  } free_ws{ws, s};
+  GP_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(ScanHeader), s));
+  {
+    const size_t waves = std::max<size_t>(1, std::min(groups, (size_t)num_cus() * 16));
+    const size_t grid = (waves + (kBlock / 64) - 1) / (kBlock / 64);
+    hipLaunchKernelGGL(index_scan_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, n, off.id0, off.id1,
+                       W, limit, ws);
+    GP_HIP_TRY(hipGetLastError());
+  }
+  char *h = static_cast<char *>(g_scan_landing.get(scan_bytes));
+  if (!h) return set_error(GP_ERR_HIP, "pinned scan buffer");
+  GP_HIP_TRY(hipMemcpyAsync(h, ws, scan_bytes, hipMemcpyDeviceToHost, s));
+  GP_HIP_TRY(hipStreamSynchronize(s));
+  const ScanHeader hdr = *reinterpret_cast<const ScanHeader *>(h);
+  const RunStart *st = reinterpret_cast<const RunStart *>(h + sizeof(ScanHeader));
+  const uint64_t *words = reinterpret_cast<const uint64_t *>(h + kScanWordsOff);
+  auto bit = [&](size_t t, int w) { return (words[3 * (t / kScanGroupTiles) + w] >> (t % kScanGroupTiles)) & 1; };
+
+  // dense runs at tile granularity, long enough for the sweep forms, whose
+  // first entry the scan recorded; the longest kMaxDeviceRuns of them
+  const size_t min_tiles = std::max<size_t>(1, kDenseRunBytes / (64 * W * sizeof(float)));
+  std::vector<DevRun> runs;
+  {
+    const unsigned ns = std::min<unsigned>(hdr.n_starts, kMaxRunStarts);
+    std::vector<RunStart> starts(st, st + ns);
+    std::sort(starts.begin(), starts.end(), [](const RunStart &a, const RunStart &b) { return a.tile < b.tile; });
+    for (const RunStart &r : starts) {
+      size_t t = r.tile + 1;
+      while (t < tiles && bit(t, 0) && bit(t, 1)) ++t;
+      if (t - r.tile >= min_tiles) {
+        const uint64_t e0 = r.tile * 64, rows = std::min<uint64_t>((t - r.tile) * 64, n - e0);
+        runs.push_back(DevRun{e0, rows, r.from, r.to});
+      }
+    }
+    if (runs.size() > (size_t)kMaxDeviceRuns) {
+      std::nth_element(runs.begin(), runs.begin() + kMaxDeviceRuns, runs.end(),
+                       [](const DevRun &a, const DevRun &b) { return a.rows > b.rows; });
+      runs.resize(kMaxDeviceRuns);
+      std::sort(runs.begin(), runs.end(), [](const DevRun &a, const DevRun &b) { return a.e0 < b.e0; });
+    }
+  }
+  for (const DevRun &r : runs) {
+    BucketPtrs b = {};
+    b.p[0] = x + r.from * W;
+    float *yr = y + r.to * W;
+    int rc;
+    if constexpr (OP == kAddFrom)
+      rc = launch_bucket_sum_nb<1>(yr, yr, b, r.rows * W, s);
+    else if constexpr (OP == kInitFrom)
+      rc = launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s);
+    else
+      rc = launch_bucket_sum_nb<0>(yr, x + r.from * W, BucketPtrs{}, r.rows * W, s);
+    if (rc != GP_OK) return rc;
+  }
+  // the residual: entry ranges between the runs
+  EntryRanges rr = {};
+  {
+    uint64_t at = 0;
+    rr.pre[0] = 0;
+    auto add = [&](uint64_t lo, uint64_t hi) {
+      if (hi <= lo) return;
+      rr.lo[rr.count] = lo;
+      rr.hi[rr.count] = hi;
+      rr.pre[rr.count + 1] = rr.pre[rr.count] + (hi - lo);
+      ++rr.count;
+    };
+    for (const DevRun &r : runs) {
+      add(at, r.e0);
+      at = r.e0 + r.rows;
+    }
+    add(at, n);
+  }
+  const size_t resid = rr.pre[rr.count];
+  if (resid == 0) return GP_OK;
+  // destinations already (mostly) ascending: keep the call's order
+  size_t resid_tiles = 0, asc_tiles = 0;
+  for (uint32_t i = 0; i < rr.count; ++i)
+    for (size_t t = rr.lo[i] / 64; t < (rr.hi[i] + 63) / 64; ++t) {
+      ++resid_tiles;
+      asc_tiles += bit(t, 2);
+    }
+  const bool ascending = asc_tiles * 10 >= resid_tiles * 9;
+  if (OP != kAddFrom || ascending || resid * W * sizeof(float) < kBinMinBytes) {
+    for (uint32_t i = 0; i < rr.count; ++i) {
+      const int rc = launch_row_op<OP>(y, x, idx + rr.lo[i], rr.hi[i] - rr.lo[i], off, W, limit, s, ascending);
+      if (rc != GP_OK) return rc;
+    }
+    return GP_OK;
+  }
+  // bin the scatter-add's residual by destination, then the sorted-residual kernel
+  int shift = kBinShiftRows;
+  while (((hdr.max_dst >> shift) + 1) > (uint64_t)kBinLds) ++shift;
+  const uint32_t nbins = (uint32_t)((hdr.max_dst >> shift) + 1);
+  char *bws = nullptr;
+  const size_t bin_bytes = resid * sizeof(gp_double_index) + 2 * (size_t)nbins * sizeof(uint32_t);
+  GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&bws), bin_bytes, s));
+  Free free_bins{bws, s};
+  gp_double_index *binned = reinterpret_cast<gp_double_index *>(bws);
+  uint32_t *count = reinterpret_cast<uint32_t *>(bws + resid * sizeof(gp_double_index));
+  uint32_t *cursor = count + nbins;
+  GP_HIP_TRY(hipMemsetAsync(count, 0, nbins * sizeof(uint32_t), s));
+  const size_t nb = std::max<size_t>(1, std::min((size_t)num_cus() * 4, (resid + 4095) / 4096));
+  const size_t per = (resid + nb - 1) / nb;
+  hipLaunchKernelGGL(bin_count_kernel<OP>, dim3((unsigned)nb), dim3(kBlock), 0, s, idx, rr, off.id0, off.id1, shift,
+                     nbins, count, per);
+  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, s, count, nbins, cursor);
+  hipLaunchKernelGGL(bin_place_kernel<OP>, dim3((unsigned)nb), dim3(kBlock), 0, s, idx, rr, off.id0, off.id1, shift,
+                     nbins, cursor, binned, per);
+  GP_HIP_TRY(hipGetLastError());
+  return launch_row_op<OP>(y, x, binned, resid, gp_double_index{0, 0}, W, limit, s, /*sorted=*/true);
+}
+
+// The unplanned calls: large ones plan themselves on the device.
+template <int OP>
+int launch_row_op_unplanned(float *y, const float *x, const gp_double_index *idx, size_t n, gp_double_index off,
+                            size_t row_size, size_t limit, hipStream_t s) {
+  if (n == 0) return GP_OK;
+  if (!y || !x || !idx) return set_error(GP_ERR_INVALID, "null pointer");
+  if (row_size == 0) return set_error(GP_ERR_INVALID, "row_size == 0");
+  const size_t min_bytes = g_analyze_min_bytes.load(std::memory_order_relaxed);
+  if (min_bytes != SIZE_MAX && n * row_size * sizeof(float) >= min_bytes && row_size % 4 == 0 && aligned16(y) &&
+      aligned16(x))
+    return launch_row_op_analyzed<OP>(y, x, idx, n, off, row_size, limit, s);
+  return launch_row_op<OP>(y, x, idx, n, off, row_size, limit, s);
+}
+
 int create_plan(gp_row_plan *plan, const gp_double_index *host_index, size_t num_rows,
                 gp_double_index offset, size_t row_size, size_t num_vals_limit, bool gather);
 
@@ -1439,19 +1839,24 @@ extern "C" {
 
 int gp_abi_version(void) { return GP_ABI_VERSION; }
 
+int gp_set_unplanned_min_bytes(size_t min_bytes) {
+  g_analyze_min_bytes.store(min_bytes, std::memory_order_relaxed);
+  return GP_OK;
+}
+
 const char *gp_last_error(void) { return g_last_error.c_str(); }
 
 int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
                         size_t num_rows, gp_double_index offset,
                         size_t row_size, size_t num_vals_limit, gp_stream s) {
-  return launch_row_op<kAddFrom>(y, x, index, num_rows, offset, row_size,
+  return launch_row_op_unplanned<kAddFrom>(y, x, index, num_rows, offset, row_size,
                                  num_vals_limit, (hipStream_t)s);
 }
 
 int gp_gather_rows(float *y, const float *x, const gp_double_index *index,
                    size_t num_rows, gp_double_index offset, size_t row_size,
                    size_t num_vals_limit, gp_stream s) {
-  return launch_row_op<kAssignTo>(y, x, index, num_rows, offset, row_size,
+  return launch_row_op_unplanned<kAssignTo>(y, x, index, num_rows, offset, row_size,
                                   num_vals_limit, (hipStream_t)s);
 }
 
@@ -1465,7 +1870,7 @@ int gp_scatter_rows(float *y, const float *x, const gp_double_index *index,
 int gp_scatter_init_rows(float *y, const float *x, const gp_double_index *index,
                          size_t num_rows, gp_double_index offset, size_t row_size,
                          size_t num_vals_limit, gp_stream s) {
-  return launch_row_op<kInitFrom>(y, x, index, num_rows, offset, row_size,
+  return launch_row_op_unplanned<kInitFrom>(y, x, index, num_rows, offset, row_size,
                                   num_vals_limit, (hipStream_t)s);
 }
 

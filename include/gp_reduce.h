@@ -60,6 +60,11 @@ typedef void *gp_event;
 
 int gp_abi_version(void);
 const char *gp_last_error(void);
+/* ABI 10: the size from which gp_scatter_add_rows / gp_scatter_init_rows /
+ * gp_gather_rows plan themselves on the device (num_rows * row_size * 4
+ * bytes; default 64 MiB; SIZE_MAX: never).  Process-wide; for tests and
+ * measurement. */
+int gp_set_unplanned_min_bytes(size_t min_bytes);
 
 /* ---------------------------------------------------------------------------
  * Row operations (client side).  Element (row r, value v) lives at
@@ -77,7 +82,15 @@ const char *gp_last_error(void);
  * (src/common/row-op-util.hpp:121-139).
  * Precondition (as for the reference kernel, whose threads race on a repeated
  * destination): destination rows index[r].id1 are distinct within one call.
- * `index` is a DEVICE pointer.  num_rows == 0 is a no-op. */
+ * `index` is a DEVICE pointer.  num_rows == 0 is a no-op.
+ * Calls of at least gp_set_unplanned_min_bytes() of rows (default 64 MiB)
+ * plan themselves on the device (ABI 10): one pass over the index finds its
+ * dense runs (moved like a row plan's, by the phase-separated sum kernels) and
+ * whether the other rows' destinations ascend (if not, they are binned by
+ * destination on the device first).  Such a call waits for the stream once,
+ * for the index summary, as the reference's call waits at its end
+ * (row-op-util.cu:141); smaller calls are fully asynchronous.  Same results
+ * either way. */
 int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
                         size_t num_rows, gp_double_index offset,
                         size_t row_size, size_t num_vals_limit, gp_stream s);
@@ -90,8 +103,8 @@ int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
  * gp_scatter_add_rows (0.0f + x maps -0.0 to +0.0 exactly as the add does).
  * Destinations NOT listed are left untouched (not zeroed): the caller uses it
  * only when the clock's update ops cover every oplog row exactly once
- * (client.cpp, FinishVirtualIteration).  Same index semantics and precondition
- * as gp_scatter_add_rows. */
+ * (client.cpp, FinishVirtualIteration).  Same index semantics, precondition
+ * and large-call planning as gp_scatter_add_rows. */
 int gp_scatter_init_rows(float *y, const float *x, const gp_double_index *index,
                          size_t num_rows, gp_double_index offset,
                          size_t row_size, size_t num_vals_limit, gp_stream s);
@@ -101,7 +114,8 @@ int gp_scatter_init_rows(float *y, const float *x, const gp_double_index *index,
  *     if (to*row_size + v < num_vals_limit)
  *       y[to*row_size + v] = x[from*row_size + v];
  * Replaces assign_rows_to_double_index_gpu (src/common/row-op-util.hpp:141-145,
- * src/common/row-op-util.cu:39-72); CPU twin :81-99. */
+ * src/common/row-op-util.cu:39-72); CPU twin :81-99.  Large calls plan
+ * themselves as gp_scatter_add_rows does (dense runs copied by the sweep). */
 int gp_gather_rows(float *y, const float *x, const gp_double_index *index,
                    size_t num_rows, gp_double_index offset, size_t row_size,
                    size_t num_vals_limit, gp_stream s);

@@ -597,6 +597,93 @@ def _plan_index(rng, kind, n_cache, W):
     return idx[rng.permutation(idx.shape[0])].astype(np.int64), idx.shape[0]
 
 
+def _op_order_index(rng, kind, n, W):
+    """An index in op order for the unplanned calls' device plans: identity;
+    a random permutation of destinations; destinations ascending with gaps and
+    random sources ("sorted"); or "runs": three dense runs (>= 4 MiB each, the
+    second's destinations below the first's) with scattered rows between and
+    around them, all in op order."""
+    if kind == "identity":
+        return np.stack([np.arange(n), np.arange(n)], 1).astype(np.int64)
+    if kind == "permuted":
+        return np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64)
+    if kind == "sorted":
+        dst = np.sort(rng.choice(n + n // 3, n, replace=False))
+        return np.stack([rng.permutation(n), dst], 1).astype(np.int64)
+    run = (4 << 20) // (W * 4) + 130
+    assert n > 3 * run + 3000
+    runs_dst = [2 * run + 50, 3, 3 * run + 500]  # destination starts, out of order
+    used = np.concatenate([d + np.arange(run) for d in runs_dst])
+    free = rng.permutation(np.setdiff1d(np.arange(n + 4 * run), used))
+    parts, j, f = [], 0, 0
+    for k, d in enumerate(runs_dst):
+        m = [700, 37, 1100][k]  # scattered rows before each run
+        parts.append(np.stack([j + np.arange(m), free[f:f + m]], 1))
+        j, f = j + m, f + m
+        parts.append(np.stack([j + np.arange(run), d + np.arange(run)], 1))
+        j += run
+    m = n - j
+    parts.append(np.stack([j + np.arange(m), free[f:f + m]], 1))
+    return np.concatenate(parts).astype(np.int64)
+
+
+@pytest.fixture
+def analyzed(dev):
+    """Every unplanned call plans itself on the device (threshold 0), for
+    this test; the default (64 MiB) afterwards."""
+    from geeps_amd import native
+    native.check(native.lib().gp_set_unplanned_min_bytes(0), "gp_set_unplanned_min_bytes")
+    yield
+    native.check(native.lib().gp_set_unplanned_min_bytes(64 << 20), "gp_set_unplanned_min_bytes")
+
+
+@pytest.mark.parametrize("kind", ["identity", "permuted", "sorted", "runs"])
+@pytest.mark.parametrize("W,limit_frac,off", [(128, None, (0, 0)), (64, 0.9, (5, 3)), (1024, None, (0, 2))])
+def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac, off):
+    """The unplanned gp_scatter_add_rows / gp_scatter_init_rows /
+    gp_gather_rows (the reference binding's calls) with the device-built plan:
+    the index scan finds the op-order dense runs (swept), the residual is
+    binned by destination (scatter-add, unsorted) or kept in order; bit for bit
+    against the oracle, with offsets and num_vals_limit tails."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(W * 13 + len(kind))
+    n = 3 * ((4 << 20) // (W * 4) + 130) + 9000
+    idx = _op_order_index(rng, kind, n, W)
+    n_cache = int(idx[:, 1].max()) + 1 + off[1]
+    limit = None if limit_frac is None else int((n + off[0]) * W * limit_frac) + 3
+    x = rng.standard_normal((n + off[0]) * W).astype(np.float32)
+    x[rng.choice(x.size, 200, replace=False)] = np.float32(-0.0)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    ti = torch.from_numpy(idx).to(dev)
+    # add
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    ty = T(y, dev)
+    rowops.add_rows_from_double_index_gpu(ty, T(x, dev), ti, n, off, W, limit)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", kind, W)
+    # init: listed rows zeroed, then the add
+    e = y.copy()
+    e.reshape(n_cache, W)[idx[:, 1] + off[1]] = 0.0
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    ty = T(y, dev)
+    rowops.init_rows_from_double_index_gpu(ty, T(x, dev), ti, n, off, W, limit)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", kind, W)
+    # gather with the index's roles swapped: y[id0] = x[id1]
+    gidx = np.ascontiguousarray(idx[:, ::-1]) if kind != "sorted" else idx
+    g_out = int(gidx[:, 0].max()) + 1 + off[0]
+    src = rng.standard_normal((int(gidx[:, 1].max()) + 1 + off[1]) * W).astype(np.float32)
+    out = rng.standard_normal(g_out * W).astype(np.float32)
+    e = out.copy()
+    g_lim = None if limit is None else int(g_out * W * 0.9) + 1
+    oracle.assign_rows_to_double_index(e, src, gidx, off, W, g_lim)
+    to = T(out, dev)
+    rowops.assign_rows_to_double_index_gpu(to, T(src, dev), torch.from_numpy(gidx).to(dev), n, off, W, g_lim)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(to.cpu().numpy()), bits(e)), ("gather", kind, W)
+
+
 @pytest.mark.parametrize("kind", ["identity", "permuted", "mixed"])
 @pytest.mark.parametrize("W,limit_frac,off", [(128, None, (0, 0)), (64, None, (5, 3)),
                                                (128, 0.83, (0, 0)), (1024, None, (0, 2)),
