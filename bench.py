@@ -444,18 +444,25 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             nbytes = (3 if name.startswith("scatter_add") else 2) * R * 512 + 16 * index_rows
             writes = R * 512
             launches, other, share, kernel_id = 1, 0, 1.0, None
+            # the unplanned calls plan themselves on the device (gp_reduce.h,
+            # ABI 10): an index scan, then the sweep forms for dense runs and
+            # the row kernels for the rest (a scatter-add's unsorted rest binned
+            # by destination first); the time includes the scan and the call's
+            # one stream sync, as the reference's call syncs too
+            scan = "index_scan_kernel + "
             if name == "scatter_add":
                 fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                    validate=False)
-                kernel = "row_op_kernel"
+                kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity"
+                                 else "bin_count/scan/place + row_wave_kernel")
             elif name == "scatter_init":
                 fn = lambda: rowops.init_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                     validate=False)
-                kernel = "row_wave_kernel"
+                kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity" else "row_wave_kernel")
             elif name == "gather":
                 fn = lambda: rowops.assign_rows_to_double_index_gpu(x, y, idx, R, (0, 0), 128, R * 128,
                                                                     validate=False)
-                kernel = "row_wave_kernel"
+                kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity" else "row_wave_kernel")
             elif name == "gather_planned":
                 fn = lambda: gplan.gather(x, y)
                 if ginfo["dense_rows"] == R:  # one dense run: the no-bucket sweep copy

@@ -171,42 +171,19 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
 }
 
 // Phase-separated form for large shards.  Every byte still moves once, but a
-// CU first READS a chunk (master + NB buckets, summed into LDS), then WRITES
-// it back, instead of interleaving its loads and stores.  Measured on MI355X
-// (scripts/tune/alloc_tune.hip, phase_tune.hip; profiles/r01b/): the nine
-// read streams of an 8-way sum alone run at 6.8-6.9 TB/s and the master's
-// write stream alone at 5.1-5.3 TB/s on every allocation, while the mixed
-// stream loses 10-25 % to read/write interleaving on HBM, most on
-// allocations whose pages mix badly.  Holding results in LDS until the
-// chunk's reads are done cut the 8-way sum from 7.25-8.25 ms to 7.17-7.64 ms
-// over the same allocations, and 2- and 4-way sums by 8-10 %.
-//
-// No grid barrier: a launch covers one chunk, and its blocks stay roughly in
-// phase because they do identical work and start together (a launch boundary
-// re-aligns them).  Each block holds 160 KiB of results in LDS -- the CU's
-// whole LDS -- at one block per CU.  Against 64 KiB at 2 blocks per CU that
-// measured 6.66-6.73 vs 7.09 ms at 8 buckets and 3-4 % faster at 1, 2 and 4
-// (profiles/r01b/phase_tune_lds160.txt).  RT more 16-KiB tiles per block are
-// held in registers (VGPRs, spilling into AGPRs, never scratch: one wave per
-// SIMD has the register file to itself), which lengthens both phases.  That
-// pays with few buckets and not with many, whose read phase needs the
-// registers for its (NB + 1) * 4 loads in flight (profiles/r01b/
-// phase_tune_reg.txt): RT = 20 at 1-2 buckets (-2-5 %), 12 at 3-4 (-1-2 %),
-// 4 at 5-8 (-1-2 %), against LDS-only chunks 2 per launch.
-// Shards of fewer than 3 such chunks are split into C <= 3 balanced chunks
-// of T <= 10 + RT tiles per block (at least one), so no launch is a sliver:
-// 2-20 % faster than the mixed form or LDS-only chunks from 8 to 200 MiB at 1
-// and 8 buckets (profiles/r01b/balance_tune*.txt; libgeeps' AlexNet-sized
-// table puts 30 MiB shards on 8 servers).  Below one tile per block (4 MiB):
-// the mixed form.
-// Every access is non-temporal here (master loads and stores too, unlike the
-// mixed form): +1.5-3 % at 1-8 buckets over plain master accesses, which
-// otherwise linger in the caches and drain to HBM during the next read phase.
-// Chunk c covers tiles [c * G * T, (c + 1) * G * T) of kTile f4 each; block g
-// takes tiles g, g + G, ...; the first 10 go to LDS, the rest to registers.
-// Only whole tiles: the caller passes n4_tiles, a multiple of kTile, and sums
-// any rest with the mixed form.  The order of the adds per element is the
-// bucket order, as in every form.
+// CU first READS a chunk (master + NB buckets, summed into LDS and registers),
+// then WRITES it back, instead of interleaving its loads and stores: on HBM
+// the mixed stream loses 10-25 % to read/write interleaving.
+// No grid barrier: a launch covers one chunk, and its blocks stay in phase
+// because they do identical work and start together (a launch boundary
+// re-aligns them).  1 block of 256 threads per CU with the CU's whole LDS
+// (160 KiB = 10 tiles of 16 KiB) plus RT register tiles; every access
+// non-temporal.  Chunk c covers tiles [c * G * T, (c + 1) * G * T) of kTile
+// f4 each; block g takes tiles g, g + G, ...; the first 10 go to LDS, the rest
+// to registers.  Only whole tiles: the caller passes n4_tiles, a multiple of
+// kTile, and sums any rest with the mixed form.  Shards below 3 chunks are
+// cut into C <= 3 balanced chunks (BAL).  The order of the adds per element is
+// the bucket order, as in every form.
 constexpr int kPhaseLdsF4 = 10240;  // 160 KiB of results per block, 1 block per CU
 constexpr int kPhaseU = 4;          // block-strides per tile
 constexpr int kPhaseTile = kBlock * kPhaseU;  // f4 per tile (16 KiB)
@@ -322,50 +299,17 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
 // block's tiles once per stream, in bucket order: pass 0 parks the master's
 // (or `in`'s) tiles, pass k adds bucket k-1's tiles into them.  So at any
 // moment the chip reads one contiguous region of one stream instead of
-// NB + 1 regions at once, and each pass keeps TG tiles' loads in flight with
-// the same registers at any NB.  The per-element order is unchanged, ((in +
-// b0) + b1) + ..., so the bits are those of every other form.  ZIN: no `in`
-// stream; pass 0 parks 0.0f + b0 (-0 -> +0, as after the memset a row plan's
-// fused init replaces).
-// Measured at 3-8 buckets (scripts/tune/bmaj_tune.hip, profiles/r01b/
-// bmaj_tune_*.txt, 3 arenas): 8 buckets 6.42-6.57 ms against 6.62-7.03 ms
-// for the tile-major form, 4 buckets 3.92-3.97 against 4.11-4.21 ms, and a
-// far smaller spread between allocations.  16 tiles per block (10 LDS + 6
-// register) make a 64-MiB chunk on 256 CUs, which divides the 4 GiB headline
-// shard and its 1/2, 1/4, 1/8 slices.
-// Measured at 0-2 buckets in round 2 (scripts/tune/lowb_tune.hip, profiles/
-// r02/tune/lowb_tune.txt, 3 arenas): the tile-major form waits for each
-// tile's loads before the next tile's issue, i.e. 16 KiB in flight per CU at
-// the zero-input form, 32 at 1 bucket, 48 at 2 -- short of the ~56 KiB per
-// CU that ~7 TB/s at ~2 us of loaded latency needs.  The sweep keeps TG tiles
-// in flight: zero-input 75.4-78.5 % of 8 TB/s against 72.0-72.1 % (64-MiB
-// chunks, TG 4); 2 buckets 80.2-80.8 % against 78.6-78.8 % and 1 bucket
-// 79.7-80.0 % against 78.8-79.4 % (96-MiB chunks: 14 register tiles, TG 8).
-// The same 96-MiB shape then measured faster at 3-8 buckets too (scripts/
-// tune/hib_tune.hip, profiles/r02/tune/hib_tune.txt, 3 arenas): per byte
-// +0.8-2.7 % at 8 buckets, +1.4-2.7 % at 4, +2.3-3.5 % at 3 against 64-MiB
-// chunks with bursts of 4.  96 MiB does not divide the 4 GiB shard, so a
-// plan takes whole 96-MiB chunks first ("big"), then whole 64-MiB chunks of
-// the 6-register-tile shape ("small": the 4 GiB shard is 42 + 1), and hands
-// the rest to the tile-major plan (at 1-2 buckets the 64-MiB sweep ran 75-80 %
-// against the tile-major form's 78.6-79.4 %, so there the rest goes straight
-// to tile-major).  Whole chunks only (no guards: the waitcnt counts stay
-// exact).  The zero-input form has one shape, 64-MiB chunks.
-// Burst depth and tile width (round 2, scripts/tune/big_tune.hip, profiles/
-// r02/tune/big_tune{2,...,7}.txt: 6 boxes x 3 arenas).  With 16-KiB tiles and
-// bursts of 8 tiles a wave keeps 32 loads in flight and the chip ~32 MiB of
-// one stream.  Bursts of 2 tiles (8 loads per wave, ~8 MiB on the chip) ran
-// +2.3-3.5 % per byte at 8 buckets and +1.3-1.9 % at 3-4: the HBM row buffers
-// see a narrower address window.  Bursts of 1 (4 loads) starve the pipe
-// (-14 %), of 3 sit in between.  The same 8 loads per wave as ONE tile of 8
-// block-strides (U = 8: a CU's burst is one contiguous 32-KiB run instead of
-// two 16-KiB tiles 4 MiB apart) gained again: +0.4-0.9 % at 8 buckets, +1.4-
-// 2.2 % at 3-4 and +1.1-2.7 % at 2 buckets, where 16-KiB bursts of 2 had
-// tied.  Same chunk, same registers: 5 LDS tiles + 7 register tiles of 32
-// KiB = 96 MiB on 256 CUs.  At 1 bucket the wide tiles tie or lose 0.7 % and
-// the zero-input form and the copy vary by +-3 % between arenas, so they keep
-// their shapes.  Capping the write phase's stores in flight (s_waitcnt
-// vmcnt(4-16) per tile) changed nothing at any bucket count.
+// NB + 1 regions at once, with bursts of TG tiles of U block-strides in
+// flight per wave.  The per-element order is unchanged, ((in + b0) + b1) +
+// ..., so the bits are those of every other form.  ZIN: no `in` stream; pass
+// 0 parks 0.0f + b0 (-0 -> +0, as after the memset a row plan's fused init
+// replaces).  Shapes (SweepShape; measured per shape in DESIGN.md §5): 96-MiB
+// chunks of 32-KiB tiles in bursts of 1 at 2-8 buckets, of 16-KiB tiles in
+// bursts of 8 at 1 bucket; 64-MiB chunks in bursts of 4 for the one-stream
+// forms (ZIN, the NB = 0 copy) and after the big chunks.  A plan takes whole
+// big chunks, then whole 64-MiB chunks (3-8 buckets), then hands the rest to
+// the tile-major form.  Whole chunks only (no guards: the waitcnt counts stay
+// exact; tests/test_kernel_schedule.py checks the schedule).
 template <int NB, bool ZIN>
 struct SweepShape {  // the big chunks: register tiles, tiles per burst, block-strides per tile
   // one stream (the zero-input form, the NB = 0 copy): 64-MiB chunks, bursts of 4 16-KiB tiles
@@ -712,18 +656,12 @@ __device__ __forceinline__ float *seg_row(const gp_row_segments &t, uint64_t row
   return t.base[s] + (row - t.first_row[s]) * row_size;
 }
 
-// Cache policy per stream, measured at 128-float rows, 8 M rows, random and
-// identity indexes on three boxes (profiles/r01b/rownt_tune*.txt):
-//  * scatter-add / fused init: the op buffer x is read once per call:
-//    non-temporal loads, 2-3 % faster.  The oplog side stays plain (nt on its
-//    loads or stores lost or tied; the server's sum reads it next and may find
-//    it in the Infinity Cache when the table is small).  At round 2's 2 blocks
-//    per CU for the op-order add, nt oplog stores gained 0.7-2.2 % in the
-//    paired probe (profiles/r02/tune/wave_tune7{,b}.txt), but the bench line
-//    with them ran the random leg at 60.5 % (profiles/r02/ntst/), below the
-//    62.8-65.4 % plain stores reached on five other boxes: not adopted.
-//  * gather (Read): non-temporal loads of the cache rows AND stores into the
-//    op buffer, 3-5 % faster; either one alone tied or lost.
+// Cache policy of row_op_kernel / row_op_seg_kernel per stream (DESIGN.md
+// §5): the op buffer x of a scatter-add / init is read once per call, with
+// non-temporal loads; the oplog side stays plain; the gather (Read) uses
+// non-temporal loads of the cache rows AND stores into the op buffer.
+// row_wave_kernel (the sorted residuals, the gather, the op-order init) has
+// its own policy: non-temporal on every access.
 template <int OP, typename T>
 __device__ __forceinline__ T ld_src(const T *p) {
   if constexpr (OP == kAddFrom || OP == kInitFrom || OP == kAssignTo)
@@ -903,21 +841,16 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-// Wave-level index map, for the gather (Read) of rows of up to 128 floats
-// (LPR <= 32 lanes per row, 2 or more rows per wave instruction).  Lane l of a wave loads entry t + l of the
-// wave's 64-row tile -- one coalesced 1-KiB read -- and resolves it to a
-// source pointer (flat cache, or the segmented cache's buffer), a destination
-// pointer and the row's num_vals_limit guard; the row groups take theirs by
-// __shfl.  The next tile's entries load while this tile's rows move, so no row
-// load waits on an index load.  Measured against the per-group index load of
-// row_op_kernel (scripts/tune/rowmap_tune.hip, profiles/r01b/rowmap_focus_*.txt):
-// 11-12 % faster for the gather at 128-float rows (1.39-1.44 ms for 8 M rows,
-// 76-78 % of 8 TB/s), 8-10 % at 64-float rows and 6-7 % at 16-float rows
-// (profiles/r01b/rowmap_short_{a,b}.txt).  In op order the scatter-add keeps
-// row_op_kernel: through this kernel it was 3-8 % slower (profiles/r01b/
-// rowmap_scatter_{a,b}.txt), and so were 1024-float rows (13 %, one row per
-// wave instruction).  The fused init runs here, and a row plan's destination-
-// sorted residual runs its add here too (launch_row_op_lpr).
+// Wave-level index map for rows of up to 128 floats (LPR <= 32 lanes per
+// row, 2 or more rows per wave instruction).  Lane l of a wave loads entry
+// t + l of the wave's 64-row tile -- one coalesced 1-KiB read -- and resolves
+// it to a source pointer (flat cache, or the segmented cache's buffer), a
+// destination pointer and the row's num_vals_limit guard; the row groups take
+// theirs by __shfl.  The next tile's entries load while this tile's rows move,
+// so no row load waits on an index load.  Used for the gather (flat and
+// segmented), the fused init, and the scatter-add of destination-sorted rows
+// (a row plan's residual, a device-binned residual); in op order the
+// scatter-add keeps row_op_kernel.  Every access non-temporal.
 template <typename T, int OP, int LPR, int RPG, int SEG>
 __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
@@ -1062,23 +995,14 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
   if constexpr (kWaveShape && (kWaveGather || kWaveScatter)) {
     // Wave-level index map (row_wave_kernel): the gather of rows up to 128
     // floats, the fused init always, the scatter-add when its rows are sorted
-    // by destination (a row plan's residual; in op order its random
-    // read-modify-write side runs 3-8 % slower here than in row_op_kernel).  Rows in flight per group: 8 at
-    // 32 lanes per row (16 spilled past 256 VGPRs: 9 % slower), 16 at 16 lanes.
+    // by destination.  Rows in flight per group: 8 at 32 lanes per row (16
+    // spill past 256 VGPRs), 16 at 16 lanes.
     constexpr int RPG = LPR == 32 ? 8 : 16;
-    // The fused init in op order stays here too: row_op_kernel at 2 blocks
-    // per CU ran 68.5-68.7 % against 60.1-60.2 % on an identity index but
-    // 64.0-64.2 % against 66.4-66.5 % on a random one in the probe
-    // (profiles/r02/tune/wave_tune6{,b}.txt), and in the bench line the
-    // random leg fell from 68.4-69.2 % to 61.2 % while identity rose only to
-    // 66.2 % (profiles/r02/rowinit/): a net loss, not adopted.
     if (kWaveGather || OP == kInitFrom || sorted) {
       auto *kern = &row_wave_kernel<T, OP, LPR, RPG, SEG>;
       size_t grid = (n + kBlock - 1) / kBlock;  // one 64-row tile per wave
-      // One resident round of blocks (every block resident from the start,
-      // none waiting for a slot): the scatter forms 73-81 % of 8 TB/s against
-      // 69-72 % at a grid of 1.3-2.7 rounds, the gather +1-2 %
-      // (profiles/r02/plan_tune*.txt).
+      // One resident round of blocks: every block resident from the start,
+      // none waiting for a slot.
       static std::atomic<int> occ{0};
       const size_t cap = (size_t)num_cus() * resident_blocks(reinterpret_cast<const void *>(kern), occ);
       if (grid > cap) grid = cap;
@@ -1092,14 +1016,9 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
   constexpr int kGroups = kBlock / LPR;
   const size_t groups = (n + RPG - 1) / RPG;
   size_t grid = (groups + kGroups - 1) / kGroups;
-  // The op-order scatter-add of RowData-sized rows with fewer blocks per CU
-  // than 8: fewer rows in flight, a narrower window of the read-modify-write
-  // side's addresses (as for the sweep sums' bursts).  Flat, 2 per CU: +3.9-
-  // 4.2 % on an identity index, +0.2-0.5 % on a random one (1 or 4 lost);
-  // segmented (read-my-writes), whose registers leave fewer waves per block
-  // resident, 4 per CU: +6.6-7.2 % identity, +5.0 % random (2 lost); the
-  // segmented gather keeps 8 (2 or 4 lost 6-25 %).  Three boxes, bit-exact
-  // (scripts/tune/wave_tune.hip, profiles/r02/tune/wave_tune{3,3b,4,4b}.txt).
+  // The op-order scatter-add of RowData-sized rows at 2 blocks per CU (4 for
+  // the segmented form): fewer rows in flight, a narrower window of the
+  // read-modify-write side's addresses.
   constexpr bool kRowAdd = OP == kAddFrom && VEC == 4 && LPR == 32;
   const size_t cap = (kRowAdd && SEG == kFlat)   ? (size_t)num_cus() * 2
                      : (kRowAdd && SEG == kSegY) ? (size_t)num_cus() * 4
