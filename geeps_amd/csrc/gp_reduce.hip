@@ -1646,9 +1646,18 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     const unsigned ns = std::min<unsigned>(hdr.n_starts, kMaxRunStarts);
     std::vector<RunStart> starts(st, st + ns);
     std::sort(starts.begin(), starts.end(), [](const RunStart &a, const RunStart &b) { return a.tile < b.tile; });
+    // first tile >= t that is not dense-and-continuing (word at a time)
+    auto run_end = [&](size_t t) {
+      while (t < tiles) {
+        const size_t g = t / kScanGroupTiles;
+        const uint64_t brk = ~(words[3 * g] & words[3 * g + 1]) >> (t % kScanGroupTiles);
+        if (brk) return std::min(tiles, t + (size_t)__builtin_ctzll(brk));
+        t = (g + 1) * kScanGroupTiles;
+      }
+      return tiles;
+    };
     for (const RunStart &r : starts) {
-      size_t t = r.tile + 1;
-      while (t < tiles && bit(t, 0) && bit(t, 1)) ++t;
+      const size_t t = run_end(r.tile + 1);
       if (t - r.tile >= min_tiles) {
         const uint64_t e0 = r.tile * 64, rows = std::min<uint64_t>((t - r.tile) * 64, n - e0);
         runs.push_back(DevRun{e0, rows, r.from, r.to});
@@ -1696,11 +1705,15 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   if (resid == 0) return GP_OK;
   // destinations already (mostly) ascending: keep the call's order
   size_t resid_tiles = 0, asc_tiles = 0;
-  for (uint32_t i = 0; i < rr.count; ++i)
-    for (size_t t = rr.lo[i] / 64; t < (rr.hi[i] + 63) / 64; ++t) {
-      ++resid_tiles;
-      asc_tiles += bit(t, 2);
-    }
+  for (uint32_t i = 0; i < rr.count; ++i) {
+    size_t t = rr.lo[i] / 64;
+    const size_t t1 = (rr.hi[i] + 63) / 64;
+    resid_tiles += t1 - t;
+    for (; t < t1 && t % kScanGroupTiles; ++t) asc_tiles += bit(t, 2);
+    for (; t + kScanGroupTiles <= t1; t += kScanGroupTiles)
+      asc_tiles += __builtin_popcountll(words[3 * (t / kScanGroupTiles) + 2]);
+    for (; t < t1; ++t) asc_tiles += bit(t, 2);
+  }
   const bool ascending = asc_tiles * 10 >= resid_tiles * 9;
   if (OP != kAddFrom || ascending || resid * W * sizeof(float) < kBinMinBytes) {
     for (uint32_t i = 0; i < rr.count; ++i) {

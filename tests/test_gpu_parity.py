@@ -750,8 +750,9 @@ def test_row_plan_repeated_destinations(dev, W, limit_frac):
     rep = rng.choice(np.concatenate([rng.choice(run, 300, replace=False), run + np.arange(400)]),
                      2000)
     extra = np.stack([run + np.arange(2000), rep], 1)
-    idx = np.concatenate([dense, extra])
-    idx = idx[rng.permutation(len(idx))]
+    # the run first in op order (its rows are the first occurrences of their
+    # destinations, so it stays one dense run), then the rest shuffled
+    idx = np.concatenate([dense, extra[rng.permutation(len(extra))]])
     n_op = len(idx)
     limit = None if limit_frac is None else int(n_op * W * limit_frac) + 5
     x = rng.standard_normal(n_op * W).astype(np.float32)
