@@ -387,8 +387,9 @@ ROWOP_LEGS = ("scatter_add", "scatter_add_planned", "scatter_init", "scatter_ini
               "gather", "gather_planned")
 
 
-def _time_calls(fn, reps, stream):
-    fn()  # warm-up
+def _time_calls(fn, reps, stream, warmup=True):
+    if warmup:
+        fn()
     ms = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -415,7 +416,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
     Algorithmic bytes per call: add 3*R*512, init / gather 2*R*512, plus the
     16-B DoubleIndex entries the kernel reads (every row unplanned; a plan's
     residual rows planned -- its dense runs read no index)."""
-    from geeps_amd import rowops
+    from geeps_amd import native, rowops
     R = rows * W // 128
     stream = torch.cuda.current_stream()
     g = torch.Generator(device=dev)
@@ -446,19 +447,23 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             launches, other, share, kernel_id = 1, 0, 1.0, None
             # the unplanned calls plan themselves on the device (gp_reduce.h,
             # ABI 10): an index scan, then the sweep forms for dense runs and
-            # the row kernels for the rest (a scatter-add's unsorted rest binned
-            # by destination first); the time includes the scan and the call's
-            # one stream sync, as the reference's call syncs too
+            # the row kernels for the rest; a scatter's unsorted rest runs in op
+            # order on the first call with an index (`first_call_ms`) and from
+            # the plan cache's destination-sorted copy after that (`avg_ms`,
+            # the reference reusing each op's DoubleIndex every clock).  The
+            # time includes the scan and the call's one stream sync, as the
+            # reference's call syncs too.
             scan = "index_scan_kernel + "
             if name == "scatter_add":
                 fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                    validate=False)
                 kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity"
-                                 else "bin_count/scan/place + row_wave_kernel")
+                                 else "row_wave_kernel (cached sorted residual)")
             elif name == "scatter_init":
                 fn = lambda: rowops.init_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                     validate=False)
-                kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity" else "row_wave_kernel")
+                kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity"
+                                 else "row_wave_kernel (cached sorted residual)")
             elif name == "gather":
                 fn = lambda: rowops.assign_rows_to_double_index_gpu(x, y, idx, R, (0, 0), 128, R * 128,
                                                                     validate=False)
@@ -493,11 +498,18 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                         launches, other, share = sp["launches"], sp["other_launches"], sp["share"]
                 else:
                     kernel = "row_wave_kernel"
+            first_ms = None
+            if not planned:  # the first call with this index (a plan-cache miss) on its own
+                native.check(native.lib().gp_unplanned_cache_clear(), "gp_unplanned_cache_clear")
+                first_ms = _time_calls(fn, 1, stream, warmup=False)
             avg = _time_calls(fn, reps, stream)
             gbps = nbytes / (avg / 1e3) / 1e9
             leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),
                    "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes": nbytes, "kernel": kernel,
                    "launches": launches, "avg_launch_ms": round(avg * share / launches, 5)}
+            if first_ms is not None:
+                leg["first_call_ms"] = round(first_ms, 4)
+                leg["first_call_frac"] = round(nbytes / (first_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
             if other:  # the rest in other kernel forms; avg_launch_ms is the dominant one's share
                 leg["other_launches"] = other
                 leg["dominant_share"] = round(share, 6)
@@ -516,6 +528,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                          if kind == "random" else "identity", **legs)
         plan.close()
         gplan.close()
+        native.check(native.lib().gp_unplanned_cache_clear(), "gp_unplanned_cache_clear")
         del idx, dst
     return out
 

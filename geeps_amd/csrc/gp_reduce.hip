@@ -39,10 +39,19 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "gp_reduce.h"
+
+// gp_sort.hip (hipCUB's radix sort, in its own translation unit): sort n
+// (key, value) pairs by the low end_bit bits of the key, stream-ordered, on
+// temporary storage from the stream-ordered pool.  Returns a GP_* status.
+int gp_internal_radix_sort_pairs_u32(const uint32_t *keys_in, uint32_t *keys_out, const uint32_t *vals_in,
+                                     uint32_t *vals_out, size_t n, int end_bit, hipStream_t s,
+                                     std::string *error);
 
 namespace {
 
@@ -1351,123 +1360,166 @@ int launch_gather_planned(float *y, const float *x, const gp_row_segments *xs,
 // gp_scatter_init_rows, gp_gather_rows): the reference's own binding passes a
 // device DoubleIndex on every call (add_rows_from_double_index_gpu,
 // row-op-util.cu:127-142, synchronous at :141), with no host copy to compile a
-// gp_row_plan from.  A large call therefore plans itself on the device first:
+// gp_row_plan from.  A large call therefore plans itself on the device:
 //  1. index_scan_kernel reads the index once (16 B per row) and writes, per
 //     64-entry tile, whether it is dense (id0 and id1 both step by one, every
 //     row clear of num_vals_limit), whether it continues the tile before, and
-//     whether its destinations ascend; plus the first entry of every tile that
-//     starts a dense run, and the largest destination row.
+//     whether its destinations ascend; the first entry of every tile that
+//     starts a dense run; the largest destination row.  When the call's index
+//     was planned before (the plan cache, below), it also compares every entry
+//     with the copy kept then.
 //  2. One D2H of that summary and a stream sync (the reference's call syncs
-//     too); the host turns it into runs, exactly like build_row_plan.
+//     too); the host turns it into runs, as build_row_plan does.
 //  3. Dense runs of at least kDenseRunBytes go to the phase-separated sum
 //     kernels (1 bucket, the zero-input form, the copy), as in a row plan.
-//  4. The other rows: a scatter-add whose destinations are not mostly sorted
-//     is binned by destination on the device first (a counting sort by
-//     destination row >> s into a workspace: histogram, scan, scatter), so
-//     the wave-map kernel walks y nearly front to back as it does for a
-//     plan's sorted residual; otherwise the rows go to the row kernels as they
-//     are.  Binning changes the order rows are visited in, which is bit-neutral
-//     under the call's precondition (distinct destinations).
-// Calls below kAnalyzeMinBytes (gp_set_unplanned_min_bytes) skip all this.
+//  4. The other rows (the residual) go to the row kernels.  A scatter-add's or
+//     init's residual whose destinations do not ascend is a random
+//     read-modify-write of y in op order (~66 % of 8 TB/s; a plan's
+//     destination-sorted residual runs ~76 %).  Sorting it costs more than it
+//     saves in one call (a radix sort of 8 M pairs ~0.3 ms; coarse binning
+//     does not recover the locality: DESIGN.md §5), but the reference reuses
+//     each op's DoubleIndex every clock.  So such a residual runs in op order
+//     once, and its destination-sorted copy is built for the calls that follow
+//     (a hipCUB radix sort, gp_sort.hip).  Later calls with the same index --
+//     same pointer, size, offsets, row size and limit, and entry for entry the
+//     same content, which the scan checks against the cached copy -- run the
+//     sorted copy.  Visiting rows in destination order is bit-neutral under
+//     the call's precondition (distinct destinations).
+// Calls below g_analyze_min_bytes (gp_set_unplanned_min_bytes) skip all this.
 // ---------------------------------------------------------------------------
-constexpr int kScanGroupTiles = 64;  // tiles of 64 entries per scan word
+constexpr int kScanGroupTiles = 64;  // tiles of 64 entries per scan word group
+constexpr int kScanWaveTiles = 16;   // tiles per wave (17 loads in flight)
 constexpr int kMaxRunStarts = 512;   // run-start entries the scan records
 constexpr int kMaxDeviceRuns = 32;   // dense runs a call sweeps (the longest)
-constexpr int kBinShiftRows = 12;    // destination bins of 4096 rows (2 MiB of RowData)
-constexpr size_t kBinMinBytes = 16u << 20;  // smaller residuals are not binned
+constexpr size_t kSortMinBytes = 16u << 20;       // smaller residuals keep op order
+constexpr size_t kPlanCacheBytes = 4ull << 30;    // device memory of cached plans (LRU)
+constexpr size_t kPlanCacheEntries = 256;
 
 struct ScanHeader {
-  unsigned long long max_dst;
   unsigned int n_starts;
-  unsigned int pad;
+  unsigned int mismatches;  // waves that saw an entry differ from the cached copy
+  uint64_t pad;
 };
 struct RunStart {
   uint64_t tile, from, to;
 };
-// workspace: [ScanHeader][RunStart x kMaxRunStarts][3 words per 64 tiles]
+// workspace: [ScanHeader][RunStart x kMaxRunStarts][4 words per group of 64
+// tiles: dense, continues, ascends (bit k = tile 64 g + k), largest destination]
 constexpr size_t kScanWordsOff = sizeof(ScanHeader) + sizeof(RunStart) * kMaxRunStarts;
+constexpr int kScanWords = 4;
 
 std::atomic<size_t> g_analyze_min_bytes{64u << 20};
 
-// The endpoints of entry e (offsets applied) and whether its guarded row is
-// whole; dead entries (e >= n) are not whole.
+int radix_sort_pairs_u32(const uint32_t *ki, uint32_t *ko, const uint32_t *vi, uint32_t *vo, size_t n, int end_bit,
+                         hipStream_t s) {
+  std::string err;
+  const int rc = gp_internal_radix_sort_pairs_u32(ki, ko, vi, vo, n, end_bit, s, &err);
+  return rc == GP_OK ? GP_OK : set_error(rc, err);
+}
+
+// Entry e (raw) and its endpoints (offsets applied); whether its guarded row
+// is whole.  Dead entries (e >= n) are not whole.
 template <int OP>
 __device__ __forceinline__ bool scan_entry(const gp_double_index *idx, size_t n, size_t e, uint64_t off0,
-                                           uint64_t off1, size_t row_size, size_t limit, uint64_t &from,
-                                           uint64_t &to) {
+                                           uint64_t off1, size_t row_size, size_t limit, gp_double_index &raw,
+                                           uint64_t &from, uint64_t &to) {
   from = to = 0;
+  raw = gp_double_index{0, 0};
   if (e >= n) return false;
-  row_endpoints<OP>(idx[e], off0, off1, from, to);
+  raw = idx[e];
+  row_endpoints<OP>(raw, off0, off1, from, to);
   return ((OP == kAssignTo ? to : from) + 1) * row_size <= limit;
 }
 
-// One wave per group of 64 tiles (4096 entries): three 64-bit words per group
-// (bit k = tile 64 g + k): dense, continues the previous tile, destinations
-// ascend (inside the tile and from the previous tile's last entry).
+// One block (4 waves) per group of 64 tiles (4096 entries); each wave takes 16
+// tiles with all 17 of its loads (the tile before its first, then its own) in
+// flight at once.  No global atomics on the common path (a per-group word
+// carries the group's largest destination).
 template <int OP>
 __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_index *__restrict__ idx, size_t n,
                                                             uint64_t off0, uint64_t off1, size_t row_size,
-                                                            size_t limit, char *__restrict__ ws) {
+                                                            size_t limit, const gp_double_index *__restrict__ cached,
+                                                            char *__restrict__ ws) {
+  static_assert(kScanWaveTiles * (kBlock / 64) == kScanGroupTiles, "a block covers one word group");
   ScanHeader *hdr = reinterpret_cast<ScanHeader *>(ws);
   RunStart *starts = reinterpret_cast<RunStart *>(ws + sizeof(ScanHeader));
   uint64_t *words = reinterpret_cast<uint64_t *>(ws + kScanWordsOff);
-  const int wl = threadIdx.x & 63;
+  __shared__ uint64_t part[kScanWords][kBlock / 64];
+  const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const size_t tiles = (n + 63) / 64;
   const size_t groups = (tiles + kScanGroupTiles - 1) / kScanGroupTiles;
-  const size_t wave = ((size_t)blockIdx.x * kBlock + threadIdx.x) / 64;
-  const size_t wstride = (size_t)gridDim.x * (kBlock / 64);
-  unsigned long long mx = 0;
-  for (size_t g = wave; g < groups; g += wstride) {
-    const size_t t0 = g * kScanGroupTiles;
-    // the tile before the group: its last entry and whether it is dense
-    uint64_t pf = 0, pt = 0;  // previous entry (lane 63 of the previous tile)
-    bool prev_dense = false;
-    if (t0 > 0) {
-      uint64_t f, t;
-      const bool w = scan_entry<OP>(idx, n, (t0 - 1) * 64 + wl, off0, off1, row_size, limit, f, t);
-      const uint64_t lf = shfl64(f, (wl + 63) & 63), lt = shfl64(t, (wl + 63) & 63);
-      prev_dense = __all(w && (wl == 0 || (f == lf + 1 && t == lt + 1)));
-      pf = shfl64(f, 63);
-      pt = shfl64(t, 63);
+  for (size_t g = blockIdx.x; g < groups; g += gridDim.x) {
+    const size_t t0 = g * kScanGroupTiles + (size_t)wv * kScanWaveTiles;  // this wave's first tile
+    uint64_t f[kScanWaveTiles + 1], to[kScanWaveTiles + 1];
+    bool whole[kScanWaveTiles + 1];
+    bool differs = false;
+#pragma unroll
+    for (int k = 0; k <= kScanWaveTiles; ++k) {  // k = 0: the tile before t0
+      gp_double_index raw;
+      if (t0 + k >= 1) {
+        const size_t e = (t0 + k - 1) * 64 + wl;
+        whole[k] = scan_entry<OP>(idx, n, e, off0, off1, row_size, limit, raw, f[k], to[k]);
+        if (cached && k > 0 && e < n) {
+          const gp_double_index c = cached[e];
+          differs = differs || c.id0 != raw.id0 || c.id1 != raw.id1;
+        }
+      } else {
+        whole[k] = false;
+        f[k] = to[k] = 0;
+      }
     }
-    uint64_t wd = 0, wc = 0, ws_ = 0;
-    for (int k = 0; k < kScanGroupTiles; ++k) {
-      const size_t t = t0 + k;
-      if (t >= tiles) break;  // wave-uniform
+    uint64_t pf = shfl64(f[0], 63), pt = shfl64(to[0], 63);
+    bool prev_dense;
+    {
+      const uint64_t lf = shfl64(f[0], (wl + 63) & 63), lt = shfl64(to[0], (wl + 63) & 63);
+      prev_dense = t0 >= 1 && __all(whole[0] && (wl == 0 || (f[0] == lf + 1 && to[0] == lt + 1)));
+    }
+    uint32_t wd = 0, wc = 0, wa = 0;
+    uint64_t mx = 0;
+#pragma unroll
+    for (int k = 1; k <= kScanWaveTiles; ++k) {
+      const size_t t = t0 + k - 1;
       const size_t e = t * 64 + wl;
-      uint64_t f, to;
-      const bool whole = scan_entry<OP>(idx, n, e, off0, off1, row_size, limit, f, to);
       const bool live = e < n;
-      const uint64_t lf = shfl64(f, (wl + 63) & 63), lt = shfl64(to, (wl + 63) & 63);
+      const uint64_t lf = shfl64(f[k], (wl + 63) & 63), lt = shfl64(to[k], (wl + 63) & 63);
       const uint64_t bf = wl == 0 ? pf : lf, bt = wl == 0 ? pt : lt;  // the entry before this one
       const bool has_before = e > 0;
-      const bool step = has_before && f == bf + 1 && to == bt + 1;
-      const bool dense = __all(whole && (wl == 0 || step));
-      const bool cont = __shfl(step ? 1 : 0, 0, 64) != 0;  // lane 0: continues the previous tile
-      const bool asc = __all(!live || !has_before || to > bt);
-      if (live && to > mx) mx = to;
-      if (dense) wd |= 1ull << k;
-      if (cont) wc |= 1ull << k;
-      if (asc) ws_ |= 1ull << k;
+      const bool step = has_before && f[k] == bf + 1 && to[k] == bt + 1;
+      const bool dense = t < tiles && __all(whole[k] && (wl == 0 || step));
+      const bool cont = __shfl(step ? 1 : 0, 0, 64) != 0;
+      const bool asc = __all(!live || !has_before || to[k] > bt);
+      if (live && to[k] > mx) mx = to[k];
+      wd |= (dense ? 1u : 0u) << (k - 1);
+      wc |= (cont ? 1u : 0u) << (k - 1);
+      wa |= (asc ? 1u : 0u) << (k - 1);
       if (dense && !(cont && prev_dense) && wl == 0) {
         const unsigned slot = atomicAdd(&hdr->n_starts, 1u);
-        if (slot < (unsigned)kMaxRunStarts) starts[slot] = RunStart{t, f, to};
+        if (slot < (unsigned)kMaxRunStarts) starts[slot] = RunStart{t, f[k], to[k]};
       }
       prev_dense = dense;
-      pf = shfl64(f, 63);
-      pt = shfl64(to, 63);
+      pf = shfl64(f[k], 63);
+      pt = shfl64(to[k], 63);
+    }
+    if (__any(differs) && wl == 0) atomicAdd(&hdr->mismatches, 1u);
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t v = shfl64(mx, (wl + o) & 63);
+      mx = v > mx ? v : mx;
     }
     if (wl == 0) {
-      words[3 * g] = wd;
-      words[3 * g + 1] = wc;
-      words[3 * g + 2] = ws_;
+      part[0][wv] = (uint64_t)wd << (wv * kScanWaveTiles);
+      part[1][wv] = (uint64_t)wc << (wv * kScanWaveTiles);
+      part[2][wv] = (uint64_t)wa << (wv * kScanWaveTiles);
+      part[3][wv] = mx;
     }
+    __syncthreads();
+    if (threadIdx.x < kScanWords) {
+      uint64_t w = 0;
+      for (int v = 0; v < kBlock / 64; ++v)
+        w = threadIdx.x == 3 ? (part[3][v] > w ? part[3][v] : w) : (w | part[threadIdx.x][v]);
+      words[kScanWords * g + threadIdx.x] = w;
+    }
+    __syncthreads();
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long v = shfl64(mx, (wl + o) & 63);
-    mx = v > mx ? v : mx;
-  }
-  if (wl == 0) atomicMax(&hdr->max_dst, mx);
 }
 
 // Residual rows of a call: up to kMaxDeviceRuns + 1 entry ranges, passed by
@@ -1483,83 +1535,34 @@ __device__ __forceinline__ size_t range_entry(const EntryRanges &r, size_t k) {
   return r.lo[i] + (k - r.pre[i]);
 }
 
-constexpr int kBinLds = 16384;  // bins counted in LDS (64 KiB)
-
-// Counting sort of the residual rows by destination row >> shift: per-bin
-// counts (LDS per block, then global atomics).
+// Sort keys (destination rows) and values (entry positions) of the residual.
 template <int OP>
-__global__ __launch_bounds__(kBlock) void bin_count_kernel(const gp_double_index *__restrict__ idx,
-                                                           EntryRanges rr, uint64_t off0, uint64_t off1,
-                                                           int shift, uint32_t nbins, uint32_t *__restrict__ count,
-                                                           size_t per_block) {
-  __shared__ uint32_t h[kBinLds];
-  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock) h[b] = 0;
-  __syncthreads();
+__global__ __launch_bounds__(kBlock) void residual_keys_kernel(const gp_double_index *__restrict__ idx, EntryRanges rr,
+                                                               uint64_t off0, uint64_t off1, uint32_t *__restrict__ key,
+                                                               uint32_t *__restrict__ val) {
   const size_t total = rr.pre[rr.count];
-  const size_t lo = (size_t)blockIdx.x * per_block, hi = min(lo + per_block, total);
-  for (size_t k = lo + threadIdx.x; k < hi; k += kBlock) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x; k < total; k += stride) {
+    const size_t e = range_entry(rr, k);
     uint64_t f, t;
-    row_endpoints<OP>(idx[range_entry(rr, k)], off0, off1, f, t);
-    atomicAdd(&h[(uint32_t)(t >> shift)], 1u);
-  }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock)
-    if (h[b]) atomicAdd(&count[b], h[b]);
-}
-
-// One block: exclusive scan of the counts into cursors (nbins <= kBinLds).
-__global__ __launch_bounds__(1024) void bin_scan_kernel(const uint32_t *__restrict__ count, uint32_t nbins,
-                                                        uint32_t *__restrict__ cursor) {
-  __shared__ uint32_t part[1024];
-  const uint32_t per = (nbins + 1023) / 1024;
-  const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nbins);
-  uint32_t s = 0;
-  for (uint32_t b = lo; b < hi; ++b) s += count[b];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (uint32_t b = lo; b < hi; ++b) {
-    cursor[b] = run;
-    run += count[b];
+    row_endpoints<OP>(idx[e], off0, off1, f, t);
+    key[k] = (uint32_t)t;
+    val[k] = (uint32_t)e;
   }
 }
 
-// Each block reserves its rows' slots per bin, then places them (order inside
-// a bin is arbitrary).  Entries are written with the offsets applied.
+// The residual's entries in sorted order, offsets applied (a scatter plan's
+// residual: {from, to}).
 template <int OP>
-__global__ __launch_bounds__(kBlock) void bin_place_kernel(const gp_double_index *__restrict__ idx,
-                                                           EntryRanges rr, uint64_t off0, uint64_t off1,
-                                                           int shift, uint32_t nbins, uint32_t *__restrict__ cursor,
-                                                           gp_double_index *__restrict__ out, size_t per_block) {
-  __shared__ uint32_t h[kBinLds];
-  __shared__ uint32_t base[kBinLds];
-  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock) h[b] = 0;
-  __syncthreads();
-  const size_t total = rr.pre[rr.count];
-  const size_t lo = (size_t)blockIdx.x * per_block, hi = min(lo + per_block, total);
-  for (size_t k = lo + threadIdx.x; k < hi; k += kBlock) {
+__global__ __launch_bounds__(kBlock) void residual_gather_kernel(const gp_double_index *__restrict__ idx,
+                                                                 const uint32_t *__restrict__ pos, size_t total,
+                                                                 uint64_t off0, uint64_t off1,
+                                                                 gp_double_index *__restrict__ out) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x; k < total; k += stride) {
     uint64_t f, t;
-    row_endpoints<OP>(idx[range_entry(rr, k)], off0, off1, f, t);
-    atomicAdd(&h[(uint32_t)(t >> shift)], 1u);
-  }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nbins; b += kBlock) {
-    base[b] = h[b] ? atomicAdd(&cursor[b], h[b]) : 0;
-    h[b] = 0;
-  }
-  __syncthreads();
-  for (size_t k = lo + threadIdx.x; k < hi; k += kBlock) {
-    const gp_double_index ix = idx[range_entry(rr, k)];
-    uint64_t f, t;
-    row_endpoints<OP>(ix, off0, off1, f, t);
-    const uint32_t b = (uint32_t)(t >> shift);
-    out[base[b] + atomicAdd(&h[b], 1u)] = OP == kAssignTo ? gp_double_index{t, f} : gp_double_index{f, t};
+    row_endpoints<OP>(idx[pos[k]], off0, off1, f, t);
+    out[k] = gp_double_index{f, t};
   }
 }
 
@@ -1600,9 +1603,121 @@ void keep_pool_memory() {
   (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
 }
 
+// ---- the plan cache --------------------------------------------------------
+struct PlanKey {
+  int device, op;
+  uintptr_t index;
+  size_t n, row_size, limit;
+  uint64_t off0, off1;
+  bool operator==(const PlanKey &o) const {
+    return device == o.device && op == o.op && index == o.index && n == o.n && row_size == o.row_size &&
+           limit == o.limit && off0 == o.off0 && off1 == o.off1;
+  }
+};
+
+struct CachedPlan {
+  PlanKey key{};
+  gp_double_index *copy = nullptr;    // the index as first seen
+  gp_double_index *sorted = nullptr;  // its residual, offsets applied, ascending destination
+  size_t resid = 0;
+  hipEvent_t ready = nullptr;  // recorded once both are built, on the building stream
+  uint64_t last_use = 0;
+  size_t bytes = 0;
+  ~CachedPlan() {
+    // hipFree waits for the device, so kernels already queued on it finish first
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != key.device) (void)hipSetDevice(key.device);
+    if (copy) (void)hipFree(copy);
+    if (sorted) (void)hipFree(sorted);
+    if (ready) (void)hipEventDestroy(ready);
+    if (cur >= 0 && cur != key.device) (void)hipSetDevice(cur);
+  }
+};
+
+std::mutex g_plan_cache_mu;
+std::vector<std::shared_ptr<CachedPlan>> g_plan_cache;  // g_plan_cache_mu
+uint64_t g_plan_cache_tick = 0;                          // g_plan_cache_mu
+
+std::shared_ptr<CachedPlan> cache_find(const PlanKey &k) {
+  std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+  for (auto &p : g_plan_cache)
+    if (p->key == k) {
+      p->last_use = ++g_plan_cache_tick;
+      return p;
+    }
+  return nullptr;
+}
+
+void cache_drop(const std::shared_ptr<CachedPlan> &p) {
+  std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+  g_plan_cache.erase(std::remove(g_plan_cache.begin(), g_plan_cache.end(), p), g_plan_cache.end());
+}
+
+void cache_insert(std::shared_ptr<CachedPlan> p) {
+  std::vector<std::shared_ptr<CachedPlan>> evicted;  // freed outside the lock
+  {
+    std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+    for (auto it = g_plan_cache.begin(); it != g_plan_cache.end();)  // a concurrent build of the same key
+      if ((*it)->key == p->key) {
+        evicted.push_back(*it);
+        it = g_plan_cache.erase(it);
+      } else {
+        ++it;
+      }
+    p->last_use = ++g_plan_cache_tick;
+    g_plan_cache.push_back(std::move(p));
+    auto total = [] {
+      size_t b = 0;
+      for (auto &q : g_plan_cache) b += q->bytes;
+      return b;
+    };
+    while (g_plan_cache.size() > 1 && (g_plan_cache.size() > kPlanCacheEntries || total() > kPlanCacheBytes)) {
+      auto lru = std::min_element(g_plan_cache.begin(), g_plan_cache.end(),
+                                  [](const auto &a, const auto &b) { return a->last_use < b->last_use; });
+      evicted.push_back(*lru);
+      g_plan_cache.erase(lru);
+    }
+  }
+}
+
 struct DevRun {
   uint64_t e0, rows, from, to;  // first entry, rows, endpoints of the first entry
 };
+
+// The destination-sorted copy of a residual, built on stream s after the
+// call's own launches (defined in gp_sort.hip's radix sort).
+template <int OP>
+int build_cached_plan(const PlanKey &key, const gp_double_index *idx, const EntryRanges &rr, uint64_t max_dst,
+                      hipStream_t s) {
+  const size_t resid = rr.pre[rr.count];
+  auto p = std::make_shared<CachedPlan>();
+  p->key = key;
+  p->resid = resid;
+  p->bytes = (key.n + resid) * sizeof(gp_double_index);
+  GP_HIP_TRY(hipMalloc(&p->copy, key.n * sizeof(gp_double_index)));
+  GP_HIP_TRY(hipMalloc(&p->sorted, resid * sizeof(gp_double_index)));
+  GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+  GP_HIP_TRY(hipMemcpyAsync(p->copy, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
+  uint32_t *kv = nullptr;  // keys, values, sorted keys, sorted values
+  GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&kv), 4 * resid * sizeof(uint32_t), s));
+  const size_t grid = std::min((resid + kBlock - 1) / kBlock, (size_t)num_cus() * 8);
+  hipLaunchKernelGGL(residual_keys_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, rr, key.off0, key.off1,
+                     kv, kv + resid);
+  int end_bit = 1;  // destination rows are below 2^32 here (checked by the caller)
+  while (end_bit < 32 && (max_dst >> end_bit)) ++end_bit;
+  int rc = radix_sort_pairs_u32(kv, kv + 2 * resid, kv + resid, kv + 3 * resid, resid, end_bit, s);
+  if (rc == GP_OK) {
+    hipLaunchKernelGGL(residual_gather_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, kv + 3 * resid,
+                       resid, key.off0, key.off1, p->sorted);
+    rc = hipGetLastError() == hipSuccess ? GP_OK : set_error(GP_ERR_HIP, "residual_gather_kernel launch");
+  }
+  GP_HIP_TRY(hipFreeAsync(kv, s));
+  if (rc != GP_OK) return rc;
+  GP_HIP_TRY(hipEventRecord(p->ready, s));
+  cache_insert(std::move(p));
+  return GP_OK;
+}
 
 // The analysed form of launch_row_op (see the section comment).
 template <int OP>
@@ -1611,7 +1726,11 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   const size_t W = row_size;
   const size_t tiles = (n + 63) / 64, groups = (tiles + kScanGroupTiles - 1) / kScanGroupTiles;
   keep_pool_memory();
-  const size_t scan_bytes = kScanWordsOff + groups * 3 * sizeof(uint64_t);
+  int dev = 0;
+  GP_HIP_TRY(hipGetDevice(&dev));
+  const PlanKey key{dev, OP, reinterpret_cast<uintptr_t>(idx), n, W, limit, off.id0, off.id1};
+  std::shared_ptr<CachedPlan> cached = OP == kAssignTo ? nullptr : cache_find(key);
+  const size_t scan_bytes = kScanWordsOff + groups * kScanWords * sizeof(uint64_t);
   char *ws = nullptr;
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), scan_bytes, s));
   struct Free {  // the workspace goes back in stream order, whatever happens
@@ -1623,10 +1742,9 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   } free_ws{ws, s};
   GP_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(ScanHeader), s));
   {
-    const size_t waves = std::max<size_t>(1, std::min(groups, (size_t)num_cus() * 16));
-    const size_t grid = (waves + (kBlock / 64) - 1) / (kBlock / 64);
+    const size_t grid = std::max<size_t>(1, std::min(groups, (size_t)num_cus() * 8));
     hipLaunchKernelGGL(index_scan_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, n, off.id0, off.id1,
-                       W, limit, ws);
+                       W, limit, cached ? cached->copy : nullptr, ws);
     GP_HIP_TRY(hipGetLastError());
   }
   char *h = static_cast<char *>(g_scan_landing.get(scan_bytes));
@@ -1636,7 +1754,15 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   const ScanHeader hdr = *reinterpret_cast<const ScanHeader *>(h);
   const RunStart *st = reinterpret_cast<const RunStart *>(h + sizeof(ScanHeader));
   const uint64_t *words = reinterpret_cast<const uint64_t *>(h + kScanWordsOff);
-  auto bit = [&](size_t t, int w) { return (words[3 * (t / kScanGroupTiles) + w] >> (t % kScanGroupTiles)) & 1; };
+  auto bit = [&](size_t t, int w) {
+    return (words[kScanWords * (t / kScanGroupTiles) + w] >> (t % kScanGroupTiles)) & 1;
+  };
+  uint64_t max_dst = 0;
+  for (size_t g = 0; g < groups; ++g) max_dst = std::max(max_dst, words[kScanWords * g + 3]);
+  if (cached && hdr.mismatches) {  // the same pointer now holds another index
+    cache_drop(cached);
+    cached.reset();
+  }
 
   // dense runs at tile granularity, long enough for the sweep forms, whose
   // first entry the scan recorded; the longest kMaxDeviceRuns of them
@@ -1650,7 +1776,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     auto run_end = [&](size_t t) {
       while (t < tiles) {
         const size_t g = t / kScanGroupTiles;
-        const uint64_t brk = ~(words[3 * g] & words[3 * g + 1]) >> (t % kScanGroupTiles);
+        const uint64_t brk = ~(words[kScanWords * g] & words[kScanWords * g + 1]) >> (t % kScanGroupTiles);
         if (brk) return std::min(tiles, t + (size_t)__builtin_ctzll(brk));
         t = (g + 1) * kScanGroupTiles;
       }
@@ -1687,7 +1813,6 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   EntryRanges rr = {};
   {
     uint64_t at = 0;
-    rr.pre[0] = 0;
     auto add = [&](uint64_t lo, uint64_t hi) {
       if (hi <= lo) return;
       rr.lo[rr.count] = lo;
@@ -1703,7 +1828,11 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   }
   const size_t resid = rr.pre[rr.count];
   if (resid == 0) return GP_OK;
-  // destinations already (mostly) ascending: keep the call's order
+  if (cached && cached->resid == resid) {  // the same index: its destination-sorted residual
+    GP_HIP_TRY(hipStreamWaitEvent(s, cached->ready, 0));
+    return launch_row_op<OP>(y, x, cached->sorted, resid, gp_double_index{0, 0}, W, limit, s, /*sorted=*/true);
+  }
+  // destinations already (mostly) ascending: the call's order is the sorted one
   size_t resid_tiles = 0, asc_tiles = 0;
   for (uint32_t i = 0; i < rr.count; ++i) {
     size_t t = rr.lo[i] / 64;
@@ -1711,38 +1840,19 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     resid_tiles += t1 - t;
     for (; t < t1 && t % kScanGroupTiles; ++t) asc_tiles += bit(t, 2);
     for (; t + kScanGroupTiles <= t1; t += kScanGroupTiles)
-      asc_tiles += __builtin_popcountll(words[3 * (t / kScanGroupTiles) + 2]);
+      asc_tiles += __builtin_popcountll(words[kScanWords * (t / kScanGroupTiles) + 2]);
     for (; t < t1; ++t) asc_tiles += bit(t, 2);
   }
   const bool ascending = asc_tiles * 10 >= resid_tiles * 9;
-  if (OP != kAddFrom || ascending || resid * W * sizeof(float) < kBinMinBytes) {
-    for (uint32_t i = 0; i < rr.count; ++i) {
-      const int rc = launch_row_op<OP>(y, x, idx + rr.lo[i], rr.hi[i] - rr.lo[i], off, W, limit, s, ascending);
-      if (rc != GP_OK) return rc;
-    }
-    return GP_OK;
+  for (uint32_t i = 0; i < rr.count; ++i) {
+    const int rc = launch_row_op<OP>(y, x, idx + rr.lo[i], rr.hi[i] - rr.lo[i], off, W, limit, s, ascending);
+    if (rc != GP_OK) return rc;
   }
-  // bin the scatter-add's residual by destination, then the sorted-residual kernel
-  int shift = kBinShiftRows;
-  while (((hdr.max_dst >> shift) + 1) > (uint64_t)kBinLds) ++shift;
-  const uint32_t nbins = (uint32_t)((hdr.max_dst >> shift) + 1);
-  char *bws = nullptr;
-  const size_t bin_bytes = resid * sizeof(gp_double_index) + 2 * (size_t)nbins * sizeof(uint32_t);
-  GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&bws), bin_bytes, s));
-  Free free_bins{bws, s};
-  gp_double_index *binned = reinterpret_cast<gp_double_index *>(bws);
-  uint32_t *count = reinterpret_cast<uint32_t *>(bws + resid * sizeof(gp_double_index));
-  uint32_t *cursor = count + nbins;
-  GP_HIP_TRY(hipMemsetAsync(count, 0, nbins * sizeof(uint32_t), s));
-  const size_t nb = std::max<size_t>(1, std::min((size_t)num_cus() * 4, (resid + 4095) / 4096));
-  const size_t per = (resid + nb - 1) / nb;
-  hipLaunchKernelGGL(bin_count_kernel<OP>, dim3((unsigned)nb), dim3(kBlock), 0, s, idx, rr, off.id0, off.id1, shift,
-                     nbins, count, per);
-  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, s, count, nbins, cursor);
-  hipLaunchKernelGGL(bin_place_kernel<OP>, dim3((unsigned)nb), dim3(kBlock), 0, s, idx, rr, off.id0, off.id1, shift,
-                     nbins, cursor, binned, per);
-  GP_HIP_TRY(hipGetLastError());
-  return launch_row_op<OP>(y, x, binned, resid, gp_double_index{0, 0}, W, limit, s, /*sorted=*/true);
+  // a scatter's large unsorted residual: sorted copy for the next call
+  if (OP != kAssignTo && !ascending && resid * W * sizeof(float) >= kSortMinBytes && max_dst < (1ull << 32) &&
+      n < (1ull << 32))
+    return build_cached_plan<OP>(key, idx, rr, max_dst, s);
+  return GP_OK;
 }
 
 // The unplanned calls: large ones plan themselves on the device.
@@ -1773,6 +1883,24 @@ int gp_abi_version(void) { return GP_ABI_VERSION; }
 
 int gp_set_unplanned_min_bytes(size_t min_bytes) {
   g_analyze_min_bytes.store(min_bytes, std::memory_order_relaxed);
+  return GP_OK;
+}
+
+int gp_unplanned_cache_clear(void) {
+  std::vector<std::shared_ptr<CachedPlan>> gone;  // freed outside the lock
+  {
+    std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+    gone.swap(g_plan_cache);
+  }
+  return GP_OK;
+}
+
+int gp_unplanned_cache_entries(size_t *entries, size_t *bytes) {
+  if (!entries || !bytes) return set_error(GP_ERR_INVALID, "null pointer");
+  std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+  *entries = g_plan_cache.size();
+  *bytes = 0;
+  for (auto &p : g_plan_cache) *bytes += p->bytes;
   return GP_OK;
 }
 

@@ -64,6 +64,8 @@ _SIGNATURES = {
     "gp_abi_version": (_i, []),
     "gp_last_error": (_c.c_char_p, []),
     "gp_set_unplanned_min_bytes": (_i, [_sz]),
+    "gp_unplanned_cache_clear": (_i, []),
+    "gp_unplanned_cache_entries": (_i, [_c.POINTER(_sz), _c.POINTER(_sz)]),
     "gp_scatter_add_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),

@@ -21,8 +21,9 @@
  *     turns a non-zero status into an abort with that message.
  *
  * All functions are re-entrant.  Global state: the thread-local error string,
- * and per-device / per-kernel launch facts cached on first use (CU count,
- * resident blocks per CU), which never change once read.
+ * per-device / per-kernel launch facts cached on first use (CU count,
+ * resident blocks per CU), which never change once read, and the unplanned
+ * calls' plan cache (mutex-protected; see gp_unplanned_cache_clear).
  */
 #ifndef GP_REDUCE_H_
 #define GP_REDUCE_H_
@@ -65,6 +66,15 @@ const char *gp_last_error(void);
  * bytes; default 64 MiB; SIZE_MAX: never).  Process-wide; for tests and
  * measurement. */
 int gp_set_unplanned_min_bytes(size_t min_bytes);
+/* The unplanned calls' plan cache (ABI 10): a large scatter-add / init whose
+ * rows outside dense runs are not in ascending destination order runs in op
+ * order once and keeps, for later calls with the same index (same pointer,
+ * size, offsets, row size and limit, and the same content, which every such
+ * call checks entry for entry on the device), a copy of the index and its
+ * rows in destination order: 32 B of HBM per row, at most 4 GiB and 256
+ * indexes, least recently used first out.  Clear it, or read its size. */
+int gp_unplanned_cache_clear(void);
+int gp_unplanned_cache_entries(size_t *entries, size_t *bytes);
 
 /* ---------------------------------------------------------------------------
  * Row operations (client side).  Element (row r, value v) lives at
@@ -86,9 +96,10 @@ int gp_set_unplanned_min_bytes(size_t min_bytes);
  * Calls of at least gp_set_unplanned_min_bytes() of rows (default 64 MiB)
  * plan themselves on the device (ABI 10): one pass over the index finds its
  * dense runs (moved like a row plan's, by the phase-separated sum kernels) and
- * whether the other rows' destinations ascend (if not, they are binned by
- * destination on the device first).  Such a call waits for the stream once,
- * for the index summary, as the reference's call waits at its end
+ * whether the other rows' destinations ascend; if they do not, the rows run in
+ * op order and a destination-sorted copy is kept for the next call with the
+ * same index (gp_unplanned_cache_clear).  Such a call waits for the stream
+ * once, for the index summary, as the reference's call waits at its end
  * (row-op-util.cu:141); smaller calls are fully asynchronous.  Same results
  * either way. */
 int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,

@@ -633,8 +633,19 @@ def analyzed(dev):
     this test; the default (64 MiB) afterwards."""
     from geeps_amd import native
     native.check(native.lib().gp_set_unplanned_min_bytes(0), "gp_set_unplanned_min_bytes")
+    native.check(native.lib().gp_unplanned_cache_clear(), "gp_unplanned_cache_clear")
     yield
     native.check(native.lib().gp_set_unplanned_min_bytes(64 << 20), "gp_set_unplanned_min_bytes")
+    native.check(native.lib().gp_unplanned_cache_clear(), "gp_unplanned_cache_clear")
+
+
+def _cache_entries():
+    import ctypes
+    from geeps_amd import native
+    e, b = ctypes.c_size_t(), ctypes.c_size_t()
+    native.check(native.lib().gp_unplanned_cache_entries(ctypes.byref(e), ctypes.byref(b)),
+                 "gp_unplanned_cache_entries")
+    return e.value, b.value
 
 
 @pytest.mark.parametrize("kind", ["identity", "permuted", "sorted", "runs"])
@@ -655,21 +666,32 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
     x[rng.choice(x.size, 200, replace=False)] = np.float32(-0.0)
     y = rng.standard_normal(n_cache * W).astype(np.float32)
     ti = torch.from_numpy(idx).to(dev)
-    # add
+    tx = T(x, dev)
+    # add, twice: the first call runs and (unsorted residual) builds the plan
+    # cache entry, the second runs the cached destination-sorted residual
     e = y.copy()
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
-    ty = T(y, dev)
-    rowops.add_rows_from_double_index_gpu(ty, T(x, dev), ti, n, off, W, limit)
-    torch.cuda.synchronize()
-    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", kind, W)
+    for call in range(2):
+        ty = T(y, dev)
+        rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, off, W, limit)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", kind, W, call)
+    cached_add = _cache_entries()[0]
     # init: listed rows zeroed, then the add
     e = y.copy()
     e.reshape(n_cache, W)[idx[:, 1] + off[1]] = 0.0
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
-    ty = T(y, dev)
-    rowops.init_rows_from_double_index_gpu(ty, T(x, dev), ti, n, off, W, limit)
-    torch.cuda.synchronize()
-    assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", kind, W)
+    for call in range(2):
+        ty = T(y, dev)
+        rowops.init_rows_from_double_index_gpu(ty, tx, ti, n, off, W, limit)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", kind, W, call)
+    # only an unsorted residual of >= 16 MiB is cached: "permuted" at 128 and
+    # 1024 floats, "runs" at 1024 (its ~9,100 scattered rows); "identity" and
+    # "sorted" residuals ascend, the rest are short
+    expect = 1 if (kind == "permuted" and W >= 128) or (kind == "runs" and W == 1024) else 0
+    assert cached_add == expect, (kind, W)
+    assert _cache_entries()[0] == 2 * cached_add
     # gather with the index's roles swapped: y[id0] = x[id1]
     gidx = np.ascontiguousarray(idx[:, ::-1]) if kind != "sorted" else idx
     g_out = int(gidx[:, 0].max()) + 1 + off[0]
@@ -682,6 +704,35 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
     rowops.assign_rows_to_double_index_gpu(to, T(src, dev), torch.from_numpy(gidx).to(dev), n, off, W, g_lim)
     torch.cuda.synchronize()
     assert np.array_equal(bits(to.cpu().numpy()), bits(e)), ("gather", kind, W)
+
+
+def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
+    """The plan cache keys on the index pointer but trusts no pointer: the same
+    device tensor refilled with another permutation (same size, offsets,
+    limit) must give the new index's sums, not the cached order's; the entry is
+    replaced and the call after that runs the new cached order."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(99)
+    W, n = 128, 40000  # 20 MiB of rows: a cached (unsorted) residual
+    x = rng.standard_normal(n * W).astype(np.float32)
+    y = rng.standard_normal(n * W).astype(np.float32)
+    tx = T(x, dev)
+    ti = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    for round_ in range(3):
+        idx = np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64)
+        if round_ == 2:  # one swapped pair: a single differing entry
+            idx = prev.copy()
+            idx[[5, n - 7], 1] = idx[[n - 7, 5], 1]
+        ti.copy_(torch.from_numpy(idx))
+        e = y.copy()
+        oracle.add_rows_from_double_index(e, x, idx, (0, 0), W)
+        for call in range(2):
+            ty = T(y, dev)
+            rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W)
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), (round_, call)
+            assert _cache_entries()[0] == 1
+        prev = idx
 
 
 @pytest.mark.parametrize("kind", ["identity", "permuted", "mixed"])

@@ -124,7 +124,9 @@ def _collect(procs, timeout):
     """Wait for every process under one deadline; on a failure or a hang, kill
     the rest and report EVERY process's output (a hang in one process usually
     starts as an abort in another)."""
-    deadline = time.monotonic() + timeout
+    # under the GPU box's 180-s silence limit, so a hang is reported here with
+    # every process's output instead of the whole run being killed
+    deadline = time.monotonic() + min(timeout, 170)
     for pr in procs:
         try:
             pr.wait(timeout=max(0.1, deadline - time.monotonic()))
