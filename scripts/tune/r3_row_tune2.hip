@@ -110,15 +110,15 @@ int main(int argc, char **argv) {
   std::printf("hipcub temp bytes %zu\n", temp_bytes);
   char *ws, *hws;
   const size_t groups = (R / 64 + kScanGroupTiles - 1) / kScanGroupTiles;
-  const size_t scan_bytes = kScanWordsOff + groups * 3 * 8;
+  const size_t scan_bytes = kScanWordsOff + groups * kScanWords * 8;
   CK(hipMalloc(&ws, scan_bytes));
   CK(hipHostMalloc(reinterpret_cast<void **>(&hws), scan_bytes, hipHostMallocDefault));
   const size_t G = (size_t)num_cus();
-  auto scan = [&](const gp_double_index *ix, bool d2h) {
+  auto scan = [&](const gp_double_index *ix, bool d2h, bool cmp = false) {
     return [=] {
       CK(hipMemsetAsync(ws, 0, sizeof(ScanHeader), 0));
       hipLaunchKernelGGL(index_scan_kernel<kAddFrom>, dim3((unsigned)std::min(groups, G * 8)), dim3(kBlock), 0, 0,
-                         ix, R, 0, 0, W, ~size_t(0), ws);
+                         ix, R, 0, 0, W, ~size_t(0), cmp ? idn : nullptr, ws);
       if (d2h) {
         CK(hipMemcpyAsync(hws, ws, scan_bytes, hipMemcpyDeviceToHost, 0));
         CK(hipStreamSynchronize(0));
@@ -159,6 +159,8 @@ int main(int argc, char **argv) {
       {"scan (prod v2)", scan(rnd, false), 16.0 * R},
       {"scan + D2H + sync", scan(rnd, true), 16.0 * R},
       {"scan ident + D2H + sync", scan(idn, true), 16.0 * R},
+      {"scan + compare (kernel only)", scan(rnd, false, true), 32.0 * R},
+      {"scan + compare + D2H + sync", scan(rnd, true, true), 32.0 * R},
       {"sort: split", sort(1), 24.0 * R},
       {"sort: split + radix 23b", sort(2), 24.0 * R},
       {"sort: split + radix + join", sort(3), 24.0 * R},
@@ -188,11 +190,12 @@ int main(int argc, char **argv) {
     scan(idn, true)();
     const ScanHeader *hd = reinterpret_cast<const ScanHeader *>(hws);
     const uint64_t *w = reinterpret_cast<const uint64_t *>(hws + kScanWordsOff);
-    std::printf("check scan ident: starts %u max %llu words %llx %llx %llx\n", hd->n_starts, hd->max_dst,
-                (unsigned long long)w[0], (unsigned long long)w[1], (unsigned long long)w[2]);
-    scan(rnd, true)();
-    std::printf("check scan rand: starts %u max %llu words %llx %llx %llx\n", hd->n_starts, hd->max_dst,
-                (unsigned long long)w[0], (unsigned long long)w[1], (unsigned long long)w[2]);
+    std::printf("check scan ident: starts %u max %llu words %llx %llx %llx\n", hd->n_starts,
+                (unsigned long long)w[3], (unsigned long long)w[0], (unsigned long long)w[1],
+                (unsigned long long)w[2]);
+    scan(rnd, true, true)();
+    std::printf("check scan rand vs ident copy: starts %u mismatching waves %u max %llu\n", hd->n_starts,
+                hd->mismatches, (unsigned long long)w[3]);
   }
   hipEvent_t ea, eb;
   CK(hipEventCreate(&ea));
