@@ -1417,25 +1417,20 @@ int radix_sort_pairs_u32(const uint32_t *ki, uint32_t *ko, const uint32_t *vi, u
   return rc == GP_OK ? GP_OK : set_error(rc, err);
 }
 
-// Entry e (raw) and its endpoints (offsets applied); whether its guarded row
-// is whole.  Dead entries (e >= n) are not whole.
-template <int OP>
-__device__ __forceinline__ bool scan_entry(const gp_double_index *idx, size_t n, size_t e, uint64_t off0,
-                                           uint64_t off1, size_t row_size, size_t limit, gp_double_index &raw,
-                                           uint64_t &from, uint64_t &to) {
-  from = to = 0;
-  raw = gp_double_index{0, 0};
-  if (e >= n) return false;
-  raw = idx[e];
-  row_endpoints<OP>(raw, off0, off1, from, to);
-  return ((OP == kAssignTo ? to : from) + 1) * row_size <= limit;
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int lane) {  // v of `lane`, wave-uniform
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // One block (4 waves) per group of 64 tiles (4096 entries); each wave takes 16
 // tiles with all 17 of its loads (the tile before its first, then its own) in
-// flight at once.  No global atomics on the common path (a per-group word
-// carries the group's largest destination).
-template <int OP>
+// flight at once.  A tile is dense when every lane's endpoints are lane 0's
+// plus the lane number (lane 0's and lane 63's values are read into scalar
+// registers, no LDS traffic); only the ascending test needs a lane shuffle.
+// No global atomics on the common path (a per-group word carries the group's
+// largest destination).
+template <int OP, bool CMP>
 __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_index *__restrict__ idx, size_t n,
                                                             uint64_t off0, uint64_t off1, size_t row_size,
                                                             size_t limit, const gp_double_index *__restrict__ cached,
@@ -1453,27 +1448,34 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
     uint64_t f[kScanWaveTiles + 1], to[kScanWaveTiles + 1];
     bool whole[kScanWaveTiles + 1];
     bool differs = false;
+    // every load unconditional (addresses clamped into the index, results
+    // masked after), so all of a wave's loads are in flight before the first wait
+    gp_double_index raw[kScanWaveTiles + 1], cp[kScanWaveTiles + 1];
 #pragma unroll
     for (int k = 0; k <= kScanWaveTiles; ++k) {  // k = 0: the tile before t0
-      gp_double_index raw;
-      if (t0 + k >= 1) {
-        const size_t e = (t0 + k - 1) * 64 + wl;
-        whole[k] = scan_entry<OP>(idx, n, e, off0, off1, row_size, limit, raw, f[k], to[k]);
-        if (cached && k > 0 && e < n) {
-          const gp_double_index c = cached[e];
-          differs = differs || c.id0 != raw.id0 || c.id1 != raw.id1;
-        }
-      } else {
-        whole[k] = false;
-        f[k] = to[k] = 0;
-      }
+      const size_t e = t0 + k >= 1 ? (t0 + k - 1) * 64 + wl : 0;
+      const size_t ec = e < n ? e : n - 1;
+      raw[k] = idx[ec];
+      if (CMP && k > 0) cp[k] = cached[ec];
     }
-    uint64_t pf = shfl64(f[0], 63), pt = shfl64(to[0], 63);
-    bool prev_dense;
-    {
-      const uint64_t lf = shfl64(f[0], (wl + 63) & 63), lt = shfl64(to[0], (wl + 63) & 63);
-      prev_dense = t0 >= 1 && __all(whole[0] && (wl == 0 || (f[0] == lf + 1 && to[0] == lt + 1)));
+#pragma unroll
+    for (int k = 0; k <= kScanWaveTiles; ++k) {  // selects, no branches: the loads stay hoisted
+      const size_t e = t0 + k >= 1 ? (t0 + k - 1) * 64 + wl : 0;
+      const bool live = (t0 + k >= 1) & (e < n);
+      uint64_t a, b;
+      row_endpoints<OP>(raw[k], off0, off1, a, b);
+      const bool wh = ((OP == kAssignTo ? b : a) + 1) * row_size <= limit;
+      whole[k] = live & wh;
+      f[k] = live ? a : 0;
+      to[k] = live ? b : 0;
+      if (CMP && k > 0) differs |= live & ((cp[k].id0 != raw[k].id0) | (cp[k].id1 != raw[k].id1));
     }
+    auto tile_dense = [&](int k) {  // every lane whole and lane 0 + lane
+      const uint64_t b0 = lane_u64(f[k], 0), b1 = lane_u64(to[k], 0);
+      return __all(whole[k] && f[k] == b0 + (uint64_t)wl && to[k] == b1 + (uint64_t)wl);
+    };
+    bool prev_dense = t0 >= 1 && tile_dense(0);
+    uint64_t pf = lane_u64(f[0], 63), pt = lane_u64(to[0], 63);  // the entry before the tile
     uint32_t wd = 0, wc = 0, wa = 0;
     uint64_t mx = 0;
 #pragma unroll
@@ -1481,24 +1483,22 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
       const size_t t = t0 + k - 1;
       const size_t e = t * 64 + wl;
       const bool live = e < n;
-      const uint64_t lf = shfl64(f[k], (wl + 63) & 63), lt = shfl64(to[k], (wl + 63) & 63);
-      const uint64_t bf = wl == 0 ? pf : lf, bt = wl == 0 ? pt : lt;  // the entry before this one
-      const bool has_before = e > 0;
-      const bool step = has_before && f[k] == bf + 1 && to[k] == bt + 1;
-      const bool dense = t < tiles && __all(whole[k] && (wl == 0 || step));
-      const bool cont = __shfl(step ? 1 : 0, 0, 64) != 0;
-      const bool asc = __all(!live || !has_before || to[k] > bt);
+      const uint64_t f0 = lane_u64(f[k], 0), to0 = lane_u64(to[k], 0);
+      const bool dense = t < tiles && tile_dense(k);
+      const bool cont = t > 0 && f0 == pf + 1 && to0 == pt + 1;  // wave-uniform
+      const uint64_t lt = shfl64(to[k], (wl + 63) & 63);
+      const bool asc = __all(!live || e == 0 || to[k] > (wl == 0 ? pt : lt));
       if (live && to[k] > mx) mx = to[k];
       wd |= (dense ? 1u : 0u) << (k - 1);
       wc |= (cont ? 1u : 0u) << (k - 1);
       wa |= (asc ? 1u : 0u) << (k - 1);
       if (dense && !(cont && prev_dense) && wl == 0) {
         const unsigned slot = atomicAdd(&hdr->n_starts, 1u);
-        if (slot < (unsigned)kMaxRunStarts) starts[slot] = RunStart{t, f[k], to[k]};
+        if (slot < (unsigned)kMaxRunStarts) starts[slot] = RunStart{t, f0, to0};
       }
       prev_dense = dense;
-      pf = shfl64(f[k], 63);
-      pt = shfl64(to[k], 63);
+      pf = lane_u64(f[k], 63);
+      pt = lane_u64(to[k], 63);
     }
     if (__any(differs) && wl == 0) atomicAdd(&hdr->mismatches, 1u);
     for (int o = 32; o > 0; o >>= 1) {
@@ -1743,8 +1743,12 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   GP_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(ScanHeader), s));
   {
     const size_t grid = std::max<size_t>(1, std::min(groups, (size_t)num_cus() * 8));
-    hipLaunchKernelGGL(index_scan_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, n, off.id0, off.id1,
-                       W, limit, cached ? cached->copy : nullptr, ws);
+    if (cached)
+      hipLaunchKernelGGL((index_scan_kernel<OP, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, idx, n, off.id0,
+                         off.id1, W, limit, cached->copy, ws);
+    else
+      hipLaunchKernelGGL((index_scan_kernel<OP, false>), dim3((unsigned)grid), dim3(kBlock), 0, s, idx, n, off.id0,
+                         off.id1, W, limit, nullptr, ws);
     GP_HIP_TRY(hipGetLastError());
   }
   char *h = static_cast<char *>(g_scan_landing.get(scan_bytes));

@@ -117,8 +117,12 @@ int main(int argc, char **argv) {
   auto scan = [&](const gp_double_index *ix, bool d2h, bool cmp = false) {
     return [=] {
       CK(hipMemsetAsync(ws, 0, sizeof(ScanHeader), 0));
-      hipLaunchKernelGGL(index_scan_kernel<kAddFrom>, dim3((unsigned)std::min(groups, G * 8)), dim3(kBlock), 0, 0,
-                         ix, R, 0, 0, W, ~size_t(0), cmp ? idn : nullptr, ws);
+      if (cmp)
+        hipLaunchKernelGGL((index_scan_kernel<kAddFrom, true>), dim3((unsigned)std::min(groups, G * 8)),
+                           dim3(kBlock), 0, 0, ix, R, 0, 0, W, ~size_t(0), idn, ws);
+      else
+        hipLaunchKernelGGL((index_scan_kernel<kAddFrom, false>), dim3((unsigned)std::min(groups, G * 8)),
+                           dim3(kBlock), 0, 0, ix, R, 0, 0, W, ~size_t(0), nullptr, ws);
       if (d2h) {
         CK(hipMemcpyAsync(hws, ws, scan_bytes, hipMemcpyDeviceToHost, 0));
         CK(hipStreamSynchronize(0));
