@@ -1397,7 +1397,7 @@ constexpr size_t kPlanCacheEntries = 256;
 
 struct ScanHeader {
   unsigned int n_starts;
-  unsigned int mismatches;  // waves that saw an entry differ from the cached copy
+  unsigned int mismatches;  // blocks that saw an entry differ from the cached copy
   uint64_t pad;
 };
 struct RunStart {
@@ -1500,7 +1500,8 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
       pf = lane_u64(f[k], 63);
       pt = lane_u64(to[k], 63);
     }
-    if (__any(differs) && wl == 0) atomicAdd(&hdr->mismatches, 1u);
+    __shared__ unsigned block_differs;
+    if (CMP && threadIdx.x == 0) block_differs = 0;
     for (int o = 32; o > 0; o >>= 1) {
       const uint64_t v = shfl64(mx, (wl + o) & 63);
       mx = v > mx ? v : mx;
@@ -1512,6 +1513,9 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
       part[3][wv] = mx;
     }
     __syncthreads();
+    if (CMP && __any(differs) && wl == 0) atomicOr(&block_differs, 1u);  // one global atomic per block, below
+    __syncthreads();
+    if (CMP && threadIdx.x == 0 && block_differs) atomicAdd(&hdr->mismatches, 1u);
     if (threadIdx.x < kScanWords) {
       uint64_t w = 0;
       for (int v = 0; v < kBlock / 64; ++v)

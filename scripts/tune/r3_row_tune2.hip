@@ -96,7 +96,7 @@ int main(int argc, char **argv) {
     b[perm[r]] = {r, perm[r]};
     c[r] = {r, r};
   }
-  gp_double_index *rnd = upload(a), *srt = upload(b), *idn = upload(c), *sorted_out;
+  gp_double_index *rnd = upload(a), *srt = upload(b), *idn = upload(c), *rnd_copy = upload(a), *sorted_out;
   CK(hipMalloc(&sorted_out, R * 16));
   uint32_t *k0, *v0, *k1, *v1;
   CK(hipMalloc(&k0, R * 4));
@@ -114,12 +114,13 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&ws, scan_bytes));
   CK(hipHostMalloc(reinterpret_cast<void **>(&hws), scan_bytes, hipHostMallocDefault));
   const size_t G = (size_t)num_cus();
-  auto scan = [&](const gp_double_index *ix, bool d2h, bool cmp = false) {
+  auto scan = [&](const gp_double_index *ix, bool d2h, bool cmp = false, const gp_double_index *cmp_against = nullptr) {
+    if (!cmp_against) cmp_against = idn;
     return [=] {
       CK(hipMemsetAsync(ws, 0, sizeof(ScanHeader), 0));
       if (cmp)
         hipLaunchKernelGGL((index_scan_kernel<kAddFrom, true>), dim3((unsigned)std::min(groups, G * 8)),
-                           dim3(kBlock), 0, 0, ix, R, 0, 0, W, ~size_t(0), idn, ws);
+                           dim3(kBlock), 0, 0, ix, R, 0, 0, W, ~size_t(0), cmp_against, ws);
       else
         hipLaunchKernelGGL((index_scan_kernel<kAddFrom, false>), dim3((unsigned)std::min(groups, G * 8)),
                            dim3(kBlock), 0, 0, ix, R, 0, 0, W, ~size_t(0), nullptr, ws);
@@ -163,8 +164,9 @@ int main(int argc, char **argv) {
       {"scan (prod v2)", scan(rnd, false), 16.0 * R},
       {"scan + D2H + sync", scan(rnd, true), 16.0 * R},
       {"scan ident + D2H + sync", scan(idn, true), 16.0 * R},
-      {"scan + compare (kernel only)", scan(rnd, false, true), 32.0 * R},
-      {"scan + compare + D2H + sync", scan(rnd, true, true), 32.0 * R},
+      {"scan + compare, all differ", scan(rnd, false, true), 32.0 * R},
+      {"scan + compare, equal (kernel)", scan(rnd, false, true, rnd_copy), 32.0 * R},
+      {"scan + compare, equal + D2H + sync", scan(rnd, true, true, rnd_copy), 32.0 * R},
       {"sort: split", sort(1), 24.0 * R},
       {"sort: split + radix 23b", sort(2), 24.0 * R},
       {"sort: split + radix + join", sort(3), 24.0 * R},

@@ -106,6 +106,9 @@ def _env(transport, jitter_us=0, empty_setup=False, extra=None):
     env["GEEPS_TRANSPORT"] = transport  # "ipc": same-node rows over IPC-mapped HBM; "tcp": sockets
     # a peer that dies before listening fails the others in a minute, not five
     env.setdefault("GEEPS_CONNECT_TIMEOUT_S", "60")
+    # a server stuck waiting for a master-version release fails loudly (with its
+    # holders matrix) well inside the test's own deadline
+    env.setdefault("GEEPS_VERSION_WAIT_S", "60")
     if jitter_us:
         env["GEEPS_TEST_JITTER_US"] = str(jitter_us)
     return env
