@@ -166,12 +166,13 @@ void ClientLib::start_network() {
       std::string err;
       const int fd = connect_tcp(config_.host_list[s], port_of(s, ch.id), connect_timeout_s(), &err);
       GP_CHECK_MSG(fd >= 0, err);
-      HelloMsg hello{};
-      hello.cmd = kHelloCmd;
-      hello.process_id = process_id_;
-      hello.ipc = ipc_to(s) ? 1u : 0u;  // takes same-node refreshes in place
-      std::memcpy(hello.pci_bus_id, pci_bus_id_, sizeof hello.pci_bus_id);
-      GP_CHECK(send_frame(fd, {Part{&hello, sizeof hello}}));
+      // ZMTP READY as the reference's client ROUTER ("client-<i>",
+      // clientlib.cpp:107); the server must answer as "tablet-<s>"
+      PeerInfo peer;
+      GP_CHECK_MSG(zmtp_handshake(fd, "client-" + std::to_string(process_id_), hello_props(s), &peer, &err),
+                   err << " (server " << s << ", channel " << ch.id << ")");
+      GP_CHECK_MSG(peer.identity == "tablet-" + std::to_string(s),
+                   "port " << port_of(s, ch.id) << " answered as '" << peer.identity << "', expected tablet-" << s);
       ch.server_fd[s] = fd;
       ch.client_readers.emplace_back([this, &ch, s, fd] { client_reader(ch, s, fd); });
     }
@@ -183,22 +184,27 @@ void ClientLib::server_accept_loop(Channel &ch, int expected) {
   for (int i = 0; i < expected; ++i) {
     const int fd = accept_tcp(ch.listen_fd);
     GP_CHECK_MSG(fd >= 0, "accept failed on channel " << ch.id);
-    std::vector<RecvPart> parts;
-    std::vector<std::vector<char>> scratch;
-    GP_CHECK(recv_frame(fd, parts, scratch, nullptr, nullptr));
-    GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(HelloMsg));
-    HelloMsg hello;
-    std::memcpy(&hello, parts[0].data, sizeof hello);
-    GP_CHECK_EQ(hello.cmd, kHelloCmd);
-    const uint32_t cid = hello.process_id;
+    // ZMTP READY as the reference's server ROUTER ("tablet-<i>",
+    // server-entry.cpp:66); the peer names itself "client-<i>"
+    PeerInfo peer;
+    std::string err;
+    GP_CHECK_MSG(zmtp_handshake(fd, "tablet-" + std::to_string(process_id_), {}, &peer, &err),
+                 err << " (channel " << ch.id << ")");
+    uint32_t cid = ~0u;
+    {
+      const std::string &id = peer.identity;
+      char *end = nullptr;
+      if (id.compare(0, 7, "client-") == 0 && id.size() > 7) cid = (uint32_t)std::strtoul(id.c_str() + 7, &end, 10);
+      GP_CHECK_MSG(end && *end == 0, "connection from '" << id << "', expected a client-<i> identity");
+    }
     GP_CHECK_LT(cid, num_processes_);
     GP_CHECK_MSG(ch.client_fd[cid] < 0, "duplicate client " << cid);
     ch.client_fd[cid] = fd;
-    ch.ipc_client[cid] = hello.ipc && ipc_to(cid);
-    hello.pci_bus_id[sizeof hello.pci_bus_id - 1] = 0;
+    const std::string *ipc = peer.prop("X-Geeps-Ipc"), *bus = peer.prop("X-Geeps-Pci-Bus-Id");
+    ch.ipc_client[cid] = ipc && *ipc == "1" && ipc_to(cid);
     // process cid hosts client cid and server cid on the same GPU, so one
-    // hello decides both directions
-    ch.other_gpu[cid] = std::strcmp(hello.pci_bus_id, pci_bus_id_) != 0;
+    // READY decides both directions
+    ch.other_gpu[cid] = !bus || *bus != pci_bus_id_;
     auto staged = [&](int mode) { return ipc_to(cid) && (mode == 1 || (mode < 0 && ch.other_gpu[cid])); };
     ch.stage_from[cid] = staged(stage_updates_mode_);
     ch.stage_refresh_from[cid] = staged(stage_refresh_mode_);

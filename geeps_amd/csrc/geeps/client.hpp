@@ -228,6 +228,11 @@ class ClientLib {
   void client_reader(Channel &ch, uint32_t server_id, int fd);
   uint16_t port_of(uint32_t process, uint32_t channel) const;
   bool ipc_to(uint32_t s) const { return s != process_id_ && same_node_[s]; }
+  // libgeeps' own READY properties to server s: takes same-node refreshes in
+  // place, and which GPU it runs on (a peer on another GPU is staged)
+  std::vector<std::pair<std::string, std::string>> hello_props(uint32_t s) const {
+    return {{"X-Geeps-Ipc", ipc_to(s) ? "1" : "0"}, {"X-Geeps-Pci-Bus-Id", pci_bus_id_}};
+  }
   bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r, bool *held);
   void send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts);
   void ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a);

@@ -1,4 +1,4 @@
-// TCP framing for libgeeps — see net.hpp.
+// ZMTP/3.0 ROUTER transport for libgeeps — see net.hpp.
 #include "net.hpp"
 
 #include <arpa/inet.h>
@@ -9,6 +9,11 @@
 #include <sys/uio.h>
 #include <unistd.h>
 
+#include <endian.h>
+#include <limits.h>
+
+#include <algorithm>
+#include <cctype>
 #include <cerrno>
 #include <chrono>
 #include <cstring>
@@ -55,42 +60,213 @@ void tune(int fd) {
   setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
 }
 
+// writev until every byte of `iov[0..n)` is out (advances over partial writes)
+bool writev_all(int fd, iovec *iov, int n) {
+  while (n > 0) {
+    msghdr m{};
+    m.msg_iov = iov;
+    m.msg_iovlen = (size_t)(n < IOV_MAX ? n : IOV_MAX);
+    ssize_t w = ::sendmsg(fd, &m, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    while (n > 0 && (size_t)w >= iov->iov_len) {
+      w -= (ssize_t)iov->iov_len;
+      ++iov;
+      --n;
+    }
+    if (n > 0) {
+      iov->iov_base = static_cast<char *>(iov->iov_base) + w;
+      iov->iov_len -= (size_t)w;
+    }
+  }
+  return true;
+}
+
+// ZMTP/3.0 (rfc.zeromq.org 23/ZMTP) constants
+constexpr uint8_t kFlagMore = 0x01, kFlagLong = 0x02, kFlagCommand = 0x04;
+constexpr size_t kGreetingBytes = 64;
+constexpr size_t kMaxCommandBytes = 1 << 20;  // a READY with a few short properties
+
+// frame header: flags + 1-byte or 8-byte big-endian size; returns its length
+size_t frame_header(uint8_t *h, uint8_t flags, uint64_t size) {
+  if (size > 255) {
+    h[0] = flags | kFlagLong;
+    const uint64_t be = htobe64(size);
+    std::memcpy(h + 1, &be, 8);
+    return 9;
+  }
+  h[0] = flags;
+  h[1] = (uint8_t)size;
+  return 2;
+}
+
+// the rest of a frame header after its flags byte
+bool read_size(int fd, uint8_t flags, uint64_t *size) {
+  if (flags & kFlagLong) {
+    uint64_t be;
+    if (!read_all(fd, &be, 8)) return false;
+    *size = be64toh(be);
+    return true;
+  }
+  uint8_t s;
+  if (!read_all(fd, &s, 1)) return false;
+  *size = s;
+  return true;
+}
+
+bool iequal(const std::string &a, const std::string &b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (std::tolower((unsigned char)a[i]) != std::tolower((unsigned char)b[i])) return false;
+  return true;
+}
+
+void put_prop(std::string &body, const std::string &name, const std::string &value) {
+  body.push_back((char)name.size());
+  body += name;
+  const uint32_t be = htobe32((uint32_t)value.size());
+  body.append(reinterpret_cast<const char *>(&be), 4);
+  body += value;
+}
+
+// the body of a command: name (short string) + data
+bool split_command(const std::vector<char> &body, std::string *name, size_t *data_at) {
+  if (body.empty()) return false;
+  const size_t n = (uint8_t)body[0];
+  if (1 + n > body.size()) return false;
+  name->assign(body.data() + 1, n);
+  *data_at = 1 + n;
+  return true;
+}
+
+bool read_command(int fd, std::vector<char> *body) {
+  uint8_t flags;
+  if (!read_all(fd, &flags, 1)) return false;
+  uint64_t size;
+  if (!(flags & kFlagCommand) || (flags & ~(kFlagLong | kFlagCommand)) || !read_size(fd, flags, &size) ||
+      size > kMaxCommandBytes)
+    return false;
+  body->resize(size);
+  return size == 0 || read_all(fd, body->data(), size);
+}
+
 }  // namespace
 
-bool send_frame(int fd, const std::vector<Part> &parts) {
-  std::vector<char> head(8 + 8 * parts.size());
-  const uint32_t magic = kFrameMagic, np = (uint32_t)parts.size();
-  std::memcpy(head.data(), &magic, 4);
-  std::memcpy(head.data() + 4, &np, 4);
-  for (size_t i = 0; i < parts.size(); ++i) {
-    const uint64_t len = parts[i].size;
-    std::memcpy(head.data() + 8 + 8 * i, &len, 8);
+const std::string *PeerInfo::prop(const std::string &name) const {
+  for (const auto &p : props)
+    if (iequal(p.first, name)) return &p.second;
+  return nullptr;
+}
+
+bool zmtp_handshake(int fd, const std::string &identity,
+                    const std::vector<std::pair<std::string, std::string>> &extra, PeerInfo *peer,
+                    std::string *err) {
+  auto fail = [&](const std::string &why) {
+    if (err) *err = "ZMTP handshake: " + why;
+    return false;
+  };
+  // greeting: signature, version 3.0, mechanism NULL, as-server 0, filler
+  uint8_t g[kGreetingBytes] = {};
+  g[0] = 0xFF;
+  g[9] = 0x7F;
+  g[10] = 3;
+  g[11] = 0;
+  std::memcpy(g + 12, "NULL", 4);
+  if (!write_all(fd, g, sizeof g)) return fail("greeting not sent");
+  uint8_t pg[kGreetingBytes];
+  if (!read_all(fd, pg, sizeof pg)) return fail("peer closed during the greeting");
+  if (pg[0] != 0xFF || !(pg[9] & 0x01)) return fail("peer is not a ZMTP 2+ endpoint");
+  if (pg[10] < 3) return fail("peer speaks ZMTP " + std::to_string(pg[10]) + ".x, need 3.x");
+  static const uint8_t null_mech[20] = {'N', 'U', 'L', 'L'};
+  if (std::memcmp(pg + 12, null_mech, 20) != 0)
+    return fail("peer asks for security mechanism '" +
+                std::string(reinterpret_cast<const char *>(pg + 12), strnlen(reinterpret_cast<const char *>(pg + 12), 20)) +
+                "', only NULL is spoken");
+  // READY, ours then theirs
+  std::string body("\x05READY", 6);
+  put_prop(body, "Socket-Type", "ROUTER");
+  put_prop(body, "Identity", identity);
+  for (const auto &p : extra) put_prop(body, p.first, p.second);
+  uint8_t h[9];
+  iovec iov[2] = {{h, frame_header(h, kFlagCommand, body.size())}, {&body[0], body.size()}};
+  if (!writev_all(fd, iov, 2)) return fail("READY not sent");
+  std::vector<char> rb;
+  if (!read_command(fd, &rb)) return fail("no READY command from the peer");
+  std::string name;
+  size_t at = 0;
+  if (!split_command(rb, &name, &at)) return fail("malformed command");
+  if (name == "ERROR") {
+    const size_t n = at < rb.size() ? (uint8_t)rb[at] : 0;
+    return fail("peer sent ERROR: " + std::string(rb.data() + at + 1, std::min(n, rb.size() - at - 1)));
   }
-  if (!write_all(fd, head.data(), head.size())) return false;
-  for (const Part &p : parts)
-    if (p.size && !write_all(fd, p.data, p.size)) return false;
+  if (name != "READY") return fail("expected READY, got '" + name + "'");
+  PeerInfo info;
+  while (at < rb.size()) {
+    const size_t nl = (uint8_t)rb[at];
+    if (at + 1 + nl + 4 > rb.size()) return fail("truncated READY property");
+    std::string pn(rb.data() + at + 1, nl);
+    uint32_t vl;
+    std::memcpy(&vl, rb.data() + at + 1 + nl, 4);
+    vl = be32toh(vl);
+    at += 1 + nl + 4;
+    if (vl > rb.size() - at) return fail("truncated READY property value");
+    info.props.emplace_back(std::move(pn), std::string(rb.data() + at, vl));
+    at += vl;
+  }
+  if (const std::string *t = info.prop("Socket-Type")) info.socket_type = *t;
+  if (const std::string *i = info.prop("Identity")) info.identity = *i;
+  if (info.socket_type != "ROUTER" && info.socket_type != "DEALER" && info.socket_type != "REQ")
+    return fail("a ROUTER cannot talk to a '" + info.socket_type + "' socket");
+  if (peer) *peer = std::move(info);
   return true;
+}
+
+bool send_frame(int fd, const std::vector<Part> &parts) {
+  if (parts.empty() || parts.size() > kMaxParts) return false;
+  uint8_t heads[kMaxParts][9];
+  iovec iov[2 * kMaxParts];
+  int n = 0;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const uint8_t flags = i + 1 < parts.size() ? kFlagMore : 0;
+    iov[n++] = {heads[i], frame_header(heads[i], flags, parts[i].size)};
+    if (parts[i].size) iov[n++] = {const_cast<void *>(parts[i].data), parts[i].size};
+  }
+  return writev_all(fd, iov, n);
 }
 
 bool recv_frame(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<char>> &scratch,
                 void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx) {
-  uint32_t hdr[2];
-  if (!read_all(fd, hdr, sizeof hdr)) return false;
-  if (hdr[0] != kFrameMagic || hdr[1] > 64) return false;
-  std::vector<uint64_t> lens(hdr[1]);
-  if (hdr[1] && !read_all(fd, lens.data(), 8 * lens.size())) return false;
-  parts.assign(lens.size(), RecvPart{nullptr, 0});
-  scratch.resize(lens.size());
-  for (size_t i = 0; i < lens.size(); ++i) {
-    void *dst = alloc ? alloc(ctx, i, lens[i]) : nullptr;
+  parts.clear();
+  scratch.resize(kMaxParts);
+  for (;;) {
+    uint8_t flags;
+    if (!read_all(fd, &flags, 1)) return false;
+    if (flags & ~(kFlagMore | kFlagLong | kFlagCommand)) return false;  // reserved bits set
+    uint64_t size;
+    if (!read_size(fd, flags, &size)) return false;
+    if (flags & kFlagCommand) {
+      // PING / PONG / SUBSCRIBE ...: nothing a ROUTER data path acts on
+      if (size > kMaxCommandBytes) return false;
+      std::vector<char> body(size);
+      if (size && !read_all(fd, body.data(), size)) return false;
+      std::string name;
+      size_t at = 0;
+      if (!split_command(body, &name, &at) || name == "ERROR") return false;
+      continue;
+    }
+    const size_t i = parts.size();
+    if (i == kMaxParts) return false;
+    void *dst = alloc ? alloc(ctx, i, size) : nullptr;
     if (!dst) {
-      scratch[i].resize(lens[i]);
+      scratch[i].resize(size);
       dst = scratch[i].data();
     }
-    if (lens[i] && !read_all(fd, dst, lens[i])) return false;
-    parts[i] = RecvPart{dst, lens[i]};
+    if (size && !read_all(fd, dst, size)) return false;
+    parts.push_back(RecvPart{dst, size});
+    if (!(flags & kFlagMore)) return true;
   }
-  return true;
 }
 
 int listen_tcp(uint16_t port, std::string *err) {

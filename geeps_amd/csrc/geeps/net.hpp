@@ -2,49 +2,65 @@
 #define GEEPS_AMD_NET_HPP_
 
 // Socket ends of the reduction path.  The reference moves update pushes and
-// shard refreshes over ZeroMQ ROUTER sockets (src/common/router-handler.cpp);
-// libgeeps uses plain TCP with a minimal multipart framing whose PARTS are the
-// reference's message frames byte for byte (wire.hpp):
+// shard refreshes between ZeroMQ ROUTER sockets (src/common/router-handler.cpp:
+// 69-120): each client's ROUTER ("client-<i>") connects to every server's
+// ROUTER ("tablet-<i>", bound on tcp_base_port + channel, server-entry.cpp:
+// 56-68), and one message is a multipart of the reference's structs
+// (encoder-decoder.cpp:105-150, server-encoder-decoder.cpp:228-250).
 //
-//   frame := magic u32 'GPS1' | nparts u32 | len u64 x nparts | part bytes ...
+// libgeeps speaks the same wire protocol natively, with no ZeroMQ library:
+// ZMTP/3.0 with the NULL security mechanism as a ROUTER socket.
 //
-// A connection opens with one HELLO frame carrying the client's process id.
-// Only the framing differs from ZMQ's ZMTP; the payloads decode with the
-// reference's structs unchanged.
+//   greeting  0xFF 0*8 0x7F | version 3.0 | "NULL" + 0*16 | as-server 0 | 0*31
+//   READY     command frame: "READY" + properties Socket-Type=ROUTER,
+//             Identity=client-<i> | tablet-<i>, plus libgeeps' own X-Geeps-*
+//             properties (same-node IPC, the GPU's PCI bus id)
+//   message   frames: flags (0x01 MORE, 0x02 LONG) | size u8 or u64 BE | body
+//
+// One TCP connection per (client, server) pair carries both directions, as the
+// reference's ROUTER-to-ROUTER connection does.  A stock libzmq ROUTER peer
+// interoperates (tests/test_zmtp.py drives one through ctypes).
 
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace geeps {
-
-constexpr uint32_t kFrameMagic = 0x31535047u;  // "GPS1"
-constexpr uint32_t kHelloCmd = 0x48454c4fu;    // "HELO"
-
-// First frame on a client -> server connection.
-struct HelloMsg {
-  uint32_t cmd;         // kHelloCmd
-  uint32_t process_id;  // the connecting client
-  uint32_t ipc;         // it takes same-node refreshes in place
-  uint32_t pad;
-  char pci_bus_id[32];  // its GPU (gp_device_pci_bus_id): a peer on another GPU
-                        // has its IPC-mapped buckets copied to local HBM first
-};
 
 struct Part {
   const void *data;
   size_t size;
 };
 
-// Blocking helpers on a connected socket.  Return false on EOF / error.
+// A ZMTP peer as its READY command described it.
+struct PeerInfo {
+  std::string socket_type;
+  std::string identity;
+  std::vector<std::pair<std::string, std::string>> props;  // every property, in order
+  const std::string *prop(const std::string &name) const;   // case-insensitive
+};
+
+// ZMTP/3.0 NULL handshake on a connected socket: greeting both ways, then our
+// READY (Socket-Type ROUTER, Identity `identity`, then `extra`) and the peer's.
+// False with `*err` set on EOF, a non-ZMTP-3 peer, another mechanism, an ERROR
+// command or a socket type a ROUTER cannot talk to.
+bool zmtp_handshake(int fd, const std::string &identity,
+                    const std::vector<std::pair<std::string, std::string>> &extra, PeerInfo *peer,
+                    std::string *err);
+
+// One multipart message (every part but the last flagged MORE).  Blocking.
 bool send_frame(int fd, const std::vector<Part> &parts);
-// Reads one frame; `alloc(i, size)` returns where part i goes (nullptr = a
-// temporary vector owned by `scratch`).
+// Reads one multipart message; `alloc(i, size)` returns where part i goes
+// (nullptr = a temporary vector owned by `scratch`).  Command frames between
+// messages (PING, PONG, ...) are skipped; an ERROR command ends the
+// connection.  False on EOF / error / more than kMaxParts parts.
 struct RecvPart {
   void *data;
   size_t size;
 };
+constexpr size_t kMaxParts = 64;
 bool recv_frame(int fd, std::vector<RecvPart> &parts,
                 std::vector<std::vector<char>> &scratch,
                 void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx);

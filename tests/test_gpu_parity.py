@@ -282,6 +282,28 @@ def test_gpu_add_and_zero(dev):
     assert int(torch.count_nonzero(ty)) == 0
 
 
+def test_hbm_read_probe_streams_the_buffer(dev):
+    """gp_hbm_probe(READ) reads every byte and writes none of them: 1 GiB takes
+    at least 1 GiB / 10 TB/s (an empty kernel body -- a dead sink lets the
+    compiler drop every load -- finished in microseconds), and the probed
+    buffer is unchanged (its sink is a device global of its own)."""
+    from geeps_amd import native
+    lib = native.lib()
+    n = 1 << 28
+    buf = torch.rand(n, dtype=torch.float32, device=dev)
+    ref = buf.clone()
+    s = torch.cuda.current_stream()
+    native.check(lib.gp_hbm_probe(0, buf.data_ptr(), n, s.cuda_stream), "gp_hbm_probe")
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    native.check(lib.gp_hbm_probe(0, buf.data_ptr(), n, s.cuda_stream), "gp_hbm_probe")
+    b.record(s)
+    b.synchronize()
+    ms = a.elapsed_time(b)
+    assert ms >= n * 4 / 10e12 * 1e3, f"read probe took {ms} ms for 1 GiB: loads were dropped"
+    assert torch.equal(buf, ref)
+
+
 def test_empty_calls_are_noops(dev):
     from geeps_amd import rowops
     y = torch.ones(256, dtype=torch.float32, device=dev)
