@@ -694,9 +694,9 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
     app links) run as P processes on this GPU, one GeePS worker + tablet server
     each, same-node IPC transport.  The table is the bench's rows x W fp32 as
     RowData rows (rows * W / 128 of them).  One clock = Read (gather from the
-    segmented param cache) -> PreUpdate -> device fill -> PostRead -> Update
-    (fused init through the row plan) -> Clock (push, the server's bucket sum,
-    the zero-copy refresh), through the public API.  P = 2 is configs[1]'s
+    segmented param cache) -> PreUpdate (the clock's oplog slice: direct
+    oplog) -> device fill -> PostRead -> Update (no rows move) -> Clock (push,
+    the server's bucket sum, the zero-copy refresh), through the public API.  P = 2 is configs[1]'s
     2 loopback clients; every worker updates every row each clock.
     delta_GBps = P * table bytes / the slowest worker's ms per clock."""
     import importlib.util

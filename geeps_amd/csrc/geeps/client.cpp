@@ -52,7 +52,7 @@ std::string ClientStats::to_json() const {
   o << "{\"nr_read\": " << nr_read << ", \"nr_update\": " << nr_update
     << ", \"nr_clock\": " << nr_clock << ", \"nr_push\": " << nr_push
     << ", \"nr_refresh\": " << nr_refresh << ", \"nr_refresh_in_place\": " << nr_refresh_in_place
-    << ", \"nr_refresh_staged\": " << nr_refresh_staged
+    << ", \"nr_refresh_staged\": " << nr_refresh_staged << ", \"nr_update_direct\": " << nr_update_direct
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -95,6 +95,8 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
   };
   stage_updates_mode_ = mode("GEEPS_STAGE_PEER_UPDATES");
   stage_refresh_mode_ = mode("GEEPS_STAGE_PEER_REFRESH");
+  const char *direct = std::getenv("GEEPS_DIRECT_OPLOG");
+  direct_oplog_ = !(direct && std::string(direct) == "0");
   const char *delay = std::getenv("GEEPS_TEST_READER_DELAY_US");
   reader_delay_us_ = delay ? std::atoi(delay) : 0;
   // Same-node peers exchange rows device to device through IPC-mapped HBM
@@ -672,6 +674,20 @@ void ClientLib::decide_fused_init() {
       ch.init_ok[t] = ok && covered == pc.num_rows;
     }
   }
+  // Direct oplog: an update op whose rows are one channel's cache rows in
+  // order, in a (channel, table) whose clock writes every oplog row once.
+  // The app's buffer then IS the oplog slice: the fused init's copy
+  // (0.0f + x) disappears.  The slice holds x instead of 0.0f + x, which
+  // differs only for -0.0 (and a signalling NaN's quiet bit); the server's
+  // master starts at +0.0 and a sum is -0.0 only when both addends are, so
+  // every master row, partial sum and refresh is bit-identical.
+  for (size_t i = 0; i < end; ++i) {
+    OpInfo &w = opseq_[i];
+    if (w.type != OpInfo::WRITE || w.local) continue;
+    OpInfo &pre = opseq_[w.prestep_handle];
+    pre.direct = direct_oplog_ && pre.direct_channel >= 0 && !pre.rows.empty() &&
+                 channels_[pre.direct_channel]->init_ok[pre.table_id];
+  }
 }
 
 // One DoubleIndex per op, grouped by channel, each channel's id1 range equal
@@ -718,6 +734,19 @@ void ClientLib::create_double_index(OpInfo &op) {
   // runs (first-access order makes an op's rows one run per channel) are
   // copied by the phase-separated kernels, which hold their rate on every
   // allocation.
+  if (op.type == OpInfo::PRE_WRITE) {
+    op.direct_channel = -1;
+    for (uint32_t c = 0; c < num_channels_; ++c) {
+      if (per[c].size() != op.rows.size() || op.rows.empty()) continue;
+      bool run = true;
+      for (size_t j = 0; j < per[c].size() && run; ++j)
+        run = per[c][j].id0 == j && per[c][j].id1 == per[c][0].id1 + j;
+      if (run) {
+        op.direct_channel = (int)c;
+        op.direct_lo = per[c][0].id1;
+      }
+    }
+  }
   if (op.type == OpInfo::PRE_WRITE || op.type == OpInfo::READ) {
     op.plans.resize(num_channels_);
     for (uint32_t c = 0; c < num_channels_; ++c)
@@ -817,6 +846,18 @@ void ClientLib::preupdate_batch(RowOpVal **buffer, int handle) {
   GP_CHECK(!op.local);
   GP_CHECK_MSG(!op.in_use, "PreUpdate of handle " << handle << " before its Update");
   op.in_use = true;
+  op.direct_now = started_ && op.direct;
+  if (op.direct_now) {
+    // the clock's oplog slice of this op's rows (not zeroed: every row of it
+    // is written by exactly one update op of the clock)
+    Channel &ch = *channels_[op.direct_channel];
+    std::lock_guard<std::mutex> lk(ch.mu);
+    ParamCache &pc = ch.tables[op.table_id];
+    auto oplog = get_oplog(pc, iteration_, ch.stream->get(), /*zero=*/false);
+    ch.stream->sync();  // a fresh pool buffer's zero fill lands before the app writes
+    *buffer = reinterpret_cast<RowOpVal *>(oplog->data() + op.direct_lo * ROW_DATA_SIZE);
+    return;
+  }
   *buffer = reinterpret_cast<RowOpVal *>(op.buffer.data());
 }
 
@@ -836,6 +877,9 @@ std::shared_ptr<DeviceArray<float>> ClientLib::get_oplog(ParamCache &pc, iter_t 
   if (!buf) {
     pc.oplog_pool.push_back(std::make_shared<DeviceArray<float>>(pc.num_rows * ROW_DATA_SIZE));
     buf = pc.oplog_pool.back();
+    // a new buffer never shows uninitialised HBM: a direct-oplog PreUpdate
+    // hands it to the app, and rows an app leaves unwritten then push zeros
+    zero = true;
   }
   if (zero) GP_CALL(gp_zero(buf->data(), pc.num_rows * ROW_DATA_SIZE, s));
   pc.oplog[clock] = buf;
@@ -858,36 +902,49 @@ void ClientLib::update_batch(int handle) {
     ParamCache &pc = ch.tables[pre.table_id];
     if (pc.num_rows == 0) continue;
     const bool fused = started_ && ch.init_ok[pre.table_id];
+    // the app wrote its rows with its own device work, typically on the null
+    // stream (the reference's worker ran on a blocking stream, which waited
+    // for it implicitly): everything this Update queues, and the push and the
+    // server's sum after it, comes after those writes
+    if (n) {
+      ch.app_written.record_default();
+      GP_CALL(gp_stream_wait_event(ch.stream->get(), ch.app_written.get()));
+    }
     auto oplog = get_oplog(pc, clock, ch.stream->get(), /*zero=*/!fused);
+    // the rows the app wrote: its op buffer, or (direct) the oplog slice itself
+    const bool in_place = pre.direct_now && (int)ch.id == pre.direct_channel;
+    const float *x = in_place ? oplog->data() + pre.direct_lo * ROW_DATA_SIZE : pre.buffer.data();
     if (n) {
       // add_rows_from_double_index_gpu (clientlib-data.cpp:385-394) through the
       // op's row plan for this channel (its index, offset 0, num_vals_limit)
       const gp_row_plan plan = pre.plans[ch.id]->get();
-      if (fused)
-        GP_CALL(gp_scatter_init_rows_planned(oplog->data(), pre.buffer.data(), plan,
-                                             ch.stream->get()));
+      if (in_place)
+        ;  // the app wrote these rows into the oplog itself
+      else if (fused)
+        GP_CALL(gp_scatter_init_rows_planned(oplog->data(), x, plan, ch.stream->get()));
       else
-        GP_CALL(gp_scatter_add_rows_planned(oplog->data(), pre.buffer.data(), plan,
-                                            ch.stream->get()));
+        GP_CALL(gp_scatter_add_rows_planned(oplog->data(), x, plan, ch.stream->get()));
       if (config_.read_my_writes && pc.segmented) {
         // (unreachable today: read-my-writes refreshes are private copies, so
         // its cache is never segmented; the unplanned add has no repeat layers)
         GP_CHECK_MSG(!pre.repeats, "read-my-writes update of an op listing a row twice into a "
                                    "segmented cache");
-        GP_CALL(gp_scatter_add_rows_segmented(&pc.segs, pre.buffer.data(),
+        GP_CALL(gp_scatter_add_rows_segmented(&pc.segs, x,
                                               pre.index.data() + pre.ch_start[ch.id], n,
                                               gp_double_index{0, 0}, ROW_DATA_SIZE,
                                               pre.num_vals_limit, ch.stream->get()));
       } else if (config_.read_my_writes)
-        GP_CALL(gp_scatter_add_rows_planned(pc.data.data(), pre.buffer.data(), plan,
-                                            ch.stream->get()));
+        GP_CALL(gp_scatter_add_rows_planned(pc.data.data(), x, plan, ch.stream->get()));
     }
     ch.stream->sync();
   }
   pre.in_use = false;
+  const bool was_direct = pre.direct_now;
+  pre.direct_now = false;
   {
     std::lock_guard<std::mutex> lk(stats_mu_);
     stats_.nr_update++;
+    if (was_direct) stats_.nr_update_direct++;
     stats_.rows_updated += pre.rows.size();
     stats_.update_time += now_s() - t0;
   }

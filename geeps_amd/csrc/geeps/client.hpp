@@ -68,6 +68,15 @@ struct OpInfo {
   // PRE_WRITE: per channel, the channel's slice of `index` as a row plan
   // (destination-sorted), which the oplog scatter-add / fused init run through
   std::vector<std::unique_ptr<RowPlan>> plans;
+  // PRE_WRITE whose rows are one channel's cache rows [direct_lo, +rows) in
+  // order (op row j -> cache row direct_lo + j, no repeats): after
+  // StartIterations, when the clock's update ops write every oplog row once,
+  // PreUpdate hands out that oplog slice itself and Update moves no rows
+  // (decide_fused_init; DESIGN §4 "direct oplog").
+  int direct_channel = -1;
+  size_t direct_lo = 0;
+  bool direct = false;                 // decided: this op writes its oplog slice in place
+  bool direct_now = false;             // the outstanding PreUpdate handed out the slice
   DeviceArray<float> buffer;           // READ / PRE_WRITE op buffer
   float *local_ptr = nullptr;          // local READ: GPU-resident storage
   bool in_use = false;
@@ -106,6 +115,7 @@ struct ClientStats {
   uint64_t nr_read = 0, nr_update = 0, nr_clock = 0, nr_push = 0, nr_refresh = 0;
   uint64_t nr_refresh_in_place = 0;  // refreshes read in place from the server's master version
   uint64_t nr_refresh_staged = 0;    // same-node refreshes peer-copied into the cache (staged)
+  uint64_t nr_update_direct = 0;     // Updates whose rows the app wrote into the oplog in place
   uint64_t rows_updated = 0, rows_read = 0, bytes_pushed_remote = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
@@ -140,6 +150,9 @@ struct Channel {
   // several processes sharing one GPU beyond the hardware's queue slots are
   // time-sliced, which cost an 8-process clock 10x.
   std::unique_ptr<Stream> stream, svc_stream;
+  // Update orders `stream` after the app's null-stream writes to its update
+  // rows (what the reference's blocking worker stream did implicitly)
+  Event app_written;
   std::unique_ptr<ChannelSink> sink;
   std::unique_ptr<TabletServer> server;
   // client side: one socket per remote server (-1 = in-process server); the
@@ -247,6 +260,7 @@ class ClientLib {
   // the peer's HBM in place over xGMI), 1 = always (tests the cross-GPU path
   // on one GPU): GEEPS_STAGE_PEER_UPDATES (buckets), GEEPS_STAGE_PEER_REFRESH
   int stage_updates_mode_ = -1;
+  bool direct_oplog_ = true;  // GEEPS_DIRECT_OPLOG=0 turns the direct oplog off
   int stage_refresh_mode_ = -1;
   int reader_delay_us_ = 0;   // GEEPS_TEST_READER_DELAY_US (test hook)
   std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)

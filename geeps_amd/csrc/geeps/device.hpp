@@ -37,6 +37,8 @@ class Event {
   Event(const Event &) = delete;
   Event &operator=(const Event &) = delete;
   void record(const Stream &s) { GP_CALL(gp_event_record(e_, s.get())); }
+  // the legacy default (null) stream: where an app's own device work goes
+  void record_default() { GP_CALL(gp_event_record(e_, nullptr)); }
   void sync() { GP_CALL(gp_event_synchronize(e_)); }
   gp_event get() const { return e_; }
 

@@ -55,6 +55,9 @@ static float delta(int p, int c, size_t e, bool fl) {
     x ^= x >> 13;
     x *= 0x5bd1e995u;
     x ^= x >> 15;
+    // 1 in 64 is -0.0f: the reference's oplog turns it into +0.0f (zerofy,
+    // then +=); libgeeps' direct oplog keeps it, which must not change a bit
+    if ((x >> 24) % 64 == 0) return -0.0f;
     return (float)(x & 0xffffff) / 16777216.0f - 0.5f;
   }
   return (float)(1 + ((p * 7 + c * 3 + e) % 5));  // 1..5

@@ -379,6 +379,27 @@ def test_peer_refresh_staged_into_local_cache(dev, P, slack, channels, updates):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P,mode,direct", [(1, "float", "1"), (1, "float", "0"), (2, "int", "1"),
+                                           (3, "int", "0")])
+def test_direct_oplog(dev, P, mode, direct):
+    """Direct oplog: an update op whose rows are one channel's
+    cache rows in order gets the clock's oplog slice itself from PreUpdate, so
+    Update moves no rows.  Default on; GEEPS_DIRECT_OPLOG=0 restores the fused
+    init's copy.  The float case's deltas include -0.0f (kept as -0.0 in the
+    direct oplog, +0.0 after the reference's zerofy + add): every Read is still
+    bit-exact against the sequential fp32 sum.  Every update after
+    StartIterations went direct, or none did."""
+    outs = _run_app(P, rows=700, clocks=8, slack=0, channels=1, rmw=0, mode=mode, transport="ipc",
+                    extra_env={"GEEPS_DIRECT_OPLOG": direct})
+    for s in _stats(outs):
+        c = s["client"]
+        if direct == "1":
+            assert c["nr_update_direct"] == c["nr_update"] - 1  # all but the setup clock's
+        else:
+            assert c["nr_update_direct"] == 0
+
+
+@pytest.mark.gpu
 def test_one_process_per_gpu(dev):
     """One process per GPU (process p on device p % count), as on an 8-GPU
     node: peers' buckets cross xGMI by the staged peer copy and refreshes are
