@@ -54,7 +54,8 @@ bool zmtp_handshake(int fd, const std::string &identity,
 bool send_frame(int fd, const std::vector<Part> &parts);
 // Reads one multipart message; `alloc(i, size)` returns where part i goes
 // (nullptr = a temporary vector owned by `scratch`).  Command frames between
-// messages (PING, PONG, ...) are skipped; an ERROR command ends the
+// messages (PING, PONG, ...) are skipped, and a PING is not answered (the
+// reference never turns on ZeroMQ heartbeats); an ERROR command ends the
 // connection.  False on EOF / error / more than kMaxParts parts.
 struct RecvPart {
   void *data;

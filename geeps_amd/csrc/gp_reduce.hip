@@ -2331,8 +2331,18 @@ int gp_device_pci_bus_id(int device, char *buf, int len) {
 
 static_assert(sizeof(hipIpcMemHandle_t) <= GP_IPC_HANDLE_BYTES, "IPC handle size");
 
+// One process's IPC calls run one at a time.  libgeeps exports and maps from
+// several threads (a server thread exporting master versions, reader threads
+// mapping a peer's versions and oplogs).  One GPU run saw hipIpcOpenMemHandle
+// reject a handle once ("IPC Attach: Invalid IPC handle",
+// profiles/r03/e2e/pytest_libgeeps_race.log, test_shuffled_update_rows) and not
+// in any rerun; a concurrent call is not proven to be the cause, so this lock
+// is a precaution (the calls run once per buffer).
+static std::mutex g_ipc_mu;
+
 int gp_ipc_get_handle(void *handle_out, void *device_base) {
   if (!handle_out || !device_base) return set_error(GP_ERR_INVALID, "null pointer");
+  std::lock_guard<std::mutex> lk(g_ipc_mu);
   hipIpcMemHandle_t h;
   GP_HIP_TRY(hipIpcGetMemHandle(&h, device_base));
   std::memset(handle_out, 0, GP_IPC_HANDLE_BYTES);
@@ -2344,11 +2354,13 @@ int gp_ipc_open_handle(void **device_ptr, const void *handle) {
   if (!device_ptr || !handle) return set_error(GP_ERR_INVALID, "null pointer");
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle, sizeof h);
+  std::lock_guard<std::mutex> lk(g_ipc_mu);
   GP_HIP_TRY(hipIpcOpenMemHandle(device_ptr, h, hipIpcMemLazyEnablePeerAccess));
   return GP_OK;
 }
 
 int gp_ipc_close_handle(void *device_ptr) {
+  std::lock_guard<std::mutex> lk(g_ipc_mu);
   if (device_ptr) GP_HIP_TRY(hipIpcCloseMemHandle(device_ptr));
   return GP_OK;
 }
