@@ -171,7 +171,10 @@ void ClientLib::start_network() {
       // ZMTP READY as the reference's client ROUTER ("client-<i>",
       // clientlib.cpp:107); the server must answer as "tablet-<s>"
       PeerInfo peer;
-      GP_CHECK_MSG(zmtp_handshake(fd, "client-" + std::to_string(process_id_), hello_props(s), &peer, &err),
+      // (the server's accept thread may still be taking an earlier channel's
+      // connections from slower processes: as long as a connect may take)
+      GP_CHECK_MSG(zmtp_handshake(fd, "client-" + std::to_string(process_id_), hello_props(s), &peer, &err,
+                                  connect_timeout_s()),
                    err << " (server " << s << ", channel " << ch.id << ")");
       GP_CHECK_MSG(peer.identity == "tablet-" + std::to_string(s),
                    "port " << port_of(s, ch.id) << " answered as '" << peer.identity << "', expected tablet-" << s);
@@ -190,7 +193,8 @@ void ClientLib::server_accept_loop(Channel &ch, int expected) {
     // server-entry.cpp:66); the peer names itself "client-<i>"
     PeerInfo peer;
     std::string err;
-    GP_CHECK_MSG(zmtp_handshake(fd, "tablet-" + std::to_string(process_id_), {}, &peer, &err),
+    GP_CHECK_MSG(zmtp_handshake(fd, "tablet-" + std::to_string(process_id_), {}, &peer, &err,
+                                connect_timeout_s()),
                  err << " (channel " << ch.id << ")");
     uint32_t cid = ~0u;
     {

@@ -6,6 +6,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -162,10 +163,29 @@ const std::string *PeerInfo::prop(const std::string &name) const {
 
 bool zmtp_handshake(int fd, const std::string &identity,
                     const std::vector<std::pair<std::string, std::string>> &extra, PeerInfo *peer,
-                    std::string *err) {
+                    std::string *err, double timeout_s) {
+  // a peer that connects and then says nothing fails the handshake after
+  // timeout_s instead of blocking this thread for ever (libzmq's
+  // ZMQ_HANDSHAKE_IVL plays this part); the socket is blocking again after
+  struct RecvTimeout {
+    int fd;
+    RecvTimeout(int f, double s) : fd(f) {
+      timeval tv{(time_t)s, (suseconds_t)((s - (double)(time_t)s) * 1e6)};
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    }
+    ~RecvTimeout() {
+      timeval tv{0, 0};
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    }
+  } guard(fd, timeout_s);
   auto fail = [&](const std::string &why) {
     if (err) *err = "ZMTP handshake: " + why;
     return false;
+  };
+  auto read_failed = [&](const std::string &what) {
+    return fail(errno == EAGAIN || errno == EWOULDBLOCK
+                    ? "no " + what + " from the peer within " + std::to_string((int)timeout_s) + " s"
+                    : "peer closed during the " + what);
   };
   // greeting: signature, version 3.0, mechanism NULL, as-server 0, filler
   uint8_t g[kGreetingBytes] = {};
@@ -176,7 +196,8 @@ bool zmtp_handshake(int fd, const std::string &identity,
   std::memcpy(g + 12, "NULL", 4);
   if (!write_all(fd, g, sizeof g)) return fail("greeting not sent");
   uint8_t pg[kGreetingBytes];
-  if (!read_all(fd, pg, sizeof pg)) return fail("peer closed during the greeting");
+  errno = 0;
+  if (!read_all(fd, pg, sizeof pg)) return read_failed("greeting");
   if (pg[0] != 0xFF || !(pg[9] & 0x01)) return fail("peer is not a ZMTP 2+ endpoint");
   if (pg[10] < 3) return fail("peer speaks ZMTP " + std::to_string(pg[10]) + ".x, need 3.x");
   static const uint8_t null_mech[20] = {'N', 'U', 'L', 'L'};
@@ -193,7 +214,8 @@ bool zmtp_handshake(int fd, const std::string &identity,
   iovec iov[2] = {{h, frame_header(h, kFlagCommand, body.size())}, {&body[0], body.size()}};
   if (!writev_all(fd, iov, 2)) return fail("READY not sent");
   std::vector<char> rb;
-  if (!read_command(fd, &rb)) return fail("no READY command from the peer");
+  errno = 0;
+  if (!read_command(fd, &rb)) return errno ? read_failed("READY command") : fail("malformed READY command");
   std::string name;
   size_t at = 0;
   if (!split_command(rb, &name, &at)) return fail("malformed command");

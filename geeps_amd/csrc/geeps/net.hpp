@@ -45,10 +45,12 @@ struct PeerInfo {
 // ZMTP/3.0 NULL handshake on a connected socket: greeting both ways, then our
 // READY (Socket-Type ROUTER, Identity `identity`, then `extra`) and the peer's.
 // False with `*err` set on EOF, a non-ZMTP-3 peer, another mechanism, an ERROR
-// command or a socket type a ROUTER cannot talk to.
+// command, a socket type a ROUTER cannot talk to, or a peer silent for
+// `timeout_s` (a ZMTP/1.0 peer, libzmq 2.x, is refused as "not a ZMTP 2+
+// endpoint").
 bool zmtp_handshake(int fd, const std::string &identity,
                     const std::vector<std::pair<std::string, std::string>> &extra, PeerInfo *peer,
-                    std::string *err);
+                    std::string *err, double timeout_s = 60.0);
 
 // One multipart message (every part but the last flagged MORE).  Blocking.
 bool send_frame(int fd, const std::vector<Part> &parts);

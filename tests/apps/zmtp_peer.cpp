@@ -33,6 +33,12 @@ int fail(const std::string &why) {
   return 1;
 }
 
+// ZMTP_PEER_HANDSHAKE_S: the handshake's time limit (default 60 s)
+double handshake_s() {
+  const char *e = std::getenv("ZMTP_PEER_HANDSHAKE_S");
+  return e ? std::atof(e) : 60.0;
+}
+
 float update_value(size_t i, size_t j) { return (float)(i * ROW_DATA_SIZE + j) + 0.25f; }
 
 int run_client(uint16_t port, uint32_t client_id, uint32_t server_id, size_t rows) {
@@ -41,7 +47,8 @@ int run_client(uint16_t port, uint32_t client_id, uint32_t server_id, size_t row
   if (fd < 0) return fail(err);
   PeerInfo peer;
   if (!zmtp_handshake(fd, "client-" + std::to_string(client_id),
-                      {{"X-Geeps-Ipc", "0"}, {"X-Geeps-Pci-Bus-Id", "0000:00:00.0"}}, &peer, &err))
+                      {{"X-Geeps-Ipc", "0"}, {"X-Geeps-Pci-Bus-Id", "0000:00:00.0"}}, &peer, &err,
+                      handshake_s()))
     return fail(err);
   std::printf("peer socket_type=%s identity=%s\n", peer.socket_type.c_str(), peer.identity.c_str());
   if (peer.identity != "tablet-" + std::to_string(server_id)) return fail("unexpected server identity");
@@ -95,7 +102,7 @@ int run_server(uint16_t port, uint32_t server_id) {
   const int fd = accept_tcp(lfd);
   if (fd < 0) return fail("accept failed");
   PeerInfo peer;
-  if (!zmtp_handshake(fd, "tablet-" + std::to_string(server_id), {}, &peer, &err)) return fail(err);
+  if (!zmtp_handshake(fd, "tablet-" + std::to_string(server_id), {}, &peer, &err, handshake_s())) return fail(err);
   std::printf("peer socket_type=%s identity=%s\n", peer.socket_type.c_str(), peer.identity.c_str());
   for (const auto &p : peer.props) std::printf("prop %s=%s\n", p.first.c_str(), p.second.c_str());
   std::vector<RecvPart> parts;

@@ -257,3 +257,28 @@ def test_curve_mechanism_is_refused():
         if p.poll() is None:
             p.kill()
             p.wait()
+
+
+def test_silent_peer_times_out_the_handshake():
+    """A peer that accepts and then says nothing fails the handshake after the
+    time limit (libgeeps uses its connect timeout) instead of hanging."""
+    port = free_port()
+    ls = socket.socket()
+    ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    ls.bind(("127.0.0.1", port))
+    ls.listen(1)
+    env = dict(os.environ, ZMTP_PEER_HANDSHAKE_S="1")
+    t0 = time.time()
+    p = subprocess.Popen([PEER, "client", str(port), "1", "0", "1"], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True, env=env)
+    try:
+        c, _ = ls.accept()
+        _, err = p.communicate(timeout=30)
+        assert p.returncode != 0 and "no greeting from the peer within 1 s" in err
+        assert time.time() - t0 < 20
+        c.close()
+    finally:
+        ls.close()
+        if p.poll() is None:
+            p.kill()
+            p.wait()
