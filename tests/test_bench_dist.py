@@ -17,7 +17,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,exchange", [(2, "a2a"), (4, "a2a"), (2, "rs")])
+@pytest.mark.parametrize("world,exchange", [(2, "a2a"), (4, "a2a"), (2, "rs"), (8, "a2a")])
 def test_bench_multirank_flow(tmp_path, world, exchange):
     argv = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--rows", "1000", "--width", "64",
             "--clients", "8", "--exchange", exchange, "--exchange-steps", "2"]

@@ -37,6 +37,8 @@ def _expected(num_rows, W, num_clients, steps):
     (2, 64, 16, 4, "a2a", 2),
     (2, 37, 12, 2, "a2a", 3),     # uneven rows: 19 + 18
     (4, 41, 8, 8, "a2a", 2),
+    (8, 83, 8, 8, "a2a", 2),      # configs[2]'s shape: 8 shards, 8 clients, one per rank
+    (8, 83, 8, 8, "rs", 1),
     (2, 64, 16, 4, "rs", 2),
     (2, 37, 12, 2, "rs", 1),
 ])
