@@ -715,6 +715,11 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
         out[f"p{P}"] = {"workers": P, "ms_per_clock": r["ms_per_clock_max"],
                         "delta_GBps": r["aggregate_delta_GBps"],
                         "ms_per_clock_each": r["ms_per_clock"]}
+    # the same clock with the direct oplog off: Update copies the app's rows
+    # into the oplog (the fused init), as before round 3
+    r = mod.run(1, rd_rows, clocks, warmup, 0, "ipc", timeout=120, extra_env={"GEEPS_DIRECT_OPLOG": "0"})
+    out["p1_copy"] = {"workers": 1, "ms_per_clock": r["ms_per_clock_max"],
+                      "delta_GBps": r["aggregate_delta_GBps"], "direct_oplog": False}
     return out
 
 

@@ -54,9 +54,10 @@ def free_base(P):
     return free_port_base(P, 1)
 
 
-def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900):
+def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900, extra_env=None):
     """Run the P processes; return the aggregate dict (raises on a failure)."""
     env = dict(os.environ)
+    env.update(extra_env or {})
     # P processes share the box's ONE GPU.  At the default 4 hardware queues
     # per process, 8 processes oversubscribe the GPU's queue slots and are
     # time-sliced: the AlexNet-table clock took 24 ms instead of 2.4 ms.  One
