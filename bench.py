@@ -979,6 +979,8 @@ def main(argv=None, backend="nccl", apply_fn=None):
                          "algorithmic_bytes_per_step": algo_bytes,
                          "algorithmic_bytes_per_launch": int(algo_bytes * share / launches)},
             "hbm_GBps_algorithmic": round((C + 2) * R * W * 4 / step_s / 1e9, 1),
+            # gradient rows reduced per second (C client rows per table row)
+            "rows_per_s": round(C * R / step_s, 1),
             "cpu_baseline": cpu,
         }
         if pmc and committed:
