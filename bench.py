@@ -424,6 +424,17 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
     x = torch.rand(R * 128, generator=g, device=dev)
     y = torch.zeros(R * 128, device=dev)
     out = {}
+    if "random" in indexes and not only:
+        # one throwaway index through the plan cache's first and second calls:
+        # the process's first radix sort loads hipCUB's kernels and grows the
+        # stream-ordered pool (one-time costs, ~5 ms), which would otherwise
+        # land in the first leg's `second_call_ms`
+        warm = torch.stack([torch.arange(R, device=dev), torch.randperm(R, generator=g, device=dev)], 1)
+        for _ in range(2):
+            rowops.add_rows_from_double_index_gpu(y, x, warm, R, (0, 0), 128, R * 128, validate=False)
+        torch.cuda.synchronize()
+        native.check(native.lib().gp_unplanned_cache_clear(), "gp_unplanned_cache_clear")
+        del warm
     for kind in indexes:
         if kind == "random":
             dst = torch.randperm(R, generator=g, device=dev)
@@ -448,9 +459,10 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             # the unplanned calls plan themselves on the device (gp_reduce.h,
             # ABI 10): an index scan, then the sweep forms for dense runs and
             # the row kernels for the rest; a scatter's unsorted rest runs in op
-            # order on the first call with an index (`first_call_ms`) and from
-            # the plan cache's destination-sorted copy after that (`avg_ms`,
-            # the reference reusing each op's DoubleIndex every clock).  The
+            # order on the first call with an index (`first_call_ms`), the
+            # second call sorts it by destination and runs that
+            # (`second_call_ms`), later calls run the plan cache's sorted copy
+            # (`avg_ms`, the reference reusing each op's DoubleIndex every clock).  The
             # time includes the scan and the call's one stream sync, as the
             # reference's call syncs too.
             scan = "index_scan_kernel + "
@@ -498,10 +510,11 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                         launches, other, share = sp["launches"], sp["other_launches"], sp["share"]
                 else:
                     kernel = "row_wave_kernel"
-            first_ms = None
-            if not planned:  # the first call with this index (a plan-cache miss) on its own
+            first_ms = second_ms = None
+            if not planned:  # the first and second calls with this index on their own
                 native.check(native.lib().gp_unplanned_cache_clear(), "gp_unplanned_cache_clear")
                 first_ms = _time_calls(fn, 1, stream, warmup=False)
+                second_ms = _time_calls(fn, 1, stream, warmup=False)
             avg = _time_calls(fn, reps, stream)
             gbps = nbytes / (avg / 1e3) / 1e9
             leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),
@@ -510,6 +523,7 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             if first_ms is not None:
                 leg["first_call_ms"] = round(first_ms, 4)
                 leg["first_call_frac"] = round(nbytes / (first_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+                leg["second_call_ms"] = round(second_ms, 4)
             if other:  # the rest in other kernel forms; avg_launch_ms is the dominant one's share
                 leg["other_launches"] = other
                 leg["dominant_share"] = round(share, 6)

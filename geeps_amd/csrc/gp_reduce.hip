@@ -1384,12 +1384,13 @@ int launch_gather_planned(float *y, const float *x, const gp_row_segments *xs,
 //     destination-sorted residual runs ~76 %).  Sorting it costs more than it
 //     saves in one call (a radix sort of 8 M pairs ~0.3 ms; coarse binning
 //     does not recover the locality: DESIGN.md §5), but the reference reuses
-//     each op's DoubleIndex every clock.  So such a residual runs in op order
-//     once, and its destination-sorted copy is built for the calls that follow
-//     (a hipCUB radix sort, gp_sort.hip).  Later calls with the same index --
-//     same pointer, size, offsets, row size and limit, and entry for entry the
-//     same content, which the scan checks against the cached copy -- run the
-//     sorted copy.  Visiting rows in destination order is bit-neutral under
+//     each op's DoubleIndex every clock.  So the first call with an index runs
+//     such a residual in op order and keeps a copy of the index; the second
+//     call with the same index -- same pointer, size, offsets, row size and
+//     limit, and entry for entry the same content, which the scan checks
+//     against the copy -- builds the destination-sorted residual (a hipCUB
+//     radix sort, gp_sort.hip) and runs it, and later calls run it at once.
+//     An index that changes every call costs one copy per call, no sort.  Visiting rows in destination order is bit-neutral under
 //     the call's precondition (distinct destinations).
 // Calls below g_analyze_min_bytes (gp_set_unplanned_min_bytes) skip all this.
 // ---------------------------------------------------------------------------
@@ -1625,22 +1626,48 @@ struct PlanKey {
   }
 };
 
+// Device memory freed with hipFree (which waits for the device, so kernels
+// already queued on it finish first) on the device it came from.
+struct DevBuf {
+  void *p = nullptr;
+  int device = 0;
+  DevBuf(size_t bytes, int dev, int *rc) : device(dev) {
+    *rc = hipMalloc(&p, bytes) == hipSuccess ? GP_OK : set_error(GP_ERR_HIP, "plan cache hipMalloc");
+  }
+  ~DevBuf() {
+    if (!p) return;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    (void)hipFree(p);
+    if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
+  }
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+};
+
+// An entry is immutable once in the cache.  The first call with an index
+// leaves a copy-only entry (`sorted` null); the next call with the same
+// content builds the destination-sorted residual into a new entry that
+// shares the copy.
 struct CachedPlan {
   PlanKey key{};
-  gp_double_index *copy = nullptr;    // the index as first seen
-  gp_double_index *sorted = nullptr;  // its residual, offsets applied, ascending destination
+  std::shared_ptr<DevBuf> copy;    // the index as first seen
+  std::shared_ptr<DevBuf> sorted;  // its residual, offsets applied, ascending destination
   size_t resid = 0;
-  hipEvent_t ready = nullptr;  // recorded once both are built, on the building stream
+  hipEvent_t ready = nullptr;  // recorded once copy (and sorted) are built, on the building stream
   uint64_t last_use = 0;
   size_t bytes = 0;
+  const gp_double_index *copy_ptr() const { return static_cast<const gp_double_index *>(copy->p); }
+  const gp_double_index *sorted_ptr() const {
+    return sorted ? static_cast<const gp_double_index *>(sorted->p) : nullptr;
+  }
   ~CachedPlan() {
-    // hipFree waits for the device, so kernels already queued on it finish first
+    if (!ready) return;
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != key.device) (void)hipSetDevice(key.device);
-    if (copy) (void)hipFree(copy);
-    if (sorted) (void)hipFree(sorted);
-    if (ready) (void)hipEventDestroy(ready);
+    (void)hipEventDestroy(ready);
     if (cur >= 0 && cur != key.device) (void)hipSetDevice(cur);
   }
 };
@@ -1695,20 +1722,41 @@ struct DevRun {
   uint64_t e0, rows, from, to;  // first entry, rows, endpoints of the first entry
 };
 
-// The destination-sorted copy of a residual, built on stream s after the
-// call's own launches (defined in gp_sort.hip's radix sort).
+// A copy-only entry for an index seen for the first time (its copy, taken on
+// stream s after the call's own launches): what the next call's scan compares.
+int cache_first_sighting(const PlanKey &key, const gp_double_index *idx, size_t resid, hipStream_t s) {
+  auto p = std::make_shared<CachedPlan>();
+  p->key = key;
+  p->resid = resid;
+  p->bytes = key.n * sizeof(gp_double_index);
+  int rc = GP_OK;
+  p->copy = std::make_shared<DevBuf>(key.n * sizeof(gp_double_index), key.device, &rc);
+  if (rc != GP_OK) return rc;
+  GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+  GP_HIP_TRY(hipMemcpyAsync(p->copy->p, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
+  GP_HIP_TRY(hipEventRecord(p->ready, s));
+  cache_insert(std::move(p));
+  return GP_OK;
+}
+
+// The second call with the same index: its residual's destination-sorted copy
+// (a hipCUB radix sort, gp_sort.hip), built on stream s into a new entry that
+// shares `seen`'s copy; returned for this call to run.
 template <int OP>
-int build_cached_plan(const PlanKey &key, const gp_double_index *idx, const EntryRanges &rr, uint64_t max_dst,
-                      hipStream_t s) {
+int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_double_index *idx,
+                          const EntryRanges &rr, uint64_t max_dst, hipStream_t s,
+                          std::shared_ptr<CachedPlan> *built) {
+  const PlanKey &key = seen->key;
   const size_t resid = rr.pre[rr.count];
   auto p = std::make_shared<CachedPlan>();
   p->key = key;
   p->resid = resid;
   p->bytes = (key.n + resid) * sizeof(gp_double_index);
-  GP_HIP_TRY(hipMalloc(&p->copy, key.n * sizeof(gp_double_index)));
-  GP_HIP_TRY(hipMalloc(&p->sorted, resid * sizeof(gp_double_index)));
+  p->copy = seen->copy;
+  int rc = GP_OK;
+  p->sorted = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
+  if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
-  GP_HIP_TRY(hipMemcpyAsync(p->copy, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
   uint32_t *kv = nullptr;  // keys, values, sorted keys, sorted values
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&kv), 4 * resid * sizeof(uint32_t), s));
   const size_t grid = std::min((resid + kBlock - 1) / kBlock, (size_t)num_cus() * 8);
@@ -1716,15 +1764,16 @@ int build_cached_plan(const PlanKey &key, const gp_double_index *idx, const Entr
                      kv, kv + resid);
   int end_bit = 1;  // destination rows are below 2^32 here (checked by the caller)
   while (end_bit < 32 && (max_dst >> end_bit)) ++end_bit;
-  int rc = radix_sort_pairs_u32(kv, kv + 2 * resid, kv + resid, kv + 3 * resid, resid, end_bit, s);
+  rc = radix_sort_pairs_u32(kv, kv + 2 * resid, kv + resid, kv + 3 * resid, resid, end_bit, s);
   if (rc == GP_OK) {
     hipLaunchKernelGGL(residual_gather_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, kv + 3 * resid,
-                       resid, key.off0, key.off1, p->sorted);
+                       resid, key.off0, key.off1, static_cast<gp_double_index *>(p->sorted->p));
     rc = hipGetLastError() == hipSuccess ? GP_OK : set_error(GP_ERR_HIP, "residual_gather_kernel launch");
   }
   GP_HIP_TRY(hipFreeAsync(kv, s));
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventRecord(p->ready, s));
+  *built = p;
   cache_insert(std::move(p));
   return GP_OK;
 }
@@ -1740,6 +1789,8 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   GP_HIP_TRY(hipGetDevice(&dev));
   const PlanKey key{dev, OP, reinterpret_cast<uintptr_t>(idx), n, W, limit, off.id0, off.id1};
   std::shared_ptr<CachedPlan> cached = OP == kAssignTo ? nullptr : cache_find(key);
+  // its copy (and sorted residual) may still be in flight on the stream that built them
+  if (cached) GP_HIP_TRY(hipStreamWaitEvent(s, cached->ready, 0));
   const size_t scan_bytes = kScanWordsOff + groups * kScanWords * sizeof(uint64_t);
   char *ws = nullptr;
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), scan_bytes, s));
@@ -1755,7 +1806,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     const size_t grid = std::max<size_t>(1, std::min(groups, (size_t)num_cus() * 8));
     if (cached)
       hipLaunchKernelGGL((index_scan_kernel<OP, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, idx, n, off.id0,
-                         off.id1, W, limit, cached->copy, ws);
+                         off.id1, W, limit, cached->copy_ptr(), ws);
     else
       hipLaunchKernelGGL((index_scan_kernel<OP, false>), dim3((unsigned)grid), dim3(kBlock), 0, s, idx, n, off.id0,
                          off.id1, W, limit, nullptr, ws);
@@ -1842,10 +1893,9 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   }
   const size_t resid = rr.pre[rr.count];
   if (resid == 0) return GP_OK;
-  if (cached && cached->resid == resid) {  // the same index: its destination-sorted residual
-    GP_HIP_TRY(hipStreamWaitEvent(s, cached->ready, 0));
-    return launch_row_op<OP>(y, x, cached->sorted, resid, gp_double_index{0, 0}, W, limit, s, /*sorted=*/true);
-  }
+  if (cached && cached->sorted && cached->resid == resid)  // the same index: its destination-sorted residual
+    return launch_row_op<OP>(y, x, cached->sorted_ptr(), resid, gp_double_index{0, 0}, W, limit, s,
+                             /*sorted=*/true);
   // destinations already (mostly) ascending: the call's order is the sorted one
   size_t resid_tiles = 0, asc_tiles = 0;
   for (uint32_t i = 0; i < rr.count; ++i) {
@@ -1858,14 +1908,24 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     for (; t < t1; ++t) asc_tiles += bit(t, 2);
   }
   const bool ascending = asc_tiles * 10 >= resid_tiles * 9;
+  // a scatter's large unsorted residual is worth a destination-sorted copy
+  // when the index comes back: the second call with the same content builds
+  // it (one radix sort, about what sorting saves in one call) and runs it
+  const bool sortable = OP != kAssignTo && !ascending && resid * W * sizeof(float) >= kSortMinBytes &&
+                        max_dst < (1ull << 32) && n < (1ull << 32);
+  if (sortable && cached && !cached->sorted && cached->resid == resid) {
+    std::shared_ptr<CachedPlan> built;
+    const int rc = cache_second_sighting<OP>(cached, idx, rr, max_dst, s, &built);
+    if (rc != GP_OK) return rc;
+    return launch_row_op<OP>(y, x, built->sorted_ptr(), resid, gp_double_index{0, 0}, W, limit, s,
+                             /*sorted=*/true);
+  }
   for (uint32_t i = 0; i < rr.count; ++i) {
     const int rc = launch_row_op<OP>(y, x, idx + rr.lo[i], rr.hi[i] - rr.lo[i], off, W, limit, s, ascending);
     if (rc != GP_OK) return rc;
   }
-  // a scatter's large unsorted residual: sorted copy for the next call
-  if (OP != kAssignTo && !ascending && resid * W * sizeof(float) >= kSortMinBytes && max_dst < (1ull << 32) &&
-      n < (1ull << 32))
-    return build_cached_plan<OP>(key, idx, rr, max_dst, s);
+  // first sighting: remember the content, so the next call can tell it is the same
+  if (sortable && !cached) return cache_first_sighting(key, idx, resid, s);
   return GP_OK;
 }
 

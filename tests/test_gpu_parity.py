@@ -689,11 +689,12 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
     y = rng.standard_normal(n_cache * W).astype(np.float32)
     ti = torch.from_numpy(idx).to(dev)
     tx = T(x, dev)
-    # add, twice: the first call runs and (unsorted residual) builds the plan
-    # cache entry, the second runs the cached destination-sorted residual
+    # add, three times: the first call runs in op order and (unsorted
+    # residual) leaves a copy of the index, the second builds and runs the
+    # destination-sorted residual, the third runs it from the cache
     e = y.copy()
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
-    for call in range(2):
+    for call in range(3):
         ty = T(y, dev)
         rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, off, W, limit)
         torch.cuda.synchronize()
@@ -703,7 +704,7 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
     e = y.copy()
     e.reshape(n_cache, W)[idx[:, 1] + off[1]] = 0.0
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
-    for call in range(2):
+    for call in range(3):
         ty = T(y, dev)
         rowops.init_rows_from_double_index_gpu(ty, tx, ti, n, off, W, limit)
         torch.cuda.synchronize()
@@ -732,7 +733,8 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
     """The plan cache keys on the index pointer but trusts no pointer: the same
     device tensor refilled with another permutation (same size, offsets,
     limit) must give the new index's sums, not the cached order's; the entry is
-    replaced and the call after that runs the new cached order."""
+    replaced by a copy of the new index (no sort), the next call builds its
+    sorted order and the one after runs it."""
     from geeps_amd import rowops
     rng = np.random.default_rng(99)
     W, n = 128, 40000  # 20 MiB of rows: a cached (unsorted) residual
@@ -748,12 +750,13 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
         ti.copy_(torch.from_numpy(idx))
         e = y.copy()
         oracle.add_rows_from_double_index(e, x, idx, (0, 0), W)
-        for call in range(2):
+        for call in range(3):
             ty = T(y, dev)
             rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W)
             torch.cuda.synchronize()
             assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), (round_, call)
-            assert _cache_entries()[0] == 1
+            # one entry: the index's copy (16 B a row), plus its sorted residual from the 2nd call on
+            assert _cache_entries() == (1, 16 * n * (1 if call == 0 else 2)), (round_, call)
         prev = idx
 
 
