@@ -1654,6 +1654,9 @@ struct CachedPlan {
   PlanKey key{};
   std::shared_ptr<DevBuf> copy;    // the index as first seen
   std::shared_ptr<DevBuf> sorted;  // its residual, offsets applied, ascending destination
+  // copy-only entry: the buffer its sorted residual will go to, allocated on
+  // the first call (the allocation overlaps that call's kernels)
+  std::shared_ptr<DevBuf> spare;
   size_t resid = 0;
   hipEvent_t ready = nullptr;  // recorded once copy (and sorted) are built, on the building stream
   uint64_t last_use = 0;
@@ -1728,9 +1731,11 @@ int cache_first_sighting(const PlanKey &key, const gp_double_index *idx, size_t 
   auto p = std::make_shared<CachedPlan>();
   p->key = key;
   p->resid = resid;
-  p->bytes = key.n * sizeof(gp_double_index);
+  p->bytes = (key.n + resid) * sizeof(gp_double_index);
   int rc = GP_OK;
   p->copy = std::make_shared<DevBuf>(key.n * sizeof(gp_double_index), key.device, &rc);
+  if (rc != GP_OK) return rc;
+  p->spare = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
   GP_HIP_TRY(hipMemcpyAsync(p->copy->p, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
@@ -1754,7 +1759,10 @@ int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_doub
   p->bytes = (key.n + resid) * sizeof(gp_double_index);
   p->copy = seen->copy;
   int rc = GP_OK;
-  p->sorted = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
+  if (seen->spare)
+    p->sorted = seen->spare;  // written only here: no call reads a copy-only entry's spare
+  else
+    p->sorted = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
   uint32_t *kv = nullptr;  // keys, values, sorted keys, sorted values

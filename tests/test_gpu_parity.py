@@ -755,8 +755,8 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
             rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W)
             torch.cuda.synchronize()
             assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), (round_, call)
-            # one entry: the index's copy (16 B a row), plus its sorted residual from the 2nd call on
-            assert _cache_entries() == (1, 16 * n * (1 if call == 0 else 2)), (round_, call)
+            # one entry: the index's copy and its sorted residual (16 B a row each)
+            assert _cache_entries() == (1, 2 * 16 * n), (round_, call)
         prev = idx
 
 
