@@ -170,11 +170,11 @@ struct Channel {
   std::vector<std::thread> server_readers;
   PinnedArray<float> reply_buf;
   // server side, same-node clients: mapped oplog buffers, whether the client
-  // takes refreshes in place (its hello said so), and which master versions'
+  // takes refreshes in place (its ZMTP READY said so), and which master versions'
   // IPC handles it already has
   std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
   std::vector<uint8_t> ipc_client;                       // [client]
-  // [process]: runs on another GPU of this node (its hello's PCI bus id)
+  // [process]: runs on another GPU of this node (its READY's PCI bus id)
   std::vector<uint8_t> other_gpu;
   // [client]: stage its oplog slices into local HBM (a peer copy over xGMI on
   // the server's copy stream) before the sum, instead of the sum reading them
