@@ -25,7 +25,8 @@ import numpy as np
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PEER = os.path.join(REPO, "build", "tests", "zmtp_peer")
+# ZMTP_PEER: another build of the same program, e.g. an ASan/UBSan one
+PEER = os.environ.get("ZMTP_PEER") or os.path.join(REPO, "build", "tests", "zmtp_peer")
 
 ZMQ_ROUTER, ZMQ_ROUTING_ID, ZMQ_SNDMORE, ZMQ_RCVMORE = 6, 5, 2, 13
 ZMQ_LINGER, ZMQ_RCVTIMEO, ZMQ_SNDTIMEO, ZMQ_ROUTER_MANDATORY = 17, 27, 28, 33
