@@ -675,7 +675,11 @@ void ClientLib::decide_fused_init() {
           ++covered;
         }
       }
-      ch.init_ok[t] = ok && covered == pc.num_rows;
+      // Read-my-writes re-applies a refresh's pending oplogs, the current
+      // clock's included (recv_row_batch): its rows must be zero until an
+      // op writes them, as after the reference's zerofy (clientlib-data.cpp:
+      // 356-371), so that mode keeps the zeroed oplog.
+      ch.init_ok[t] = ok && covered == pc.num_rows && !config_.read_my_writes;
     }
   }
   // Direct oplog: an update op whose rows are one channel's cache rows in
