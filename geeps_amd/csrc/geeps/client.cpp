@@ -926,12 +926,12 @@ void ClientLib::update_batch(int handle) {
       // add_rows_from_double_index_gpu (clientlib-data.cpp:385-394) through the
       // op's row plan for this channel (its index, offset 0, num_vals_limit)
       const gp_row_plan plan = pre.plans[ch.id]->get();
-      if (in_place)
-        ;  // the app wrote these rows into the oplog itself
-      else if (fused)
-        GP_CALL(gp_scatter_init_rows_planned(oplog->data(), x, plan, ch.stream->get()));
-      else
-        GP_CALL(gp_scatter_add_rows_planned(oplog->data(), x, plan, ch.stream->get()));
+      if (!in_place) {  // (in place: the app wrote these rows into the oplog itself)
+        if (fused)
+          GP_CALL(gp_scatter_init_rows_planned(oplog->data(), x, plan, ch.stream->get()));
+        else
+          GP_CALL(gp_scatter_add_rows_planned(oplog->data(), x, plan, ch.stream->get()));
+      }
       if (config_.read_my_writes && pc.segmented) {
         // (unreachable today: read-my-writes refreshes are private copies, so
         // its cache is never segmented; the unplanned add has no repeat layers)
