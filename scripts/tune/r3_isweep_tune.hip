@@ -18,6 +18,8 @@
 // phase a wave loads its slot's index entries of the NEXT launch, so they sit
 // in L2 / MALL when that launch starts.
 // Every variant is bit-checked against the production planned call.
+// Probe 7 (psweep_kernel): the same slices in one persistent launch, the next
+// slice's index entries loaded under this slice's writes.
 // Usage: r3_isweep_tune [rounds]
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
@@ -119,6 +121,85 @@ __global__ __launch_bounds__(kBlock) void isweep_kernel(float *__restrict__ y, c
   if (PF) asm volatile("" ::"v"(nx0.id0), "v"(nx1.id0));
 }
 
+// Persistent form (probe 7): each wave loops over slices wave, wave + waves,
+// ... of 128 plan entries; the next slice's entries load into registers while
+// this slice's rows are written, so no slice waits for a dependent index load
+// (the launch-start bubble of isweep_kernel).  One launch.
+template <int OP, int TG>
+__global__ __launch_bounds__(kBlock) void psweep_kernel(float *__restrict__ y, const float *__restrict__ x,
+                                                        const gp_double_index *__restrict__ index,
+                                                        size_t n_rows) {
+  typedef __attribute__((address_space(1))) f4 GT;
+  static_assert(kPairs % TG == 0, "whole bursts");
+  __shared__ f4 lds[4][kLdsRows * 32];
+  const int wv = threadIdx.x / 64, wl = threadIdx.x % 64, lane = wl % 32, gw = wl / 32;
+  const size_t waves = (size_t)gridDim.x * 4;
+  const size_t stride = waves * kWaveRows;
+  size_t base = ((size_t)blockIdx.x * 4 + wv) * kWaveRows;
+  if (base >= n_rows) return;
+  auto resolve = [&](size_t b, uint64_t *src, uint64_t *dst) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const size_t e = b + k * 64 + wl;
+      src[k] = dst[k] = kNone;
+      if (e < n_rows) {
+        const gp_double_index ix = index[e];
+        uint64_t from, to;
+        row_endpoints<OP>(ix, 0, 0, from, to);
+        src[k] = reinterpret_cast<uint64_t>(x + from * W);
+        dst[k] = reinterpret_cast<uint64_t>(y + to * W);
+      }
+    }
+  };
+  uint64_t src[2], dst[2];
+  resolve(base, src, dst);
+  for (; base < n_rows; base += stride) {
+    f4 keep[kRegPairs];
+#pragma unroll
+    for (int p0 = 0; p0 < kPairs; p0 += TG) {
+      f4 v[TG];
+#pragma unroll
+      for (int j = 0; j < TG; ++j) {
+        const int p = p0 + j, r = 2 * p;
+        const uint64_t sp = shfl64(src[r / 64], (r % 64) + gw);
+        v[j] = f4(0.0f);
+        if (sp != kNone) v[j] = __builtin_nontemporal_load(reinterpret_cast<const GT *>(sp) + lane);
+      }
+#pragma unroll
+      for (int j = 0; j < TG; ++j) {
+        const int p = p0 + j;
+        const f4 val = OP == kInitFrom ? f4(0.0f) + v[j] : v[j];
+        if (p < kLdsPairs)
+          lds[wv][(2 * p + gw) * 32 + lane] = val;
+        else
+          keep[p >= kLdsPairs ? p - kLdsPairs : 0] = val;
+      }
+    }
+    uint64_t nsrc[2], ndst[2];
+    resolve(base + stride, nsrc, ndst);  // the next slice's entries, under this slice's writes
+#pragma unroll
+    for (int p = 0; p < kPairs; ++p) {
+      const int r = 2 * p;
+      const uint64_t dp = shfl64(dst[r / 64], (r % 64) + gw);
+      if (dp != kNone)
+        __builtin_nontemporal_store(p < kLdsPairs ? lds[wv][(2 * p + gw) * 32 + lane]
+                                                  : keep[p >= kLdsPairs ? p - kLdsPairs : 0],
+                                    reinterpret_cast<GT *>(dp) + lane);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      src[k] = nsrc[k];
+      dst[k] = ndst[k];
+    }
+  }
+}
+
+template <int OP, int TG>
+void launch_psweep(float *y, const float *x, const gp_double_index *ix, size_t n) {
+  const size_t G = (size_t)num_cus();
+  hipLaunchKernelGGL((psweep_kernel<OP, TG>), dim3((unsigned)G), dim3(kBlock), 0, 0, y, x, ix, n);
+}
+
 __global__ void mismatch_kernel(const uint32_t *a, const uint32_t *b, size_t n, unsigned long long *cnt) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   unsigned long long c = 0;
@@ -185,13 +266,17 @@ int main(int argc, char **argv) {
   vs.push_back({"gath isweep TG8  PF", [&] { launch_isweep<kAssignTo, 8, true>(y, x, igat, R); }, 1});
   vs.push_back({"gath isweep TG16 PF", [&] { launch_isweep<kAssignTo, 16, true>(y, x, igat, R); }, 1});
   vs.push_back({"gath isweep TG32 PF", [&] { launch_isweep<kAssignTo, 32, true>(y, x, igat, R); }, 1});
+  vs.push_back({"gath psweep TG16", [&] { launch_psweep<kAssignTo, 16>(y, x, igat, R); }, 1});
+  vs.push_back({"gath psweep TG32", [&] { launch_psweep<kAssignTo, 32>(y, x, igat, R); }, 1});
   vs.push_back({"init prod (wave, plan)", [&] { gp_scatter_init_rows_planned(y, x, pi, 0); }, 2});
+  vs.push_back({"init psweep TG32", [&] { launch_psweep<kInitFrom, 32>(y, x, iini, R); }, 2});
   vs.push_back({"init isweep TG16", [&] { launch_isweep<kInitFrom, 16, false>(y, x, iini, R); }, 2});
   vs.push_back({"init isweep TG16 PF", [&] { launch_isweep<kInitFrom, 16, true>(y, x, iini, R); }, 2});
   vs.push_back({"init isweep TG32 PF", [&] { launch_isweep<kInitFrom, 32, true>(y, x, iini, R); }, 2});
   vs.push_back({"ident copy prod (dense sweep)", [&] { gp_gather_rows_planned(y, x, pid, 0); }, 3});
   vs.push_back({"ident isweep TG16", [&] { launch_isweep<kAssignTo, 16, false>(y, x, iident, R); }, 3});
   vs.push_back({"ident isweep TG16 PF", [&] { launch_isweep<kAssignTo, 16, true>(y, x, iident, R); }, 3});
+  vs.push_back({"ident psweep TG32", [&] { launch_psweep<kAssignTo, 32>(y, x, iident, R); }, 3});
 
   for (int c = 1; c <= 3; ++c) {
     if (c == 1) GK(gp_gather_rows_planned(yr, x, pg, 0));
