@@ -283,3 +283,74 @@ def test_silent_peer_times_out_the_handshake():
         if p.poll() is None:
             p.kill()
             p.wait()
+
+
+ZMQ_DEALER = 5
+
+
+def test_libzmq_dealer_client_and_a_large_push():
+    """A ROUTER talks to DEALER peers too: a libzmq DEALER named client-6
+    pushes a 20,000-row CLOCK_WITH_UPDATES_BATCH (10 MiB in one frame) to a
+    libgeeps tablet-1 and gets the READ_ROW_BATCH back, no routing frames on
+    the DEALER side."""
+    port = free_port()
+    rows = 20000
+    p = subprocess.Popen([PEER, "server", str(port), "1"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True)
+    r = Router(b"client-6")
+    try:
+        ZMQ.zmq_close(r.s)  # the same options on a DEALER socket instead
+        r.s = ZMQ.zmq_socket(r.ctx, ZMQ_DEALER)
+        r._opt(ZMQ_ROUTING_ID, b"client-6")
+        r._int(ZMQ_LINGER, 0)
+        r._int(ZMQ_RCVTIMEO, 20000)
+        r._int(ZMQ_SNDTIMEO, 20000)
+        assert p.stdout.readline().strip() == "listening"
+        assert ZMQ.zmq_connect(r.s, f"tcp://127.0.0.1:{port}".encode()) == 0
+        vals = update_rows(rows)
+        hdr = struct.pack("<B3xIiIii", CLOCK_WITH_UPDATES_BATCH, 6, 3, 0, 0, 0)
+        parts = [hdr, keys(rows).tobytes(), vals.tobytes()]
+        for i, part in enumerate(parts):  # a DEALER sends the message parts only
+            buf = ctypes.create_string_buffer(part, len(part))
+            assert ZMQ.zmq_send(r.s, buf, len(part), ZMQ_SNDMORE if i + 1 < len(parts) else 0) == len(part)
+        got, _ = r.recv()
+        assert len(got) == 3
+        cmd, server_id, data_age, _, table_id, _ = struct.unpack("<B3xIiiIi", got[0])
+        assert (cmd, server_id, data_age, table_id) == (READ_ROW_BATCH, 1, 3, 0)
+        np.testing.assert_array_equal(np.frombuffer(got[2], np.float32).reshape(-1, W), vals + vals)
+        r.close()
+        r = None
+        out, err = p.communicate(timeout=30)  # the DEALER closed: the server reads EOF
+        assert p.returncode == 0, err
+        assert "prop Socket-Type=DEALER" in out and "served=1" in out
+    finally:
+        if r is not None:
+            r.close()
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+
+
+def test_incompatible_socket_type_is_refused():
+    """A peer whose READY names a socket type a ROUTER cannot talk to (PUB) is
+    refused by name."""
+    port = free_port()
+    ls = socket.socket()
+    ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    ls.bind(("127.0.0.1", port))
+    ls.listen(1)
+    p = subprocess.Popen([PEER, "client", str(port), "1", "0", "1"], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        c, _ = ls.accept()
+        greeting = b"\xff" + bytes(8) + b"\x7f" + b"\x03\x00" + b"NULL".ljust(20, b"\0") + b"\x00" + bytes(31)
+        body = b"\x05READY" + b"\x0bSocket-Type" + struct.pack(">I", 3) + b"PUB"
+        c.sendall(greeting + bytes([0x04, len(body)]) + body)
+        _, err = p.communicate(timeout=30)
+        assert p.returncode != 0 and "a ROUTER cannot talk to a 'PUB' socket" in err
+        c.close()
+    finally:
+        ls.close()
+        if p.poll() is None:
+            p.kill()
+            p.wait()
