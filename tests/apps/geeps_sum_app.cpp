@@ -19,7 +19,8 @@
 // process per GPU, as on an 8-GPU node), selected before GeePs is created.
 // GEEPS_TEST_SHUFFLE_UPDATES=1: every PreUpdate lists its blob's rows in a
 // shuffled order (seeded per blob), so the update op's DoubleIndex maps op
-// rows to cache rows by a permutation and libgeeps' row plan reorders it.
+// rows to cache rows by a permutation and libgeeps' row plan reorders it;
+// =odd: only the odd blobs' (the even ones can take the direct oplog).
 //
 // `layers` (comma-separated row counts, summing to `rows`) switches to a
 // Caffe-like op sequence: a Read per parameter blob in forward order, then per
@@ -144,11 +145,14 @@ int main(int argc, char **argv) {
     return ids;
   };
   // upd_row[l][j]: the blob row the update op's buffer row j carries
-  const bool shuffle = std::getenv("GEEPS_TEST_SHUFFLE_UPDATES") != nullptr;
+  // ("odd": only the odd blobs, so one clock mixes in-order and shuffled ops)
+  const char *shuffle_env = std::getenv("GEEPS_TEST_SHUFFLE_UPDATES");
+  const bool shuffle_odd = shuffle_env && std::string(shuffle_env) == "odd";
   std::vector<std::vector<size_t>> upd_row(L);
   for (size_t l = 0; l < L; ++l) {
     upd_row[l].resize(layer_rows[l]);
     for (size_t r = 0; r < layer_rows[l]; ++r) upd_row[l][r] = r;
+    const bool shuffle = shuffle_env && (!shuffle_odd || l % 2 == 1);
     uint32_t st = 0x2545f491u ^ (uint32_t)(l * 2654435761u + 17);
     for (size_t r = layer_rows[l]; shuffle && r > 1; --r) {  // Fisher-Yates
       st ^= st << 13;

@@ -429,3 +429,22 @@ def test_shuffled_update_rows(dev, P, mode, slack):
     procs = [_spawn([SUM_APP, str(p), str(P), str(base), "2000", "6", str(slack), "2", "0", mode,
                      "700,5,900,395"], env) for p in range(P)]
     _collect(procs, 240)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,mode", [(1, "float"), (2, "int")])
+def test_direct_and_copied_updates_share_a_clock(dev, P, mode):
+    """One clock mixes update ops that write the oplog in place (in-order blobs
+    within one channel: the direct oplog) with ops the fused init copies in
+    (shuffled blobs, and a blob spanning both channels): every Read exact
+    (bit-exact with float deltas at one process), and both kinds ran."""
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    base = _ports(P, 2)
+    env = _env("ipc", extra={"GEEPS_TEST_SHUFFLE_UPDATES": "odd"})
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), "2000", "6", "0", "2", "0", mode,
+                     "700,5,900,395"], env) for p in range(P)]
+    for s in _stats(_collect(procs, 240)):
+        c = s["client"]
+        assert 0 < c["nr_update_direct"] < c["nr_update"] - 4, c  # 4 setup-clock updates
+
