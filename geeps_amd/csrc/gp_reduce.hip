@@ -866,7 +866,13 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // segmented), the fused init, and the scatter-add of destination-sorted rows
 // (a row plan's residual, a device-binned residual); in op order the
 // scatter-add keeps row_op_kernel.  Every access non-temporal.
-template <typename T, int OP, int LPR, int RPG, int SEG>
+// MAP 0 (production): wave w takes tiles w, w + waves, ... (grid-stride).
+// MAP 2 (tuning harnesses only): the blocks of one XCD -- dealt round-robin,
+// so blocks b and b + 8 share one (MI355X_MICROARCH.md, workgroup dispatch)
+// -- take one contiguous eighth of the tiles, grid-stride inside it; needs a
+// multiple of 8 blocks.  It tied or lost on a random index (probe 8,
+// profiles/r03/tune/r3_tilemap_tune.txt).
+template <typename T, int OP, int LPR, int RPG, int SEG, int MAP = 0>
 __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
     const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
@@ -885,8 +891,19 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
   const int wl = threadIdx.x & 63, lane = wl % LPR, gw = wl / LPR;
   const size_t wave = ((size_t)blockIdx.x * kBlock + threadIdx.x) / 64;
   const size_t wstride = (size_t)gridDim.x * (kBlock / 64) * 64;
+  // MAP 2: this XCD's region of tiles [r0, r1) (rows), walked from lw by lstride
+  size_t r1 = num_rows, lstride = wstride;
   size_t t = wave * 64;
-  if (t >= num_rows) return;  // wave-uniform: every lane of a wave reaches each __shfl
+  if constexpr (MAP == 2) {
+    const size_t tiles = (num_rows + 63) / 64, region = (tiles + 7) / 8 * 64;
+    const size_t xcd = blockIdx.x % 8, per = gridDim.x / 8;
+    const size_t lw = (blockIdx.x / 8) * (kBlock / 64) + threadIdx.x / 64;
+    lstride = per * (kBlock / 64) * 64;
+    const size_t r0 = xcd * region;
+    r1 = r0 + region < num_rows ? r0 + region : num_rows;
+    t = r0 + lw * 64;
+  }
+  if (t >= r1) return;  // wave-uniform: every lane of a wave reaches each __shfl
 
   // this lane's row of the current tile: source / destination row pointers,
   // and whether the row is clear of num_vals_limit (guarded on the
@@ -915,9 +932,9 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     if (live) ix = index[t + wl];
     resolve(ix, live);
   }
-  for (; t < num_rows; t += wstride) {
-    const size_t nr = t + wstride + wl;  // next tile's entry, in flight meanwhile
-    const bool nlive = nr < num_rows;
+  for (; t < r1; t += lstride) {
+    const size_t nr = t + lstride + wl;  // next tile's entry, in flight meanwhile
+    const bool nlive = MAP == 2 ? t + lstride < r1 && nr < num_rows : nr < num_rows;
     gp_double_index nix = {0, 0};
     if (nlive) nix = index[nr];
     const size_t rows_here = num_rows - t < 64 ? num_rows - t : 64;
