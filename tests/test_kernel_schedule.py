@@ -67,7 +67,8 @@ def test_wave_kernels_fit_their_occupancy(asm):
     limit-straddle path must not index register arrays at run time (that cost
     86-91 more VGPRs and halved the resident blocks; profiles/r02)."""
     for op, max_vgpr in ((0, 168), (1, 128), (3, 128)):  # add, gather, init at 128-float rows
-        pat = rf"_ZN12_GLOBAL__N_115row_wave_kernelIDv4_fLi{op}ELi32ELi8ELi0EEE"
+        # <f4, OP, 32 lanes, 8 rows, flat, MAP 0 (the production tile map)>
+        pat = rf"_ZN12_GLOBAL__N_115row_wave_kernelIDv4_fLi{op}ELi32ELi8ELi0ELi0EEE"
         name = re.search(rf"^({pat}\S*):", asm, re.M).group(1)
         n = int(re.search(rf"\.set {re.escape(name)}\.num_vgpr, (\d+)", asm).group(1))
         assert n <= max_vgpr, (op, n)
