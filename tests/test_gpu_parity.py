@@ -4,6 +4,8 @@ Bar: bit-exact.  Every kernel here is integer indexing plus fp32 adds in the
 reference's order, so results must match the oracle bit for bit (compared as
 uint32 views, so -0.0 / NaN payloads count too).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -1026,7 +1028,12 @@ def _fuzz_index(rng, n_cache, W):
     return idx[rng.permutation(idx.shape[0])], idx.shape[0]
 
 
-@pytest.mark.parametrize("case", range(24))
+# GEEPS_FUZZ_CASES=<n> widens the fuzzed parity tests below (a one-off
+# campaign, scripts/gpu_runs/r03/fuzz.sh); the default keeps the suite short.
+_FUZZ_CASES = int(os.environ.get("GEEPS_FUZZ_CASES", "24"))
+
+
+@pytest.mark.parametrize("case", range(_FUZZ_CASES))
 def test_row_plans_fuzz(dev, case):
     """Random op indexes (dense runs around the plan threshold, short runs,
     scattered rows), row sizes, offsets and num_vals_limit: the scatter plan's
@@ -1210,3 +1217,48 @@ def test_bucket_sum_plan_boundaries_fuzz(dev, case):
         out = master
     torch.cuda.synchronize()
     assert torch.equal(out.view(torch.int32), expect.view(torch.int32)), (n, N, out_of_place)
+
+
+@pytest.mark.parametrize("case", range(max(6, _FUZZ_CASES // 4)))
+def test_unplanned_calls_fuzz(analyzed, dev, case):
+    """The reference binding's unplanned calls through the device plan and
+    its plan cache, on fuzzed indexes (dense runs around the sweep threshold,
+    short runs, scattered rows, in shuffled op order), row sizes, offsets and
+    num_vals_limit: three scatter-adds (first call in op order, second builds
+    the sorted residual, third runs it), two inits and a gather, each bit for
+    bit against the oracle."""
+    from geeps_amd import rowops
+    rng = np.random.default_rng(7000 + case)
+    W = int(rng.choice([4, 64, 128, 132, 256]))
+    n_cache = 3 * max(1, (4 << 20) // (W * 4)) + int(rng.integers(100, 5000))
+    off = (int(rng.integers(0, 4)), int(rng.integers(0, 4)))
+    idx, n_op = _fuzz_index(rng, n_cache - off[1], W)
+    n_x = n_op + off[0]
+    limit = None if rng.random() < 0.5 else int(rng.integers(1, n_x * W + 1))
+    x = rng.standard_normal(n_x * W).astype(np.float32)
+    x[rng.choice(x.size, min(x.size, 200), replace=False)] = np.float32(-0.0)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    tx, ti = T(x, dev), torch.from_numpy(idx).to(dev)
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    for call in range(3):
+        ty = T(y, dev)
+        rowops.add_rows_from_double_index_gpu(ty, tx, ti, n_op, off, W, limit)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", case, call, W, off, limit)
+    e = y.copy()
+    e.reshape(n_cache, W)[idx[:, 1] + off[1]] = 0.0
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    for call in range(2):
+        ty = T(y, dev)
+        rowops.init_rows_from_double_index_gpu(ty, tx, ti, n_op, off, W, limit)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", case, call, W, off, limit)
+    dst = rng.standard_normal(n_x * W).astype(np.float32)
+    e = dst.copy()
+    oracle.assign_rows_to_double_index(e, y, idx, off, W, limit)
+    td = T(dst, dev)
+    rowops.assign_rows_to_double_index_gpu(td, T(y, dev), ti, n_op, off, W, limit)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(td.cpu().numpy()), bits(e)), ("gather", case, W, off, limit)
+
