@@ -448,3 +448,51 @@ def test_direct_and_copied_updates_share_a_clock(dev, P, mode):
         c = s["client"]
         assert 0 < c["nr_update_direct"] < c["nr_update"] - 4, c  # 4 setup-clock updates
 
+
+
+# GEEPS_STRESS_CASES=<n> widens the randomized configurations below (a one-off
+# campaign, scripts/gpu_runs/r03/stress.sh); the default keeps the suite short.
+_STRESS_CASES = int(os.environ.get("GEEPS_STRESS_CASES", "4"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(_STRESS_CASES))
+def test_randomized_configurations(dev, case):
+    """Seeded random mixes of what the other tests vary one at a time:
+    processes, slack, channels, tables, read-my-writes, a local-access op,
+    transport, layer shapes, shuffled update rows, jitter, the direct oplog and
+    both peer-staging switches.  Every Read is checked by the app (exact at
+    BSP, within the SSP bounds otherwise)."""
+    import random
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    rng = random.Random(4200 + case)
+    P = rng.choice([1, 2, 2, 3, 4])
+    slack = rng.choice([0, 0, 1, 2])
+    channels = rng.choice([1, 2])
+    rmw = 1 if rng.random() < 0.3 else 0
+    tables = rng.choice([1, 1, 2])
+    local = rng.choice([0, 0, 1])
+    mode = "float" if P == 1 and rng.random() < 0.5 else "int"
+    rows = rng.randrange(300, 3000)
+    cuts = sorted(rng.sample(range(1, rows), rng.randrange(0, 5)))
+    layers = [b - a for a, b in zip([0] + cuts, cuts + [rows])]
+    tables = min(tables, len(layers))  # every table written (clientlib-viter.cpp:800 CHECKs it)
+    extra = {"GEEPS_TEST_JITTER_US": str(rng.choice([0, 0, 1500]))}
+    shuffle = rng.choice([None, "odd", "1"])
+    if shuffle:
+        extra["GEEPS_TEST_SHUFFLE_UPDATES"] = shuffle
+    extra["GEEPS_DIRECT_OPLOG"] = rng.choice(["1", "1", "0"])
+    for k in ("GEEPS_STAGE_PEER_UPDATES", "GEEPS_STAGE_PEER_REFRESH"):
+        v = rng.choice([None, "0", "1"])
+        if v:
+            extra[k] = v
+    transport = rng.choice(["ipc", "ipc", "tcp"])
+    desc = dict(P=P, slack=slack, channels=channels, rmw=rmw, tables=tables, local=local, mode=mode,
+                layers=layers, transport=transport, **extra)
+    print("config", desc)
+    base = _ports(P, channels)
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), "8", str(slack), str(channels),
+                     str(rmw), mode, ",".join(map(str, layers)), str(tables), str(local)],
+                    _env(transport, extra=extra)) for p in range(P)]
+    _collect(procs, 240)
