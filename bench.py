@@ -737,6 +737,12 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
     r = mod.run(1, rd_rows, clocks, warmup, 0, "ipc", timeout=120, extra_env={"GEEPS_DIRECT_OPLOG": "0"})
     out["p1_copy"] = {"workers": 1, "ms_per_clock": r["ms_per_clock_max"],
                       "delta_GBps": r["aggregate_delta_GBps"], "direct_oplog": False}
+    # the same clock with direct reads (GEEPS_DIRECT_READ=1, opt-in: the app
+    # treats Read buffers as read-only): Read hands out the in-place master
+    # version's rows, so the gather's copy goes too (one shard: P = 1)
+    r = mod.run(1, rd_rows, clocks, warmup, 0, "ipc", timeout=120, extra_env={"GEEPS_DIRECT_READ": "1"})
+    out["p1_direct_read"] = {"workers": 1, "ms_per_clock": r["ms_per_clock_max"],
+                             "delta_GBps": r["aggregate_delta_GBps"], "direct_read": True}
     # configs[4]'s shape: the AlexNet-sized table (60,965,224 parameters in
     # 476,292 RowData rows, blobs padded to whole rows) clocked by 8 worker
     # processes (8 server shards) sharing this GPU, staleness bound 1

@@ -53,6 +53,7 @@ std::string ClientStats::to_json() const {
     << ", \"nr_clock\": " << nr_clock << ", \"nr_push\": " << nr_push
     << ", \"nr_refresh\": " << nr_refresh << ", \"nr_refresh_in_place\": " << nr_refresh_in_place
     << ", \"nr_refresh_staged\": " << nr_refresh_staged << ", \"nr_update_direct\": " << nr_update_direct
+    << ", \"nr_read_direct\": " << nr_read_direct << ", \"nr_read_pin_deferred\": " << nr_read_pin_deferred
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -97,6 +98,8 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
   stage_refresh_mode_ = mode("GEEPS_STAGE_PEER_REFRESH");
   const char *direct = std::getenv("GEEPS_DIRECT_OPLOG");
   direct_oplog_ = !(direct && std::string(direct) == "0");
+  const char *direct_read = std::getenv("GEEPS_DIRECT_READ");
+  direct_read_ = direct_read && std::string(direct_read) == "1";
   const char *delay = std::getenv("GEEPS_TEST_READER_DELAY_US");
   reader_delay_us_ = delay ? std::atoi(delay) : 0;
   // Same-node peers exchange rows device to device through IPC-mapped HBM
@@ -436,6 +439,19 @@ void ClientLib::ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a) {
                "refresh ACK to server " << s << " failed");
 }
 
+void ClientLib::give_back(Channel &ch, uint32_t s, uint32_t table, int v) {
+  if (s == process_id_) {
+    ch.server->release(process_id_, table, v);
+    return;
+  }
+  RefreshAckMsg a{};
+  a.cmd = kCmdRefreshAck;
+  a.client_id = process_id_;
+  a.table_id = table;
+  a.version = v;
+  ack_to_server(ch, s, a);
+}
+
 void ClientLib::remote_shutdown_ack(uint32_t channel, uint32_t client_id) {
   if (client_id == process_id_) return;
   Channel &ch = *channels_[channel];
@@ -598,6 +614,8 @@ void ClientLib::finish_virtual_iteration() {
       pc.live_ver.assign(num_processes_, -1);
       pc.live_ptr.assign(num_processes_, nullptr);
       pc.server_versions.resize(num_processes_);
+      pc.pins.assign(num_processes_, {});
+      pc.deferred.assign(num_processes_, {});
       pc.server_clock.assign(num_processes_, INITIAL_DATA_AGE);
     }
     ch.stream->sync();
@@ -742,7 +760,7 @@ void ClientLib::create_double_index(OpInfo &op) {
   // runs (first-access order makes an op's rows one run per channel) are
   // copied by the phase-separated kernels, which hold their rate on every
   // allocation.
-  if (op.type == OpInfo::PRE_WRITE) {
+  if (op.type == OpInfo::PRE_WRITE || op.type == OpInfo::READ) {
     op.direct_channel = -1;
     for (uint32_t c = 0; c < num_channels_; ++c) {
       if (per[c].size() != op.rows.size() || op.rows.empty()) continue;
@@ -800,6 +818,7 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
   const double t0 = now_s();
   const iter_t need = iteration_ - op.slack - 1;
   double waited = 0;
+  float *direct = nullptr;
   for (auto &chp : channels_) {
     Channel &ch = *chp;
     ParamCache &pc = ch.tables[op.table_id];
@@ -814,6 +833,23 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
       }
     }
     waited += now_s() - w0;
+    if (direct_read_ && started_ && op.direct_channel == (int)ch.id) {
+      // Direct read: the op's rows are one server's shard rows in order and
+      // that shard is read in place, so the buffer is the master version's own
+      // rows.  The version stays pinned (not given back, so the server never
+      // writes it) until PostRead.
+      const size_t lo = op.direct_lo, n = op.rows.size();
+      for (uint32_t s = 0; s < num_processes_; ++s) {
+        const size_t first = pc.server_row_start[s];
+        if (lo < first || lo + n > first + pc.server_num_rows[s] || pc.live_ver[s] < 0) continue;
+        direct = const_cast<float *>(pc.live_ptr[s]) + (lo - first) * ROW_DATA_SIZE;
+        op.pin_server = (int)s;
+        op.pin_version = pc.live_ver[s];
+        ++pc.pins[s][op.pin_version];
+        break;
+      }
+      if (direct) continue;
+    }
     // assign_rows_to_double_index_gpu (clientlib-data.cpp:254-278) through the
     // op's gather plan for this channel (its index, offset 0, num_vals_limit)
     float *const y = reinterpret_cast<float *>(op.buffer.data());
@@ -823,10 +859,11 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
       GP_CALL(gp_gather_rows_planned(y, pc.data.data(), op.plans[ch.id]->get(), ch.stream->get()));
     ch.stream->sync();
   }
-  *buffer = reinterpret_cast<RowData *>(op.buffer.data());
+  *buffer = reinterpret_cast<RowData *>(direct ? direct : op.buffer.data());
   op.in_use = true;
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_read++;
+  if (direct) stats_.nr_read_direct++;
   stats_.rows_read += op.rows.size();
   stats_.read_wait_time += waited;
   stats_.read_time += now_s() - t0;
@@ -842,6 +879,29 @@ void ClientLib::postread_batch(int handle) {
   // GPU-resident local data is used in place, so `keep` needs no copy back
   // (the reference copies back only for CPU-placed local data).
   pre.in_use = false;
+  if (pre.pin_server < 0) return;
+  // A direct Read's pin ends: a version a refresh replaced meanwhile goes back
+  // to its server once no direct Read pins it (outside ch.mu, as the reader
+  // threads give versions back).
+  Channel &ch = *channels_[pre.direct_channel];
+  const uint32_t s = (uint32_t)pre.pin_server;
+  const int v = pre.pin_version;
+  pre.pin_server = pre.pin_version = -1;
+  bool back = false;
+  {
+    std::lock_guard<std::mutex> lk(ch.mu);
+    ParamCache &pc = ch.tables[pre.table_id];
+    auto it = pc.pins[s].find(v);
+    GP_CHECK(it != pc.pins[s].end() && it->second > 0);
+    if (--it->second == 0) {
+      pc.pins[s].erase(it);
+      back = pc.deferred[s].erase(v) > 0;
+    }
+  }
+  if (!back) return;
+  give_back(ch, s, pre.table_id, v);
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nr_read_pin_deferred++;
 }
 
 // ---------------------------------------------------------------------------
@@ -1142,6 +1202,14 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
       ch.svc_stream->sync();
       rebuild_segments(pc);
     }
+    // a replaced version goes back now, or at the PostRead of the last direct
+    // Read pinning it
+    auto retire = [&](int v) {
+      if (pc.pins[server_id].count(v))
+        pc.deferred[server_id].insert(v);
+      else
+        released.push_back(v);
+    };
     if (num_rows) {
       const int prev = pc.live_ver[server_id];
       staged = version >= 0 && ch.stage_refresh_from[server_id];
@@ -1151,7 +1219,7 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
         // never rewritten while we hold it; the one it replaces goes back.
         in_place = true;
         if (prev != version) {
-          if (prev >= 0) released.push_back(prev);
+          if (prev >= 0) retire(prev);
           pc.live_ver[server_id] = version;
           pc.live_ptr[server_id] = rows;
           rebuild_segments(pc);
@@ -1179,7 +1247,7 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
         ch.svc_stream->sync();
         if (version >= 0) released.push_back(version);  // copied: give it back now
         if (prev >= 0) {
-          released.push_back(prev);
+          retire(prev);
           pc.live_ver[server_id] = -1;
           pc.live_ptr[server_id] = nullptr;
           rebuild_segments(pc);

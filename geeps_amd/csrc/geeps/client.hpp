@@ -68,15 +68,19 @@ struct OpInfo {
   // PRE_WRITE: per channel, the channel's slice of `index` as a row plan
   // (destination-sorted), which the oplog scatter-add / fused init run through
   std::vector<std::unique_ptr<RowPlan>> plans;
-  // PRE_WRITE whose rows are one channel's cache rows [direct_lo, +rows) in
-  // order (op row j -> cache row direct_lo + j, no repeats): after
-  // StartIterations, when the clock's update ops write every oplog row once,
-  // PreUpdate hands out that oplog slice itself and Update moves no rows
-  // (decide_fused_init; DESIGN §4 "direct oplog").
+  // READ / PRE_WRITE whose rows are one channel's cache rows [direct_lo,
+  // +rows) in order (op row j -> cache row direct_lo + j, no repeats).
+  // PRE_WRITE: after StartIterations, when the clock's update ops write every
+  // oplog row once, PreUpdate hands out that oplog slice itself and Update
+  // moves no rows (decide_fused_init; DESIGN §4 "direct oplog").  READ, with
+  // GEEPS_DIRECT_READ=1: when the rows also lie in one server's shard and that
+  // shard is read in place, Read hands out the slice of the server's master
+  // version and pins the version until PostRead (DESIGN §4 "direct read").
   int direct_channel = -1;
   size_t direct_lo = 0;
   bool direct = false;                 // decided: this op writes its oplog slice in place
   bool direct_now = false;             // the outstanding PreUpdate handed out the slice
+  int pin_server = -1, pin_version = -1;  // the outstanding direct Read's pinned version
   DeviceArray<float> buffer;           // READ / PRE_WRITE op buffer
   float *local_ptr = nullptr;          // local READ: GPU-resident storage
   bool in_use = false;
@@ -107,6 +111,11 @@ struct ParamCache {
   std::vector<int> live_ver;
   std::vector<const float *> live_ptr;
   std::vector<std::map<int, void *>> server_versions;  // [server]: IPC-mapped versions
+  // Direct Reads (GEEPS_DIRECT_READ=1) hand out a slice of a live master version:
+  // pins[s][v] counts the outstanding ones; a pinned version that a refresh
+  // replaces waits in deferred[s] and goes back to the server at the last PostRead.
+  std::vector<std::map<int, int>> pins;
+  std::vector<std::set<int>> deferred;
   gp_row_segments segs{};
   bool segmented = false;
 };
@@ -116,6 +125,8 @@ struct ClientStats {
   uint64_t nr_refresh_in_place = 0;  // refreshes read in place from the server's master version
   uint64_t nr_refresh_staged = 0;    // same-node refreshes peer-copied into the cache (staged)
   uint64_t nr_update_direct = 0;     // Updates whose rows the app wrote into the oplog in place
+  uint64_t nr_read_direct = 0;       // Reads that handed out a master version's rows in place
+  uint64_t nr_read_pin_deferred = 0; // replaced versions a direct Read kept until its PostRead
   uint64_t rows_updated = 0, rows_read = 0, bytes_pushed_remote = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
@@ -249,6 +260,8 @@ class ClientLib {
   bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r, bool *held);
   void send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts);
   void ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a);
+  // hand master version v of server s's shard of `table` back to that server
+  void give_back(Channel &ch, uint32_t s, uint32_t table, int v);
 
   const uint32_t process_id_;
   const GeePsConfig config_;
@@ -261,6 +274,7 @@ class ClientLib {
   // on one GPU): GEEPS_STAGE_PEER_UPDATES (buckets), GEEPS_STAGE_PEER_REFRESH
   int stage_updates_mode_ = -1;
   bool direct_oplog_ = true;  // GEEPS_DIRECT_OPLOG=0 turns the direct oplog off
+  bool direct_read_ = false;  // GEEPS_DIRECT_READ=1: Read buffers are read-only (§4)
   int stage_refresh_mode_ = -1;
   int reader_delay_us_ = 0;   // GEEPS_TEST_READER_DELAY_US (test hook)
   std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)

@@ -181,7 +181,13 @@ int main(int argc, char **argv) {
   ps->VirtualClock();
   ps->FinishVirtualIteration();
 
-  std::vector<float> host(n), got(n);
+  std::vector<float> host(n), got(n), again;
+  std::vector<RowData *> rbufs(L, nullptr);
+  // GEEPS_TEST_REREAD=1: each Read buffer is read again just before its
+  // PostRead and must not have changed (a direct Read's master version stays
+  // pinned while refreshes arrive).
+  const bool reread = std::getenv("GEEPS_TEST_REREAD") != nullptr;
+  int bad = 0;
   // PreUpdate -> fill on the device -> [PostRead] -> Update, in declared order.
   auto push = [&](int c, bool post_read) {
     for (size_t l = L; l-- > 0;) {
@@ -193,6 +199,14 @@ int main(int argc, char **argv) {
           host[e0 + j * ROW_DATA_SIZE + v] =
               delta(pid, c, e0 + upd_row[l][j] * ROW_DATA_SIZE + v, fl);
       HCK(hipMemcpy(buf, host.data() + e0, ne * 4, hipMemcpyHostToDevice));
+      if (post_read && reread) {
+        again.resize(ne);
+        HCK(hipMemcpy(again.data(), rbufs[l], ne * 4, hipMemcpyDeviceToHost));
+        if (std::memcmp(again.data(), got.data() + e0, ne * 4) != 0 && bad < 5) {
+          std::fprintf(stderr, "p%d clock %d layer %zu: Read buffer changed before PostRead\n", pid, c, l);
+          ++bad;
+        }
+      }
       if (post_read) ps->PostRead(h_post[l]);
       ps->Update(h_upd[l]);
     }
@@ -218,7 +232,6 @@ int main(int argc, char **argv) {
   ps->Clock();
   ps->StartIterations();
 
-  int bad = 0;
   std::vector<float> lbuf(local_rows * ROW_DATA_SIZE);
   const char *jit = std::getenv("GEEPS_TEST_JITTER_US");
   const unsigned jitter_us = jit ? (unsigned)std::strtoul(jit, nullptr, 10) : 0;
@@ -249,6 +262,7 @@ int main(int argc, char **argv) {
       RowData *rbuf = nullptr;
       jitter();
       ps->Read(h_read[l], &rbuf);
+      rbufs[l] = rbuf;
       const size_t e0 = first[l] * ROW_DATA_SIZE, ne = layer_rows[l] * ROW_DATA_SIZE;
       HCK(hipMemcpy(got.data() + e0, rbuf, ne * 4, hipMemcpyDeviceToHost));
     }

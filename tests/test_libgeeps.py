@@ -400,6 +400,45 @@ def test_direct_oplog(dev, P, mode, direct):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P,mode,slack,channels,spec,delay_us", [
+    (1, "float", 0, 1, "2000", 0),
+    (2, "int", 0, 1, "700,5,900,395", 0),
+    (3, "int", 1, 2, "300,500,200,700,300", 0),
+    (2, "int", 2, 1, "700,5,900,395", 15000),
+])
+def test_direct_read(dev, P, mode, slack, channels, spec, delay_us):
+    """Direct read (GEEPS_DIRECT_READ=1): a Read whose rows are one
+    server's shard rows in order, with that shard read in place, hands out the
+    master version's own rows and pins the version until PostRead.  Blobs that
+    straddle two shards or channels still gather.  Every Read is checked (bit-
+    exact at one process), and each Read buffer is read again just before its
+    PostRead: a refresh arriving in between must not change it (the replaced
+    version is given back at PostRead instead, nr_read_pin_deferred).  The last
+    case adds a reader that takes refreshes 15 ms late under slack 2, so the
+    server runs at its clients + 2 version cap with direct Reads pinning."""
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    base = _ports(P, channels)
+    extra = {"GEEPS_DIRECT_READ": "1", "GEEPS_TEST_REREAD": "1"}
+    if delay_us:
+        extra["GEEPS_TEST_READER_DELAY_US"] = str(delay_us)
+    env = _env("ipc", jitter_us=300 if P > 1 else 0, extra=extra)
+    rows = sum(int(x) for x in spec.split(","))
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), "12", str(slack), str(channels),
+                     "0", mode, spec], env) for p in range(P)]
+    st = _stats(_collect(procs, 300))
+    direct = [s["client"]["nr_read_direct"] for s in st]
+    reads = [s["client"]["nr_read"] for s in st]
+    print("direct reads:", direct, "of", reads, "deferred:",
+          [s["client"]["nr_read_pin_deferred"] for s in st])
+    assert all(d > 0 for d in direct)
+    if P == 1:
+        assert direct == reads  # one shard, one channel: every Read is direct
+    else:
+        assert all(d < r for d, r in zip(direct, reads))  # straddling blobs gather
+
+
+@pytest.mark.gpu
 def test_one_process_per_gpu(dev):
     """One process per GPU (process p on device p % count), as on an 8-GPU
     node: peers' buckets cross xGMI by the staged peer copy and refreshes are
@@ -460,8 +499,8 @@ _STRESS_CASES = int(os.environ.get("GEEPS_STRESS_CASES", "4"))
 def test_randomized_configurations(dev, case):
     """Seeded random mixes of what the other tests vary one at a time:
     processes, slack, channels, tables, read-my-writes, a local-access op,
-    transport, layer shapes, shuffled update rows, jitter, the direct oplog and
-    both peer-staging switches.  Every Read is checked by the app (exact at
+    transport, layer shapes, shuffled update rows, jitter, the direct oplog,
+    both peer-staging switches and direct reads.  Every Read is checked by the app (exact at
     BSP, within the SSP bounds otherwise)."""
     import random
     if not os.path.exists(SUM_APP):
@@ -488,6 +527,8 @@ def test_randomized_configurations(dev, case):
         if v:
             extra[k] = v
     transport = rng.choice(["ipc", "ipc", "tcp"])
+    if rng.random() < 0.5:  # direct reads, each buffer re-read before its PostRead
+        extra.update(GEEPS_DIRECT_READ="1", GEEPS_TEST_REREAD="1")
     desc = dict(P=P, slack=slack, channels=channels, rmw=rmw, tables=tables, local=local, mode=mode,
                 layers=layers, transport=transport, **extra)
     print("config", desc)
