@@ -9,8 +9,12 @@
 // push of each server's slice (zero-copy in process, D2H + TCP otherwise), the
 // server's bucket sum into its master shard, the refresh of every client's
 // param cache, and the gather into the Read buffer.  Prints one JSON line.
+// CLOCK_BENCH_READ_PER_SHARD=1 declares one Read op per server shard instead
+// (as per-blob ops mostly fall within one shard), which direct reads
+// (GEEPS_DIRECT_READ=1) can hand out in place.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -44,9 +48,18 @@ int main(int argc, char **argv) {
   GeePs *ps = new GeePs(pid, cfg);
   std::vector<size_t> ids(rows);
   for (size_t r = 0; r < rows; ++r) ids[r] = r;
-  const int hr = ps->VirtualRead(0, ids, slack);
+  // the reference partition of the table's rows over the servers
+  // (clientlib-viter.cpp:674-682): P contiguous ranges
+  const bool per_shard = std::getenv("CLOCK_BENCH_READ_PER_SHARD") != nullptr;
+  std::vector<int> hr, hpr;
+  for (int s = 0; s < (per_shard ? P : 1); ++s) {
+    const size_t div = rows / P, res = rows % P;
+    const size_t lo = per_shard ? div * s + std::min<size_t>(s, res) : 0;
+    const size_t hi = per_shard ? lo + div + ((size_t)s < res ? 1 : 0) : rows;
+    hr.push_back(ps->VirtualRead(0, std::vector<size_t>(ids.begin() + lo, ids.begin() + hi), slack));
+  }
   const int hp = ps->VirtualPreUpdate(0, ids);
-  const int hpr = ps->VirtualPostRead(hr);
+  for (int h : hr) hpr.push_back(ps->VirtualPostRead(h));
   const int hu = ps->VirtualUpdate(hp);
   ps->VirtualClock();
   ps->FinishVirtualIteration();
@@ -63,18 +76,18 @@ int main(int argc, char **argv) {
   for (int c = 0; c < warmup + clocks; ++c) {
     if (c == warmup) t0 = clk::now();
     RowData *rb = nullptr;
-    ps->Read(hr, &rb);
+    for (int h : hr) ps->Read(h, &rb);
     ps->PreUpdate(hp, &ub);
     // the app's "gradient": 0.5 everywhere, written on the device
     HCK(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(ub), 0x3f000000, rows * ROW_DATA_SIZE));
     HCK(hipDeviceSynchronize());
-    ps->PostRead(hpr);
+    for (int h : hpr) ps->PostRead(h);
     ps->Update(hu);
     ps->Clock();
   }
   // the last Read waits for the last clock's refresh: include it
   RowData *rb = nullptr;
-  ps->Read(hr, &rb);
+  for (int h : hr) ps->Read(h, &rb);
   const double s = std::chrono::duration<double>(clk::now() - t0).count();
   float probe = 0;
   HCK(hipMemcpy(&probe, rb, 4, hipMemcpyDeviceToHost));
