@@ -1406,7 +1406,9 @@ int launch_gather_planned(float *y, const float *x, const gp_row_segments *xs,
 //     call with the same index -- same pointer, size, offsets, row size and
 //     limit, and entry for entry the same content, which the scan checks
 //     against the copy -- builds the destination-sorted residual (a hipCUB
-//     radix sort, gp_sort.hip) and runs it, and later calls run it at once.
+//     radix sort, gp_sort.hip) and runs it.  Later calls skip the scan: they
+//     only compare the index with the copy (index_compare_kernel) and run the
+//     cached dense runs and sorted residual.
 //     An index that changes every call costs one copy per call, no sort.  Visiting rows in destination order is bit-neutral under
 //     the call's precondition (distinct destinations).
 // Calls below g_analyze_min_bytes (gp_set_unplanned_min_bytes) skip all this.
@@ -1550,6 +1552,30 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
   }
 }
 
+// A planned index seen again: only whether every entry still equals the cached
+// copy (32 B read per entry, no tile analysis).  Each thread holds 4 entries'
+// loads in flight; one global atomic per wave that saw a difference.
+constexpr int kCmpPerThread = 4;
+__global__ __launch_bounds__(kBlock) void index_compare_kernel(const gp_double_index *__restrict__ idx,
+                                                               const gp_double_index *__restrict__ cached, size_t n,
+                                                               ScanHeader *__restrict__ hdr) {
+  const size_t step = (size_t)gridDim.x * kBlock * kCmpPerThread;
+  bool differs = false;
+  for (size_t base = (size_t)blockIdx.x * kBlock * kCmpPerThread + threadIdx.x; base < n; base += step) {
+    gp_double_index a[kCmpPerThread], b[kCmpPerThread];
+#pragma unroll
+    for (int k = 0; k < kCmpPerThread; ++k) {  // clamped, unconditional: all loads in flight
+      const size_t e = base + (size_t)k * kBlock;
+      const size_t ec = e < n ? e : n - 1;
+      a[k] = idx[ec];
+      b[k] = cached[ec];
+    }
+#pragma unroll
+    for (int k = 0; k < kCmpPerThread; ++k) differs |= (a[k].id0 != b[k].id0) | (a[k].id1 != b[k].id1);
+  }
+  if (__any(differs) && (threadIdx.x & 63) == 0) atomicAdd(&hdr->mismatches, 1u);
+}
+
 // Residual rows of a call: up to kMaxDeviceRuns + 1 entry ranges, passed by
 // value; `pre[i]` = rows in ranges before i.
 struct EntryRanges {
@@ -1663,6 +1689,10 @@ struct DevBuf {
   DevBuf &operator=(const DevBuf &) = delete;
 };
 
+struct DevRun {
+  uint64_t e0, rows, from, to;  // first entry, rows, endpoints of the first entry
+};
+
 // An entry is immutable once in the cache.  The first call with an index
 // leaves a copy-only entry (`sorted` null); the next call with the same
 // content builds the destination-sorted residual into a new entry that
@@ -1675,6 +1705,7 @@ struct CachedPlan {
   // the first call (the allocation overlaps that call's kernels)
   std::shared_ptr<DevBuf> spare;
   size_t resid = 0;
+  std::vector<DevRun> runs;    // with `sorted`: the index's dense runs (the rest is the residual)
   hipEvent_t ready = nullptr;  // recorded once copy (and sorted) are built, on the building stream
   uint64_t last_use = 0;
   size_t bytes = 0;
@@ -1738,10 +1769,6 @@ void cache_insert(std::shared_ptr<CachedPlan> p) {
   }
 }
 
-struct DevRun {
-  uint64_t e0, rows, from, to;  // first entry, rows, endpoints of the first entry
-};
-
 // A copy-only entry for an index seen for the first time (its copy, taken on
 // stream s after the call's own launches): what the next call's scan compares.
 int cache_first_sighting(const PlanKey &key, const gp_double_index *idx, size_t resid, hipStream_t s) {
@@ -1766,13 +1793,14 @@ int cache_first_sighting(const PlanKey &key, const gp_double_index *idx, size_t 
 // shares `seen`'s copy; returned for this call to run.
 template <int OP>
 int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_double_index *idx,
-                          const EntryRanges &rr, uint64_t max_dst, hipStream_t s,
-                          std::shared_ptr<CachedPlan> *built) {
+                          const EntryRanges &rr, const std::vector<DevRun> &runs, uint64_t max_dst,
+                          hipStream_t s, std::shared_ptr<CachedPlan> *built) {
   const PlanKey &key = seen->key;
   const size_t resid = rr.pre[rr.count];
   auto p = std::make_shared<CachedPlan>();
   p->key = key;
   p->resid = resid;
+  p->runs = runs;
   p->bytes = (key.n + resid) * sizeof(gp_double_index);
   p->copy = seen->copy;
   int rc = GP_OK;
@@ -1826,7 +1854,45 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
       if (p) (void)hipFreeAsync(p, s);
     }
   } free_ws{ws, s};
+  auto launch_runs = [&](const std::vector<DevRun> &rs) {
+    for (const DevRun &r : rs) {
+      BucketPtrs b = {};
+      b.p[0] = x + r.from * W;
+      float *yr = y + r.to * W;
+      int rc;
+      if constexpr (OP == kAddFrom)
+        rc = launch_bucket_sum_nb<1>(yr, yr, b, r.rows * W, s);
+      else if constexpr (OP == kInitFrom)
+        rc = launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s);
+      else
+        rc = launch_bucket_sum_nb<0>(yr, x + r.from * W, BucketPtrs{}, r.rows * W, s);
+      if (rc != GP_OK) return rc;
+    }
+    return (int)GP_OK;
+  };
   GP_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(ScanHeader), s));
+  if (cached && cached->sorted) {
+    // A planned index seen again: compare it with the copy (no tile analysis);
+    // the same content runs the cached dense runs and sorted residual at once.
+    const size_t per_block = (size_t)kBlock * kCmpPerThread;
+    const size_t grid = std::max<size_t>(1, std::min((n + per_block - 1) / per_block, (size_t)num_cus() * 8));
+    hipLaunchKernelGGL(index_compare_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, cached->copy_ptr(), n,
+                       reinterpret_cast<ScanHeader *>(ws));
+    GP_HIP_TRY(hipGetLastError());
+    char *h = static_cast<char *>(g_scan_landing.get(sizeof(ScanHeader)));
+    if (!h) return set_error(GP_ERR_HIP, "pinned scan buffer");
+    GP_HIP_TRY(hipMemcpyAsync(h, ws, sizeof(ScanHeader), hipMemcpyDeviceToHost, s));
+    GP_HIP_TRY(hipStreamSynchronize(s));
+    if (reinterpret_cast<const ScanHeader *>(h)->mismatches == 0) {
+      const int rc = launch_runs(cached->runs);
+      if (rc != GP_OK) return rc;
+      return launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
+                               /*sorted=*/true);
+    }
+    cache_drop(cached);  // the same pointer now holds another index: plan it afresh
+    cached.reset();
+    GP_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(ScanHeader), s));
+  }
   {
     const size_t grid = std::max<size_t>(1, std::min(groups, (size_t)num_cus() * 8));
     if (cached)
@@ -1886,19 +1952,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
       std::sort(runs.begin(), runs.end(), [](const DevRun &a, const DevRun &b) { return a.e0 < b.e0; });
     }
   }
-  for (const DevRun &r : runs) {
-    BucketPtrs b = {};
-    b.p[0] = x + r.from * W;
-    float *yr = y + r.to * W;
-    int rc;
-    if constexpr (OP == kAddFrom)
-      rc = launch_bucket_sum_nb<1>(yr, yr, b, r.rows * W, s);
-    else if constexpr (OP == kInitFrom)
-      rc = launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s);
-    else
-      rc = launch_bucket_sum_nb<0>(yr, x + r.from * W, BucketPtrs{}, r.rows * W, s);
-    if (rc != GP_OK) return rc;
-  }
+  if (const int rc = launch_runs(runs); rc != GP_OK) return rc;
   // the residual: entry ranges between the runs
   EntryRanges rr = {};
   {
@@ -1940,7 +1994,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
                         max_dst < (1ull << 32) && n < (1ull << 32);
   if (sortable && cached && !cached->sorted && cached->resid == resid) {
     std::shared_ptr<CachedPlan> built;
-    const int rc = cache_second_sighting<OP>(cached, idx, rr, max_dst, s, &built);
+    const int rc = cache_second_sighting<OP>(cached, idx, rr, runs, max_dst, s, &built);
     if (rc != GP_OK) return rc;
     return launch_row_op<OP>(y, x, built->sorted_ptr(), resid, gp_double_index{0, 0}, W, limit, s,
                              /*sorted=*/true);
