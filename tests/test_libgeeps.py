@@ -288,21 +288,28 @@ def test_config4_inception_cifar_two_workers(dev, transport):
 
 @pytest.mark.gpu
 @pytest.mark.slow
-@pytest.mark.parametrize("transport", ["ipc", "tcp"])
+@pytest.mark.parametrize("transport", ["ipc", "tcp", "ipc+direct_read"])
 def test_config5_alexnet_8_workers_8_shards_staleness_1(dev, transport):
+    """configs[4]'s shape: per-blob ops over 8 shards, slack 1.  The third case
+    adds direct reads (most blobs lie in one shard), each Read buffer re-read
+    before its PostRead."""
     rows, spec = _layer_spec(ALEXNET_BLOBS)
-    _run_app_layers(8, rows, spec, clocks=4, slack=1, timeout=900, transport=transport)
+    extra = None
+    if transport == "ipc+direct_read":
+        transport, extra = "ipc", {"GEEPS_DIRECT_READ": "1", "GEEPS_TEST_REREAD": "1"}
+    _run_app_layers(8, rows, spec, clocks=4, slack=1, timeout=900, transport=transport, extra_env=extra)
 
 
 def _run_app_layers(P, rows, spec, clocks, slack, timeout=600, transport="ipc", tables=1,
-                    local=0, out_dir=""):
+                    local=0, out_dir="", extra_env=None):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(P, 1)
     procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
-                     "1", "0", "int", spec, str(tables), str(local), out_dir], _env(transport))
+                     "1", "0", "int", spec, str(tables), str(local), out_dir],
+                    _env(transport, extra=extra_env))
              for p in range(P)]
-    _collect(procs, timeout)
+    return _collect(procs, timeout)
 
 
 @pytest.mark.gpu
