@@ -125,7 +125,9 @@ def parse(argv=None):
     p.add_argument("--no-per-rank", action="store_true",
                    help="skip the one-GPU emulation of the N-GPU runs' per-rank work")
     p.add_argument("--no-e2e", action="store_true",
-                   help="skip the libgeeps end-to-end clock leg")
+                   help="skip the libgeeps end-to-end clock legs")
+    p.add_argument("--no-multi-e2e", action="store_true",
+                   help="at N > 1, skip the libgeeps one-process-per-GPU leg")
     p.add_argument("--no-hbm-probe", action="store_true")
     p.add_argument("--no-separate-alloc", action="store_true",
                    help="skip timing the headline sum on separately allocated buffers")
@@ -705,6 +707,96 @@ def measure_traffic(rows, W, clients, kernel_id, timeout_s=150):
 ALEXNET_ROWS = 476292  # tests/test_libgeeps.py ALEXNET_BLOBS, each blob padded to 128-float rows
 
 
+def _clock_bench_module():
+    import importlib.util
+    path = os.path.join(REPO, "scripts", "run_clock_bench.py")
+    spec = importlib.util.spec_from_file_location("run_clock_bench", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# The two cross-GPU data paths of libgeeps: "staged" =
+# a peer's oplog slice and a peer's refreshed shard each peer-copied over xGMI
+# into local HBM once (the default across GPUs); "in_place" = the server's sum
+# and the client's Reads load the peer's HBM directly over xGMI.
+PEER_PATHS = {"staged": {"GEEPS_STAGE_PEER_UPDATES": "1", "GEEPS_STAGE_PEER_REFRESH": "1"},
+              "in_place": {"GEEPS_STAGE_PEER_UPDATES": "0", "GEEPS_STAGE_PEER_REFRESH": "0"}}
+
+
+def libgeeps_multi_gpu_leg(n_gpus, rows, W, clocks=5, warmup=2, alex_clocks=10, gpus_seen=None,
+                           tables=("1Mx1024", "alexnet")):
+    """configs[2] / configs[4] through the drop-in, one process per GPU: the
+    clock bench (scripts/apps/geeps_clock_bench.cpp through include/geeps.hpp)
+    as n_gpus worker + tablet-server processes, process p on GPU p % count
+    (GEEPS_TEST_SPREAD_DEVICES=1), same-node IPC transport, for both
+    cross-GPU data paths (PEER_PATHS), on two tables:
+      1Mx1024  the bench's rows x W fp32 table as RowData rows, BSP
+      alexnet  the AlexNet-sized table (configs[4]), staleness bound 1
+    Each worker checks its last Read over every element (read_ok).  Rank 0 of
+    `bench.py --gpus N` runs this before any rank opens a GPU; on a one-GPU box
+    the same code runs every process on GPU 0 (a rehearsal: both switches
+    forced, so the staged copies run as peer copies within one GPU)."""
+    mod = _clock_bench_module()
+    if not os.path.exists(mod.BIN):
+        return {"skipped": f"{os.path.relpath(mod.BIN, REPO)} not built (__graft_entry__.build())"}
+    rd_rows = rows * W // 128
+    gpus = gpus_seen if gpus_seen is not None else torch.cuda.device_count()
+    out = {"app": "scripts/apps/geeps_clock_bench.cpp", "processes": n_gpus, "gpus_seen": gpus,
+           "one_process_per_gpu": gpus >= n_gpus, "transport": "ipc (same node)", "clocks": clocks,
+           "warmup": warmup}
+    base_env = {"GEEPS_TEST_SPREAD_DEVICES": "1"}
+    if gpus >= n_gpus:  # one process per GPU: the default hardware queues
+        base_env["CLOCK_BENCH_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES", "4")
+    for table, nrows, slack, ck in (("1Mx1024", rd_rows, 0, clocks), ("alexnet", ALEXNET_ROWS, 1, alex_clocks)):
+        if table not in tables:
+            continue
+        for path, env in PEER_PATHS.items():
+            key = f"{table}_{path}"
+            try:
+                r = mod.run(n_gpus, nrows, ck, warmup, slack, "ipc", timeout=300,
+                            extra_env=dict(base_env, **env))
+            except Exception as exc:  # report, keep the other cases
+                out[key] = {"error": f"{type(exc).__name__}: {str(exc)[-800:]}"}
+                continue
+            out[key] = {"rows": nrows, "slack": slack, "ms_per_clock": r["ms_per_clock_max"],
+                        "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],
+                        "read_checked": r["read_checked"], "devices": r["devices"],
+                        "nr_peer_staged": r.get("nr_peer_staged"),
+                        "nr_refresh_staged": r.get("nr_refresh_staged"),
+                        "nr_refresh_in_place": r.get("nr_refresh_in_place")}
+    return out
+
+
+def pre_gpu_multi_leg(args, backend):
+    """At N > 1 (one rank per GPU under torch.distributed.run): rank 0 runs
+    libgeeps_multi_gpu_leg across the N GPUs while the other ranks wait on a
+    file store WITHOUT touching a GPU; nothing of the RCCL harness exists yet.
+    Returns rank 0's result (None elsewhere and at N = 1)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 or backend != "nccl" or args.no_e2e or args.no_multi_e2e:
+        return None
+    import datetime
+    import tempfile
+    rank = int(os.environ.get("RANK", "0"))
+    # every rank of one torch.distributed.run has the same parent (the agent)
+    path = os.path.join(tempfile.gettempdir(),
+                        f"geeps_bench_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}")
+    store = dist.FileStore(path, world)
+    store.set_timeout(datetime.timedelta(seconds=1500))
+    res = None
+    if rank == 0:
+        log(f"[rank 0] libgeeps one-process-per-GPU leg over {world} GPUs (before any rank opens a GPU)")
+        try:
+            res = libgeeps_multi_gpu_leg(world, args.rows, args.width)
+        except Exception as exc:
+            res = {"error": f"{type(exc).__name__}: {str(exc)[-500:]}"}
+        store.set("libgeeps_leg_done", "1")
+    else:
+        store.wait(["libgeeps_leg_done"])
+    return res
+
+
 def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
     """The drop-in path end to end: scripts/apps/geeps_clock_bench (built by
     __graft_entry__.build() against libgeeps.so and include/geeps.hpp, as an
@@ -716,11 +808,7 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
     the server's bucket sum, the zero-copy refresh), through the public API.  P = 2 is configs[1]'s
     2 loopback clients; every worker updates every row each clock.
     delta_GBps = P * table bytes / the slowest worker's ms per clock."""
-    import importlib.util
-    path = os.path.join(REPO, "scripts", "run_clock_bench.py")
-    spec = importlib.util.spec_from_file_location("run_clock_bench", path)
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
+    mod = _clock_bench_module()
     if not os.path.exists(mod.BIN):
         return {"skipped": f"{os.path.relpath(mod.BIN, REPO)} not built (__graft_entry__.build())"}
     rd_rows = rows * W // 128
@@ -870,6 +958,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
             e2e_first = libgeeps_leg(args.rows, args.width)
         except Exception as exc:  # a side leg: report it, keep the headline line
             e2e_first = {"error": f"{type(exc).__name__}: {str(exc)[-500:]}"}
+    multi_e2e = pre_gpu_multi_leg(args, backend)
     rank, world, dev = init_dist(args.gpus, backend)
     import geeps_amd
     from geeps_amd.shard import ShardedReducer
@@ -1045,8 +1134,40 @@ def main(argv=None, backend="nccl", apply_fn=None):
             line["roofline"]["same_box_model_ms"] = round(mm, 4)
             line["roofline"]["frac_of_same_box_model"] = round(mm / avg_kernel_ms_max, 4)
             line["hbm_probe"] = probe
+        # scalar copies of nested facts: the driver's parsed record keeps a
+        # nested object's scalar fields only
+        rl = line["roofline"]
+        if traffic:
+            rl["traffic_over_algorithmic"] = round(traffic["bytes_per_launch"] /
+                                                   (algo_bytes * share / launches), 5)
+            rl["traffic_measured_in_run"] = bool(pmc)
+        if cpu and "all_cores" in cpu:
+            cpu["all_cores_GBps"] = round(cpu["all_cores"]["value"], 2)
+            cpu["all_cores_threads"] = cpu["all_cores"]["cores"]
+            cpu["all_cores_from"] = cpu["all_cores"]["threads_from"]
         if sep_alloc:
             line["roofline"]["separate_alloc"] = sep_alloc
+            if "frac" in sep_alloc:
+                rl["separate_alloc_frac"] = sep_alloc["frac"]
+        if rowops_res:
+            for kind in ("random", "identity"):
+                for leg in ("scatter_add", "scatter_add_planned", "scatter_init", "scatter_init_planned",
+                            "gather", "gather_planned"):
+                    v = rowops_res.get(kind, {}).get(leg)
+                    if v and "frac" in v:
+                        rl[f"rowops_{kind}_{leg}_frac"] = v["frac"]
+        if config2:
+            rl["config2_frac"] = config2["frac"]
+        if e2e:
+            for k, v in e2e.items():
+                if isinstance(v, dict) and "ms_per_clock" in v:
+                    rl[f"libgeeps_{k}_ms_per_clock"] = v["ms_per_clock"]
+        if multi_e2e:
+            line["libgeeps_multi_gpu"] = multi_e2e
+            for k, v in multi_e2e.items():
+                if isinstance(v, dict) and "ms_per_clock" in v:
+                    rl[f"libgeeps_{k}_ms_per_clock"] = v["ms_per_clock"]
+                    rl[f"libgeeps_{k}_read_ok"] = v["read_ok"]
         if config2:
             line["config2"] = config2
         if per_rank:

@@ -54,6 +54,7 @@ std::string ClientStats::to_json() const {
     << ", \"nr_refresh\": " << nr_refresh << ", \"nr_refresh_in_place\": " << nr_refresh_in_place
     << ", \"nr_refresh_staged\": " << nr_refresh_staged << ", \"nr_update_direct\": " << nr_update_direct
     << ", \"nr_read_direct\": " << nr_read_direct << ", \"nr_read_pin_deferred\": " << nr_read_pin_deferred
+    << ", \"nr_read_direct_capped\": " << nr_read_direct_capped
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -597,10 +598,13 @@ void ClientLib::finish_virtual_iteration() {
         if (pc.num_rows) GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.stream->get()));
       }
       planned += pc.num_rows * kRowBytes * ((copies ? 1 : 0) + entries);
-      // the server's staging buckets for peers' slices: at most one per
-      // pending bucket (the queue is applied at kMaxPendingBuckets)
+      // the server's staging buckets: one per pending bucket of a peer on
+      // another GPU (its slice peer-copied in) or of a remote client (its
+      // socket rows copied in), at most kMaxPendingBuckets (the queue is
+      // applied when it reaches that many)
       size_t staged_peers = 0;
-      for (uint32_t s = 0; s < num_processes_; ++s) staged_peers += ch.stage_from[s] ? 1 : 0;
+      for (uint32_t s = 0; s < num_processes_; ++s)
+        staged_peers += (ch.stage_from[s] || (s != process_id_ && !ipc_to(s))) ? 1 : 0;
       pc.server_row_start.resize(num_processes_);
       pc.server_num_rows.resize(num_processes_);
       const size_t div = pc.num_rows / num_processes_, res = pc.num_rows % num_processes_;
@@ -608,14 +612,18 @@ void ClientLib::finish_virtual_iteration() {
         pc.server_row_start[i] = div * i + std::min(i, res);
         pc.server_num_rows[i] = div + (i < res ? 1 : 0);
       }
+      // + this process's server's master versions of the shard: two (the
+      // current one and the next, built beside it while clients read it in
+      // place); a lagging reader can make it up to clients + 2 (server.hpp)
       planned += pc.server_num_rows[process_id_] * kRowBytes *
-                 std::min<size_t>(staged_peers, TabletServer::kMaxPendingBuckets);
+                 (std::min<size_t>(staged_peers, TabletServer::kMaxPendingBuckets) + 2);
       pc.per_server_data_age.assign(num_processes_, INITIAL_DATA_AGE);
       pc.live_ver.assign(num_processes_, -1);
       pc.live_ptr.assign(num_processes_, nullptr);
       pc.server_versions.resize(num_processes_);
       pc.pins.assign(num_processes_, {});
       pc.deferred.assign(num_processes_, {});
+      pc.read_events.assign(num_processes_, {});
       pc.server_clock.assign(num_processes_, INITIAL_DATA_AGE);
     }
     ch.stream->sync();
@@ -649,11 +657,17 @@ void ClientLib::finish_virtual_iteration() {
   GP_CALL(gp_device_synchronize());
   decide_fused_init();
   if (planned > config_.gpu_memory_capacity) {
+    // The reference places what does not fit in CPU memory and accumulates it
+    // there (update_batch_cpu, clientlib-viter.cpp:492-611; clientlib-data.cpp:
+    // 398-434).  libgeeps has no CPU tier: every row lives in HBM (288 GB per
+    // MI355X), so past the capacity it warns, or fails at mm_warning_level >= 2.
     std::ostringstream o;
     o << "planned HBM use " << planned << " B exceeds gpu_memory_capacity "
-      << config_.gpu_memory_capacity << " B";
+      << config_.gpu_memory_capacity
+      << " B; libgeeps keeps every row in HBM (no CPU param-cache tier: the reference's "
+         "CPU placement, clientlib-viter.cpp:492-611, is not built)";
     GP_CHECK_MSG(config_.mm_warning_level < 2, o.str());
-    std::cerr << "libgeeps WARNING: " << o.str() << " (all data kept in HBM)\n";
+    std::cerr << "libgeeps WARNING: " << o.str() << "\n";
   }
 }
 
@@ -819,6 +833,7 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
   const iter_t need = iteration_ - op.slack - 1;
   double waited = 0;
   float *direct = nullptr;
+  bool capped = false;
   for (auto &chp : channels_) {
     Channel &ch = *chp;
     ParamCache &pc = ch.tables[op.table_id];
@@ -833,7 +848,10 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
       }
     }
     waited += now_s() - w0;
-    if (direct_read_ && started_ && op.direct_channel == (int)ch.id) {
+    // (an op whose last row straddles num_vals_limit gathers: its buffer holds
+    // zeros past the limit, which the master's rows do not)
+    if (direct_read_ && started_ && op.direct_channel == (int)ch.id &&
+        op.num_vals_limit >= op.rows.size() * ROW_DATA_SIZE) {
       // Direct read: the op's rows are one server's shard rows in order and
       // that shard is read in place, so the buffer is the master version's own
       // rows.  The version stays pinned (not given back, so the server never
@@ -842,6 +860,13 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
       for (uint32_t s = 0; s < num_processes_; ++s) {
         const size_t first = pc.server_row_start[s];
         if (lo < first || lo + n > first + pc.server_num_rows[s] || pc.live_ver[s] < 0) continue;
+        // at most one deferred (replaced but pinned) version per server: a
+        // second one could leave the server's version cap waiting on this app
+        // thread's PostRead while the thread waits in a Read
+        if (!pc.deferred[s].empty() && !pc.pins[s].count(pc.live_ver[s])) {
+          capped = true;
+          break;
+        }
         direct = const_cast<float *>(pc.live_ptr[s]) + (lo - first) * ROW_DATA_SIZE;
         op.pin_server = (int)s;
         op.pin_version = pc.live_ver[s];
@@ -864,6 +889,7 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_read++;
   if (direct) stats_.nr_read_direct++;
+  if (capped) stats_.nr_read_direct_capped++;
   stats_.rows_read += op.rows.size();
   stats_.read_wait_time += waited;
   stats_.read_time += now_s() - t0;
@@ -882,23 +908,35 @@ void ClientLib::postread_batch(int handle) {
   if (pre.pin_server < 0) return;
   // A direct Read's pin ends: a version a refresh replaced meanwhile goes back
   // to its server once no direct Read pins it (outside ch.mu, as the reader
-  // threads give versions back).
+  // threads give versions back).  The app's device work that reads the buffer
+  // was queued before this call, typically on the null stream, and may still
+  // run: the event recorded here orders every later release of the version
+  // after it (the mirror of Update's app_written).
   Channel &ch = *channels_[pre.direct_channel];
   const uint32_t s = (uint32_t)pre.pin_server;
   const int v = pre.pin_version;
   pre.pin_server = pre.pin_version = -1;
+  if (!pre.read_done) pre.read_done = std::make_unique<Event>();
+  pre.read_done->record_default();
   bool back = false;
+  std::set<Event *> wait;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[pre.table_id];
     auto it = pc.pins[s].find(v);
     GP_CHECK(it != pc.pins[s].end() && it->second > 0);
+    pc.read_events[s][v].insert(pre.read_done.get());
     if (--it->second == 0) {
       pc.pins[s].erase(it);
       back = pc.deferred[s].erase(v) > 0;
+      if (back) {
+        wait.swap(pc.read_events[s][v]);
+        pc.read_events[s].erase(v);
+      }
     }
   }
   if (!back) return;
+  for (Event *e : wait) e->sync();
   give_back(ch, s, pre.table_id, v);
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_read_pin_deferred++;
@@ -1172,6 +1210,7 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
   const double t0 = now_s();
   Channel &ch = *channels_[channel];
   std::vector<int> released;
+  std::set<Event *> read_waits;
   bool in_place = false, staged = false;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
@@ -1203,12 +1242,19 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
       rebuild_segments(pc);
     }
     // a replaced version goes back now, or at the PostRead of the last direct
-    // Read pinning it
+    // Read pinning it; either way after the app's device work on the direct
+    // Reads' buffers (their PostRead events, waited on below)
     auto retire = [&](int v) {
-      if (pc.pins[server_id].count(v))
+      if (pc.pins[server_id].count(v)) {
         pc.deferred[server_id].insert(v);
-      else
-        released.push_back(v);
+        return;
+      }
+      auto ev = pc.read_events[server_id].find(v);
+      if (ev != pc.read_events[server_id].end()) {
+        read_waits.insert(ev->second.begin(), ev->second.end());
+        pc.read_events[server_id].erase(ev);
+      }
+      released.push_back(v);
     };
     if (num_rows) {
       const int prev = pc.live_ver[server_id];
@@ -1257,6 +1303,7 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
     pc.data_age = *std::min_element(pc.per_server_data_age.begin(), pc.per_server_data_age.end());
   }
   ch.cv.notify_all();
+  for (Event *e : read_waits) e->sync();  // before the caller gives `released` back
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_refresh++;
   if (in_place) stats_.nr_refresh_in_place++;

@@ -81,6 +81,10 @@ struct OpInfo {
   bool direct = false;                 // decided: this op writes its oplog slice in place
   bool direct_now = false;             // the outstanding PreUpdate handed out the slice
   int pin_server = -1, pin_version = -1;  // the outstanding direct Read's pinned version
+  // READ with direct reads: recorded on the null stream at each PostRead, so a
+  // version the app's queued device work still reads goes back to its server
+  // only after that work (ParamCache::read_events)
+  std::unique_ptr<Event> read_done;
   DeviceArray<float> buffer;           // READ / PRE_WRITE op buffer
   float *local_ptr = nullptr;          // local READ: GPU-resident storage
   bool in_use = false;
@@ -114,8 +118,17 @@ struct ParamCache {
   // Direct Reads (GEEPS_DIRECT_READ=1) hand out a slice of a live master version:
   // pins[s][v] counts the outstanding ones; a pinned version that a refresh
   // replaces waits in deferred[s] and goes back to the server at the last PostRead.
+  // At most one version per server is deferred at a time: a Read takes the
+  // direct path only if deferred[s] is empty or the live version is already
+  // pinned (else it gathers), which keeps the server's clients + 2 version cap
+  // live (server.hpp, "Versions").
   std::vector<std::map<int, int>> pins;
   std::vector<std::set<int>> deferred;
+  // read_events[s][v]: the PostRead events of the direct Reads that read
+  // version v; a release of v first waits for them (the app's device work on
+  // the buffer, queued before PostRead, must be done before the server may
+  // write the version again).
+  std::vector<std::map<int, std::set<Event *>>> read_events;
   gp_row_segments segs{};
   bool segmented = false;
 };
@@ -127,6 +140,7 @@ struct ClientStats {
   uint64_t nr_update_direct = 0;     // Updates whose rows the app wrote into the oplog in place
   uint64_t nr_read_direct = 0;       // Reads that handed out a master version's rows in place
   uint64_t nr_read_pin_deferred = 0; // replaced versions a direct Read kept until its PostRead
+  uint64_t nr_read_direct_capped = 0; // direct-eligible Reads that gathered: a version already deferred
   uint64_t rows_updated = 0, rows_read = 0, bytes_pushed_remote = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;

@@ -20,12 +20,15 @@ double now_s() {
 }
 
 // How long free_version waits with no release at all before it gives up:
-// GEEPS_VERSION_WAIT_S seconds (default 300).
+// GEEPS_VERSION_WAIT_S seconds; unset or 0 = wait forever with the 12-s
+// warnings, as the reference waits for its clients (a paused worker -- a
+// checkpoint, a long evaluation -- must not kill the job).  The
+// tests set a limit, so a stuck reader fails them with the holders matrix.
 double version_wait_limit_s() {
   static const double limit = [] {
     const char *v = std::getenv("GEEPS_VERSION_WAIT_S");
     const double d = v ? std::atof(v) : 0.0;
-    return d > 0 ? d : 300.0;
+    return d > 0 ? d : 0.0;
   }();
   return limit;
 }
@@ -278,11 +281,11 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
 
 // A version no client holds, other than the current one; a new one when
 // every version is held and fewer than clients + 2 exist; otherwise wait for
-// a release (see server.hpp: it comes from a reader thread catching up).  The
-// wait is bounded: every release restarts the clock, and after
-// version_wait_limit_s() with none the server fails loudly with the holders
-// matrix (a reader thread stuck or dead without a SHUTDOWN) instead of
-// stalling the channel forever.
+// a release (see server.hpp: it comes from a reader thread catching up, or
+// from a direct Read's PostRead).  With GEEPS_VERSION_WAIT_S set the wait is
+// bounded: every release restarts the clock, and after that long with none the
+// server fails loudly with the holders matrix (a reader thread stuck or dead
+// without a SHUTDOWN) instead of stalling the channel forever.
 int TabletServer::free_version(DataTable &t) {
   std::unique_lock<std::mutex> lk(hold_mu_);
   const double t0 = now_s();
@@ -311,7 +314,7 @@ int TabletServer::free_version(DataTable &t) {
     if (releases_ != seen) {
       seen = releases_;
       progress_t = now;
-    } else if (now - progress_t > version_wait_limit_s()) {
+    } else if (version_wait_limit_s() > 0 && now - progress_t > version_wait_limit_s()) {
       std::ostringstream o;
       o << "tablet server " << server_id_ << " channel " << channel_id_ << ": no master version "
         << "released for " << (now - progress_t) << " s (GEEPS_VERSION_WAIT_S); holders "

@@ -34,10 +34,18 @@
 // holding a version when the refresh is SENT, and gives the one before back
 // when its reader thread TAKES the next refresh, so under SSP a lagging reader
 // can hold several (up to slack + 2).  When every version is held and the cap
-// is reached, the apply waits for a release: releases arrive on the socket
+// is reached, the apply waits for a release.  Releases arrive on the socket
 // reader threads (or inside this thread for the in-process client, which
-// holds only the current version), never on this thread, and each is the
-// reader catching up on refreshes already sent, so the wait always ends.
+// holds only the current version), each the reader catching up on refreshes
+// already sent -- progress that needs nothing from this thread -- except for
+// direct Reads (GEEPS_DIRECT_READ=1): a version a direct Read pins when a
+// refresh replaces it goes back only at the app thread's PostRead, and that
+// thread may be blocked in a Read of another table waiting on this very
+// server.  A client therefore keeps at most ONE such deferred version per
+// (server, table) -- a Read that would pin a second one gathers instead
+// (client.cpp, read_batch).  Of the clients + 1 versions other than the one
+// being replaced, at most `clients` are then deferred, so at least one is free
+// or held only by readers that will catch up: the wait always ends.
 
 #include <condition_variable>
 #include <deque>

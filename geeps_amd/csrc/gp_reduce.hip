@@ -114,6 +114,40 @@ struct BucketPtrs {
   const float *p[kMaxBucketsPerLaunch];
 };
 
+// A launch that runs or exits at its start by a device word an earlier launch
+// on the same stream wrote: the unplanned calls' steady state (§ "Device-built
+// plans" below) launches both the cached plan and the op-order fallback right
+// behind the index check, and exactly one of them does any work, with no host
+// round trip.  `word` holds the generation of the last call whose check found
+// the index changed; this call's generation is `gen`.  A kernel's GATED = true
+// instantiation runs this test first and takes the Gate as its last argument;
+// GATED = false (the default, every other launch) compiles to the same code as
+// without it (tests/test_kernel_schedule.py checks the sweep kernel's schedule).
+struct Gate {
+  const unsigned *word;
+  unsigned gen;
+  unsigned run_if_changed;  // 0: the cached plan's launches; 1: the fallback's
+};
+
+__device__ __forceinline__ bool gate_closed(const Gate &g) {
+  const unsigned w = __hip_atomic_load(g.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (w == g.gen) != (g.run_if_changed != 0);  // block-uniform
+}
+
+// hipLaunchKernelGGL of kernel K, or of its GATED form GK with *g last.  C:
+// a compile-time condition for instantiating GK at all (only the forms the
+// unplanned calls' steady state launches have gated twins).
+#define GP_LAUNCH_GATED(C, g, K, GK, grid, block, s, ...)                 \
+  do {                                                                    \
+    if constexpr (C) {                                                    \
+      if (g) {                                                            \
+        hipLaunchKernelGGL(GK, grid, block, 0, s, __VA_ARGS__, *(g));     \
+        break;                                                            \
+      }                                                                   \
+    }                                                                     \
+    hipLaunchKernelGGL(K, grid, block, 0, s, __VA_ARGS__, Gate{});       \
+  } while (0)
+
 __device__ __forceinline__ f4 ld_stream(const f4 *p) {
   // Each bucket byte is read exactly once: non-temporal keeps the stream
   // from evicting anything useful from L2 / Infinity Cache.
@@ -125,9 +159,12 @@ __device__ __forceinline__ f4 ld_stream(const f4 *p) {
 // below has it): `in` is not read and the sum starts from +0.0f, so
 // out = 0.0f + b0 -- the fused zerofy + scatter-add of a row plan's dense run
 // (gp_scatter_init_rows_planned; 0.0f + -0.0f = +0.0f as after a memset).
-template <int NB, int UNROLL, bool ZIN = false>
+template <int NB, int UNROLL, bool ZIN = false, bool GATED = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
-    f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4) {
+    f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4, Gate gate = Gate{}) {
+  if constexpr (GATED) {
+    if (gate_closed(gate)) return;
+  }
   const size_t tile = (size_t)kBlock * UNROLL;
   const size_t stride = (size_t)gridDim.x * tile;
   const f4 *bp[NB > 0 ? NB : 1];  // NB = 0: a plain copy out = in (a gather plan's dense runs)
@@ -166,10 +203,13 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_vec_kernel(
 }
 
 // Scalar form: unaligned pointers and the < 4-float tail.
-template <int NB, bool ZIN = false>
+template <int NB, bool ZIN = false, bool GATED = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_scalar_kernel(
     float *__restrict__ out, const float *__restrict__ in, BucketPtrs b,
-    size_t n) {
+    size_t n, Gate gate = Gate{}) {
+  if constexpr (GATED) {
+    if (gate_closed(gate)) return;
+  }
   const size_t stride = (size_t)gridDim.x * kBlock;
   for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     float acc = ZIN ? 0.0f : in[i];
@@ -233,10 +273,13 @@ PhasePlan phase_plan(size_t n4_tiles) {
 // all compile-time: the fixed forms measured 18 % slower with the tile count
 // and chunks per launch passed at run time: "prod" rows at 200 and 512 MiB
 // in profiles/r01b/balance_tune_runtime_tiles.txt.
-template <int NB, int RT, bool BAL, bool ZIN = false>
+template <int NB, int RT, bool BAL, bool ZIN = false, bool GATED = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
-    size_t chunk0, int bal_tiles) {
+    size_t chunk0, int bal_tiles, Gate gate = Gate{}) {
+  if constexpr (GATED) {
+    if (gate_closed(gate)) return;
+  }
   constexpr int U = kPhaseU;
   constexpr int kT = kPhaseLdsTiles + RT;
   const int tiles = BAL ? bal_tiles : kT;
@@ -295,12 +338,13 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_phased_kernel(
 
 template <int NB, int RT, bool BAL, bool ZIN = false>
 void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_tiles,
-                   const PhasePlan &p, hipStream_t s) {
+                   const PhasePlan &p, hipStream_t s, const Gate *g = nullptr) {
   const size_t G = (size_t)num_cus();
   for (size_t l = 0; l < p.launches; ++l)
-    hipLaunchKernelGGL((bucket_sum_phased_kernel<NB, RT, BAL, ZIN>), dim3((unsigned)G), dim3(kBlock), 0,
-                       s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
-                       n4_tiles, l * (size_t)p.per_launch, p.tiles);
+    GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_phased_kernel<NB, RT, BAL, ZIN>),
+                    (bucket_sum_phased_kernel<NB, RT, BAL, ZIN, true>), dim3((unsigned)G), dim3(kBlock), s,
+                    reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b, n4_tiles,
+                    l * (size_t)p.per_launch, p.tiles);
 }
 
 // Stream-by-stream ("sweep") form of the phased sum.  Same chunk scheme (LDS
@@ -336,10 +380,13 @@ constexpr int kSweepTG = 4;
 // RT register tiles, bursts of TG tiles of U block-strides (4 KiB each)
 // (template arguments so the tuning harnesses can instantiate other shapes;
 // production uses SweepShape).
-template <int NB, int RT = kSweepRT, int TG = kSweepTG, bool ZIN = false, int U = kPhaseU>
+template <int NB, int RT = kSweepRT, int TG = kSweepTG, bool ZIN = false, int U = kPhaseU, bool GATED = false>
 __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
-    size_t chunk) {
+    size_t chunk, Gate gate = Gate{}) {
+  if constexpr (GATED) {
+    if (gate_closed(gate)) return;
+  }
   constexpr int kTile = kBlock * U;            // f4 per tile
   constexpr int kLds = kPhaseLdsF4 / kTile;    // tiles parked in LDS
   static_assert(kLds * kTile == kPhaseLdsF4, "whole LDS tiles");
@@ -447,10 +494,10 @@ BucketPtrs offset_buckets(const BucketPtrs &b, size_t off) {
 // whole 16-KiB tiles of a large shard, the mixed dwordx4 form over what is
 // left of the 16-B-aligned part, the scalar form over the rest.  ZIN: `in` is
 // ignored (may be null) and out[i] = 0.0f + b0[i] + ...  The CU count is read
-// once, so the plan and every grid of the call agree.
+// once, so the plan and every grid of the call agree.  `g`: every launch gated.
 template <int NB, bool ZIN = false>
 int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
-                         size_t n, hipStream_t s) {
+                         size_t n, hipStream_t s, const Gate *g = nullptr) {
   const size_t G = (size_t)num_cus();
   bool vec = aligned16(out) && (ZIN || aligned16(in));
   for (int k = 0; k < NB; ++k) vec = vec && aligned16(b.p[k]);
@@ -460,17 +507,18 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     using SS = SweepShape<NB, ZIN>;
     const SweepSplit sp = sweep_split<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
     for (size_t c = 0; c < sp.big; ++c)
-      hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN, SS::U>), dim3((unsigned)G),
-                         dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out),
-                         reinterpret_cast<const f4 *>(in), b, n / 4, c);
+      GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN, SS::U>),
+                      (bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN, SS::U, true>), dim3((unsigned)G),
+                      dim3(kBlock), s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
+                      n / 4, c);
     done = sp.big * sp.big_f4 * 4;
     if constexpr (!SS::kOne) {
       const BucketPtrs bo = offset_buckets<NB>(b, done);
       for (size_t c = 0; c < sp.small; ++c)
-        hipLaunchKernelGGL((bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN>), dim3((unsigned)G),
-                           dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out + done),
-                           reinterpret_cast<const f4 *>(ZIN ? nullptr : in + done), bo,
-                           (n - done) / 4, c);
+        GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN>),
+                        (bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN, kPhaseU, true>), dim3((unsigned)G),
+                        dim3(kBlock), s, reinterpret_cast<f4 *>(out + done),
+                        reinterpret_cast<const f4 *>(ZIN ? nullptr : in + done), bo, (n - done) / 4, c);
       done += sp.small * sp.small_f4 * 4;
     }
     // the rest (all of it below 3 sweep chunks): the tile-major phased form
@@ -480,9 +528,9 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
       const BucketPtrs bo = offset_buckets<NB>(b, done);
       const float *ip = ZIN ? nullptr : in + done;
       if (p.balanced)
-        launch_phased<NB, phase_reg_tiles<NB>(), true, ZIN>(out + done, ip, bo, n4_tiles, p, s);
+        launch_phased<NB, phase_reg_tiles<NB>(), true, ZIN>(out + done, ip, bo, n4_tiles, p, s, g);
       else
-        launch_phased<NB, phase_reg_tiles<NB>(), false, ZIN>(out + done, ip, bo, n4_tiles, p, s);
+        launch_phased<NB, phase_reg_tiles<NB>(), false, ZIN>(out + done, ip, bo, n4_tiles, p, s, g);
       done += n4_tiles * 4;
     }
   }
@@ -497,9 +545,9 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     const size_t tiles = (n4 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
     const size_t cap = G * kPerCU;
     const size_t grid = tiles < cap ? tiles : cap;
-    hipLaunchKernelGGL((bucket_sum_vec_kernel<NB, U, ZIN>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, s, reinterpret_cast<f4 *>(out + done),
-                       reinterpret_cast<const f4 *>(in_at), offset_buckets<NB>(b, done), n4);
+    GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_vec_kernel<NB, U, ZIN>), (bucket_sum_vec_kernel<NB, U, ZIN, true>),
+                    dim3((unsigned)grid), dim3(kBlock), s, reinterpret_cast<f4 *>(out + done),
+                    reinterpret_cast<const f4 *>(in_at), offset_buckets<NB>(b, done), n4);
     done += n4 * 4;
     in_at = ZIN ? nullptr : in + done;
   }
@@ -507,8 +555,8 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     const size_t rem = n - done;
     size_t grid = (rem + kBlock - 1) / kBlock;
     if (grid > G * kBlocksPerCU) grid = G * kBlocksPerCU;
-    hipLaunchKernelGGL((bucket_sum_scalar_kernel<NB, ZIN>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, s, out + done, in_at, offset_buckets<NB>(b, done), rem);
+    GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_scalar_kernel<NB, ZIN>), (bucket_sum_scalar_kernel<NB, ZIN, true>),
+                    dim3((unsigned)grid), dim3(kBlock), s, out + done, in_at, offset_buckets<NB>(b, done), rem);
   }
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;
@@ -696,11 +744,14 @@ __device__ __forceinline__ void st_copy(T *p, T v) {
 // T = f4 (VEC 4) or float (VEC 1).  A group of LPR consecutive lanes owns a
 // row; each group handles RPG rows per iteration, all their loads issued
 // before the first store.  `vw` = row_size / VEC (vectors per row).
-template <typename T, int VEC, int OP, int LPR, int RPG>
+template <typename T, int VEC, int OP, int LPR, int RPG, bool GATED = false>
 __global__ __launch_bounds__(kBlock) void row_op_kernel(
     float *__restrict__ y, const float *__restrict__ x,
     const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
-    uint64_t off1, size_t row_size, size_t vw, size_t limit) {
+    uint64_t off1, size_t row_size, size_t vw, size_t limit, Gate gate = Gate{}) {
+  if constexpr (GATED) {
+    if (gate_closed(gate)) return;
+  }
   constexpr int kGroups = kBlock / LPR;
   const int lane = threadIdx.x % LPR;
   const size_t group = (size_t)blockIdx.x * kGroups + threadIdx.x / LPR;
@@ -872,11 +923,14 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // -- take one contiguous eighth of the tiles, grid-stride inside it; needs a
 // multiple of 8 blocks.  It tied or lost on a random index (probe 8,
 // profiles/r03/tune/r3_tilemap_tune.txt).
-template <typename T, int OP, int LPR, int RPG, int SEG, int MAP = 0>
+template <typename T, int OP, int LPR, int RPG, int SEG, int MAP = 0, bool GATED = false>
 __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
     const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
-    uint64_t off1, size_t row_size, size_t vw, size_t limit, const SegArg<SEG> seg) {
+    uint64_t off1, size_t row_size, size_t vw, size_t limit, const SegArg<SEG> seg, Gate gate = Gate{}) {
+  if constexpr (GATED) {
+    if (gate_closed(gate)) return;
+  }
   static_assert((OP == kAssignTo && (SEG == kFlat || SEG == kSegX)) ||
                     ((OP == kAddFrom || OP == kInitFrom) && SEG == kFlat),
                 "gather (flat / segmented source) or flat scatter-add / init");
@@ -1020,8 +1074,11 @@ inline int resident_blocks(const void *kernel, std::atomic<int> &cache) {
 template <typename T, int VEC, int OP, int SEG, int LPR>
 void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
                        size_t n, uint64_t off0, uint64_t off1, size_t row_size,
-                       size_t limit, const SegArg<SEG> &seg, bool sorted, hipStream_t s) {
+                       size_t limit, const SegArg<SEG> &seg, bool sorted, hipStream_t s,
+                       const Gate *g) {
   constexpr bool kWaveShape = VEC == 4 && LPR <= 32;
+  // the unplanned calls' steady state gates its flat scatter-add / init launches
+  constexpr bool kGatable = SEG == kFlat && (OP == kAddFrom || OP == kInitFrom);
   constexpr bool kWaveGather = OP == kAssignTo && (SEG == kFlat || SEG == kSegX);
   constexpr bool kWaveScatter = (OP == kAddFrom || OP == kInitFrom) && SEG == kFlat;
   if constexpr (kWaveShape && (kWaveGather || kWaveScatter)) {
@@ -1038,8 +1095,8 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
       static std::atomic<int> occ{0};
       const size_t cap = (size_t)num_cus() * resident_blocks(reinterpret_cast<const void *>(kern), occ);
       if (grid > cap) grid = cap;
-      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, s, y, x, idx, n, off0, off1,
-                         row_size, row_size / VEC, limit, seg);
+      GP_LAUNCH_GATED(kGatable, g, kern, (row_wave_kernel<T, OP, LPR, RPG, SEG, 0, true>), dim3((unsigned)grid),
+                      dim3(kBlock), s, y, x, idx, n, off0, off1, row_size, row_size / VEC, limit, seg);
       return;
     }
   }
@@ -1057,10 +1114,10 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
                                                  : grid_cap();
   if (grid > cap) grid = cap;
   if constexpr (SEG == kFlat)
-    hipLaunchKernelGGL((row_op_kernel<T, VEC, OP, LPR, RPG>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, s, y, x, idx, n, off0, off1, row_size,
-                       row_size / VEC, limit);
-  else
+    GP_LAUNCH_GATED(kGatable, g, (row_op_kernel<T, VEC, OP, LPR, RPG>), (row_op_kernel<T, VEC, OP, LPR, RPG, true>),
+                    dim3((unsigned)grid), dim3(kBlock), s, y, x, idx, n, off0, off1, row_size,
+                    row_size / VEC, limit);
+  else  // (never gated)
     hipLaunchKernelGGL((row_op_seg_kernel<T, VEC, OP, LPR, RPG, SEG>), dim3((unsigned)grid),
                        dim3(kBlock), 0, s, y, x, idx, n, off0, off1, row_size,
                        row_size / VEC, limit, seg);
@@ -1069,11 +1126,12 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
 template <typename T, int VEC, int OP, int SEG>
 void launch_row_op_t(float *y, const float *x, const gp_double_index *idx,
                      size_t n, uint64_t off0, uint64_t off1, size_t row_size,
-                     size_t limit, const SegArg<SEG> &seg, bool sorted, hipStream_t s) {
+                     size_t limit, const SegArg<SEG> &seg, bool sorted, hipStream_t s,
+                     const Gate *g = nullptr) {
   const size_t vw = row_size / VEC;
   // Lanes per row: the smallest power of two covering the row, capped at a
   // wave; short rows (64 / 128 floats) pack 4 / 2 rows into one wave.
-#define GP_LPR(L) launch_row_op_lpr<T, VEC, OP, SEG, L>(y, x, idx, n, off0, off1, row_size, limit, seg, sorted, s)
+#define GP_LPR(L) launch_row_op_lpr<T, VEC, OP, SEG, L>(y, x, idx, n, off0, off1, row_size, limit, seg, sorted, s, g)
   if (vw <= 1)
     GP_LPR(1);
   else if (vw <= 2)
@@ -1094,17 +1152,17 @@ void launch_row_op_t(float *y, const float *x, const gp_double_index *idx,
 template <int OP>
 int launch_row_op(float *y, const float *x, const gp_double_index *idx,
                   size_t n, gp_double_index off, size_t row_size, size_t limit,
-                  hipStream_t s, bool sorted = false) {
+                  hipStream_t s, bool sorted = false, const Gate *g = nullptr) {
   if (n == 0) return GP_OK;
   if (!y || !x || !idx) return set_error(GP_ERR_INVALID, "null pointer");
   if (row_size == 0) return set_error(GP_ERR_INVALID, "row_size == 0");
   const SegArg<kFlat> flat{};
   if (row_size % 4 == 0 && aligned16(y) && aligned16(x))
     launch_row_op_t<f4, 4, OP, kFlat>(y, x, idx, n, off.id0, off.id1, row_size, limit, flat, sorted,
-                                      s);
+                                      s, g);
   else
     launch_row_op_t<float, 1, OP, kFlat>(y, x, idx, n, off.id0, off.id1, row_size, limit, flat,
-                                         sorted, s);
+                                         sorted, s, g);
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;
 }
@@ -1406,9 +1464,15 @@ int launch_gather_planned(float *y, const float *x, const gp_row_segments *xs,
 //     call with the same index -- same pointer, size, offsets, row size and
 //     limit, and entry for entry the same content, which the scan checks
 //     against the copy -- builds the destination-sorted residual (a hipCUB
-//     radix sort, gp_sort.hip) and runs it.  Later calls skip the scan: they
-//     only compare the index with the copy (index_compare_kernel) and run the
-//     cached dense runs and sorted residual.
+//     radix sort, gp_sort.hip) and runs it.  Later calls (the steady state)
+//     skip the scan and the host round trip: index_verify_kernel compares the
+//     index with the copy and, if any entry changed, writes the call's
+//     generation into a gate word; the cached dense runs and sorted residual
+//     are launched behind it gated to run only if nothing changed, and the
+//     op-order form of the whole call gated to run only if something did
+//     (Gate, the GATED kernel forms).  No D2H, no stream sync: the call is as
+//     asynchronous as a planned one.  The check also sets a host-visible word,
+//     which a later call reads to drop the stale entry and plan afresh.
 //     An index that changes every call costs one copy per call, no sort.  Visiting rows in destination order is bit-neutral under
 //     the call's precondition (distinct destinations).
 // Calls below g_analyze_min_bytes (gp_set_unplanned_min_bytes) skip all this.
@@ -1552,13 +1616,18 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
   }
 }
 
-// A planned index seen again: only whether every entry still equals the cached
-// copy (32 B read per entry, no tile analysis).  Each thread holds 4 entries'
-// loads in flight; one global atomic per wave that saw a difference.
+// The steady state's check of a planned index seen again: whether every entry
+// still equals the cached copy (32 B read per entry, no tile analysis).  Each
+// thread holds 4 entries' loads in flight.  A wave that saw a difference
+// stores this call's generation into the call's gate word (the gated launches
+// behind it read it) and into the entry's host-visible word (the next call
+// drops the entry).  Plain vector stores, idempotent: no atomics needed.
 constexpr int kCmpPerThread = 4;
-__global__ __launch_bounds__(kBlock) void index_compare_kernel(const gp_double_index *__restrict__ idx,
-                                                               const gp_double_index *__restrict__ cached, size_t n,
-                                                               ScanHeader *__restrict__ hdr) {
+constexpr unsigned kGateSlots = 64;  // gate words per entry: calls in flight on one entry
+__global__ __launch_bounds__(kBlock) void index_verify_kernel(const gp_double_index *__restrict__ idx,
+                                                              const gp_double_index *__restrict__ cached, size_t n,
+                                                              unsigned *__restrict__ gate_word,
+                                                              unsigned *__restrict__ host_word, unsigned gen) {
   const size_t step = (size_t)gridDim.x * kBlock * kCmpPerThread;
   bool differs = false;
   for (size_t base = (size_t)blockIdx.x * kBlock * kCmpPerThread + threadIdx.x; base < n; base += step) {
@@ -1573,7 +1642,10 @@ __global__ __launch_bounds__(kBlock) void index_compare_kernel(const gp_double_i
 #pragma unroll
     for (int k = 0; k < kCmpPerThread; ++k) differs |= (a[k].id0 != b[k].id0) | (a[k].id1 != b[k].id1);
   }
-  if (__any(differs) && (threadIdx.x & 63) == 0) atomicAdd(&hdr->mismatches, 1u);
+  if (__any(differs) && (threadIdx.x & 63) == 0) {
+    __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Residual rows of a call: up to kMaxDeviceRuns + 1 entry ranges, passed by
@@ -1693,6 +1765,33 @@ struct DevRun {
   uint64_t e0, rows, from, to;  // first entry, rows, endpoints of the first entry
 };
 
+// A host-visible word in pinned (fine-grained, coherent) host memory that a
+// kernel may store to.  Freed only after the device is idle: a check still in
+// flight may write it.
+struct PinnedWord {
+  unsigned *p = nullptr;
+  int device = 0;
+  PinnedWord(int dev, int *rc) : device(dev) {
+    void *q = nullptr;
+    *rc = hipHostMalloc(&q, 64, hipHostMallocCoherent) == hipSuccess ? GP_OK
+                                                                      : set_error(GP_ERR_HIP, "plan cache hipHostMalloc");
+    p = static_cast<unsigned *>(q);
+    if (p) __atomic_store_n(p, 0u, __ATOMIC_RELEASE);
+  }
+  ~PinnedWord() {
+    if (!p) return;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
+    (void)hipHostFree(p);
+    if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
+  }
+  unsigned load() const { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+  PinnedWord(const PinnedWord &) = delete;
+  PinnedWord &operator=(const PinnedWord &) = delete;
+};
+
 // An entry is immutable once in the cache.  The first call with an index
 // leaves a copy-only entry (`sorted` null); the next call with the same
 // content builds the destination-sorted residual into a new entry that
@@ -1706,6 +1805,12 @@ struct CachedPlan {
   std::shared_ptr<DevBuf> spare;
   size_t resid = 0;
   std::vector<DevRun> runs;    // with `sorted`: the index's dense runs (the rest is the residual)
+  // with `sorted`, the steady state's gate: kGateSlots device words (call
+  // generation g uses word g % kGateSlots), the host-visible "the index
+  // changed" word, and the generation counter (0 never used)
+  std::shared_ptr<DevBuf> gate;
+  std::shared_ptr<PinnedWord> changed;
+  std::atomic<unsigned> gen{0};
   hipEvent_t ready = nullptr;  // recorded once copy (and sorted) are built, on the building stream
   uint64_t last_use = 0;
   size_t bytes = 0;
@@ -1713,6 +1818,7 @@ struct CachedPlan {
   const gp_double_index *sorted_ptr() const {
     return sorted ? static_cast<const gp_double_index *>(sorted->p) : nullptr;
   }
+  unsigned *gate_words() const { return static_cast<unsigned *>(gate->p); }
   ~CachedPlan() {
     if (!ready) return;
     int cur = -1;
@@ -1809,6 +1915,11 @@ int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_doub
   else
     p->sorted = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
   if (rc != GP_OK) return rc;
+  p->gate = std::make_shared<DevBuf>(kGateSlots * sizeof(unsigned), key.device, &rc);
+  if (rc != GP_OK) return rc;
+  p->changed = std::make_shared<PinnedWord>(key.device, &rc);
+  if (rc != GP_OK) return rc;
+  GP_HIP_TRY(hipMemsetAsync(p->gate->p, 0, kGateSlots * sizeof(unsigned), s));
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
   uint32_t *kv = nullptr;  // keys, values, sorted keys, sorted values
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&kv), 4 * resid * sizeof(uint32_t), s));
@@ -1842,8 +1953,52 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   GP_HIP_TRY(hipGetDevice(&dev));
   const PlanKey key{dev, OP, reinterpret_cast<uintptr_t>(idx), n, W, limit, off.id0, off.id1};
   std::shared_ptr<CachedPlan> cached = OP == kAssignTo ? nullptr : cache_find(key);
+  // a steady-state call since the last host look found the index changed: the
+  // entry is stale, plan this call afresh (scan, host round trip)
+  if (cached && cached->sorted && cached->changed->load() != 0) {
+    cache_drop(cached);
+    cached.reset();
+  }
   // its copy (and sorted residual) may still be in flight on the stream that built them
   if (cached) GP_HIP_TRY(hipStreamWaitEvent(s, cached->ready, 0));
+  auto launch_runs = [&](const std::vector<DevRun> &rs, const Gate *g) {
+    for (const DevRun &r : rs) {
+      BucketPtrs b = {};
+      b.p[0] = x + r.from * W;
+      float *yr = y + r.to * W;
+      int rc;
+      if constexpr (OP == kAddFrom)
+        rc = launch_bucket_sum_nb<1>(yr, yr, b, r.rows * W, s, g);
+      else if constexpr (OP == kInitFrom)
+        rc = launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s, g);
+      else
+        rc = launch_bucket_sum_nb<0>(yr, x + r.from * W, BucketPtrs{}, r.rows * W, s);
+      if (rc != GP_OK) return rc;
+    }
+    return (int)GP_OK;
+  };
+  if (cached && cached->sorted) {
+    // The steady state: a planned index seen again.  Check it against the copy
+    // and launch both outcomes behind the check, each gated on its result:
+    // the cached dense runs and sorted residual (unchanged), or this call's
+    // rows in op order (changed; as a first call runs its residual).  Exactly
+    // one does any work; nothing waits for the host.
+    unsigned gen = ++cached->gen;
+    if (gen == 0) gen = ++cached->gen;  // 0 is the gate words' initial value
+    unsigned *word = cached->gate_words() + gen % kGateSlots;
+    const size_t per_block = (size_t)kBlock * kCmpPerThread;
+    const size_t grid = std::max<size_t>(1, std::min((n + per_block - 1) / per_block, (size_t)num_cus() * 8));
+    hipLaunchKernelGGL(index_verify_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, cached->copy_ptr(), n,
+                       word, cached->changed->p, gen);
+    GP_HIP_TRY(hipGetLastError());
+    const Gate same{word, gen, 0}, changed{word, gen, 1};
+    int rc = launch_runs(cached->runs, &same);
+    if (rc != GP_OK) return rc;
+    rc = launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
+                           /*sorted=*/true, &same);
+    if (rc != GP_OK) return rc;
+    return launch_row_op<OP>(y, x, idx, n, off, W, limit, s, /*sorted=*/false, &changed);
+  }
   const size_t scan_bytes = kScanWordsOff + groups * kScanWords * sizeof(uint64_t);
   char *ws = nullptr;
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), scan_bytes, s));
@@ -1854,45 +2009,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
       if (p) (void)hipFreeAsync(p, s);
     }
   } free_ws{ws, s};
-  auto launch_runs = [&](const std::vector<DevRun> &rs) {
-    for (const DevRun &r : rs) {
-      BucketPtrs b = {};
-      b.p[0] = x + r.from * W;
-      float *yr = y + r.to * W;
-      int rc;
-      if constexpr (OP == kAddFrom)
-        rc = launch_bucket_sum_nb<1>(yr, yr, b, r.rows * W, s);
-      else if constexpr (OP == kInitFrom)
-        rc = launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s);
-      else
-        rc = launch_bucket_sum_nb<0>(yr, x + r.from * W, BucketPtrs{}, r.rows * W, s);
-      if (rc != GP_OK) return rc;
-    }
-    return (int)GP_OK;
-  };
   GP_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(ScanHeader), s));
-  if (cached && cached->sorted) {
-    // A planned index seen again: compare it with the copy (no tile analysis);
-    // the same content runs the cached dense runs and sorted residual at once.
-    const size_t per_block = (size_t)kBlock * kCmpPerThread;
-    const size_t grid = std::max<size_t>(1, std::min((n + per_block - 1) / per_block, (size_t)num_cus() * 8));
-    hipLaunchKernelGGL(index_compare_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, cached->copy_ptr(), n,
-                       reinterpret_cast<ScanHeader *>(ws));
-    GP_HIP_TRY(hipGetLastError());
-    char *h = static_cast<char *>(g_scan_landing.get(sizeof(ScanHeader)));
-    if (!h) return set_error(GP_ERR_HIP, "pinned scan buffer");
-    GP_HIP_TRY(hipMemcpyAsync(h, ws, sizeof(ScanHeader), hipMemcpyDeviceToHost, s));
-    GP_HIP_TRY(hipStreamSynchronize(s));
-    if (reinterpret_cast<const ScanHeader *>(h)->mismatches == 0) {
-      const int rc = launch_runs(cached->runs);
-      if (rc != GP_OK) return rc;
-      return launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
-                               /*sorted=*/true);
-    }
-    cache_drop(cached);  // the same pointer now holds another index: plan it afresh
-    cached.reset();
-    GP_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(ScanHeader), s));
-  }
   {
     const size_t grid = std::max<size_t>(1, std::min(groups, (size_t)num_cus() * 8));
     if (cached)
@@ -1952,7 +2069,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
       std::sort(runs.begin(), runs.end(), [](const DevRun &a, const DevRun &b) { return a.e0 < b.e0; });
     }
   }
-  if (const int rc = launch_runs(runs); rc != GP_OK) return rc;
+  if (const int rc = launch_runs(runs, nullptr); rc != GP_OK) return rc;
   // the residual: entry ranges between the runs
   EntryRanges rr = {};
   {
@@ -1972,9 +2089,6 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   }
   const size_t resid = rr.pre[rr.count];
   if (resid == 0) return GP_OK;
-  if (cached && cached->sorted && cached->resid == resid)  // the same index: its destination-sorted residual
-    return launch_row_op<OP>(y, x, cached->sorted_ptr(), resid, gp_double_index{0, 0}, W, limit, s,
-                             /*sorted=*/true);
   // destinations already (mostly) ascending: the call's order is the sorted one
   size_t resid_tiles = 0, asc_tiles = 0;
   for (uint32_t i = 0; i < rr.count; ++i) {

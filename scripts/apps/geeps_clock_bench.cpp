@@ -12,6 +12,14 @@
 // CLOCK_BENCH_READ_PER_SHARD=1 declares one Read op per server shard instead
 // (as per-blob ops mostly fall within one shard), which direct reads
 // (GEEPS_DIRECT_READ=1) can hand out in place.
+// GEEPS_TEST_SPREAD_DEVICES=1: process p works on GPU p % device_count (one
+// process per GPU, as on an 8-GPU node), selected before GeePs is created.
+//
+// Read check: every worker adds 0.5 to every element each clock (the setup
+// clock adds 0), so the last Read after K timed + warm-up clocks must hold
+// 0.5 * P * K in every element at slack 0 (exact in fp32), and lie in
+// [0.5 * P * (K - slack), 0.5 * P * K] under SSP.  A device kernel counts the
+// elements outside that range over every Read buffer ("read_bad").
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,6 +39,15 @@
     }                                                              \
   } while (0)
 
+__global__ void count_outside(const float *x, size_t n, float lo, float hi, unsigned long long *bad) {
+  unsigned long long local = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    local += (v >= lo && v <= hi) ? 0 : 1;
+  }
+  if (local) atomicAdd(bad, local);
+}
+
 int main(int argc, char **argv) {
   if (argc < 7) {
     std::fprintf(stderr, "usage: %s pid nproc base_port rows clocks warmup\n", argv[0]);
@@ -40,6 +57,13 @@ int main(int argc, char **argv) {
   const size_t rows = std::strtoull(argv[4], 0, 10);
   const int clocks = std::atoi(argv[5]), warmup = std::atoi(argv[6]);
   const int slack = argc > 7 ? std::atoi(argv[7]) : 0;
+  int device = 0;
+  if (std::getenv("GEEPS_TEST_SPREAD_DEVICES")) {
+    int count = 0;
+    HCK(hipGetDeviceCount(&count));
+    device = pid % count;
+  }
+  HCK(hipSetDevice(device));
   GeePsConfig cfg;
   for (int i = 0; i < P; ++i) {
     cfg.host_list.push_back("127.0.0.1");
@@ -52,11 +76,13 @@ int main(int argc, char **argv) {
   // (clientlib-viter.cpp:674-682): P contiguous ranges
   const bool per_shard = std::getenv("CLOCK_BENCH_READ_PER_SHARD") != nullptr;
   std::vector<int> hr, hpr;
+  std::vector<size_t> hr_rows;
   for (int s = 0; s < (per_shard ? P : 1); ++s) {
     const size_t div = rows / P, res = rows % P;
     const size_t lo = per_shard ? div * s + std::min<size_t>(s, res) : 0;
     const size_t hi = per_shard ? lo + div + ((size_t)s < res ? 1 : 0) : rows;
     hr.push_back(ps->VirtualRead(0, std::vector<size_t>(ids.begin() + lo, ids.begin() + hi), slack));
+    hr_rows.push_back(hi - lo);
   }
   const int hp = ps->VirtualPreUpdate(0, ids);
   for (int h : hr) hpr.push_back(ps->VirtualPostRead(h));
@@ -86,16 +112,34 @@ int main(int argc, char **argv) {
     ps->Clock();
   }
   // the last Read waits for the last clock's refresh: include it
-  RowData *rb = nullptr;
-  for (int h : hr) ps->Read(h, &rb);
+  std::vector<RowData *> last(hr.size(), nullptr);
+  for (size_t i = 0; i < hr.size(); ++i) ps->Read(hr[i], &last[i]);
   const double s = std::chrono::duration<double>(clk::now() - t0).count();
   float probe = 0;
-  HCK(hipMemcpy(&probe, rb, 4, hipMemcpyDeviceToHost));
+  HCK(hipMemcpy(&probe, last.back(), 4, hipMemcpyDeviceToHost));
+  // every element of every Read buffer against the expected range (untimed)
+  const int K = warmup + clocks;
+  const float hi = 0.5f * (float)P * (float)K, lo = 0.5f * (float)P * (float)(K - slack);
+  unsigned long long *dbad = nullptr, bad = 0;
+  HCK(hipMalloc(&dbad, sizeof *dbad));
+  HCK(hipMemset(dbad, 0, sizeof *dbad));
+  size_t checked = 0;
+  for (size_t i = 0; i < hr.size(); ++i) {
+    const size_t n = hr_rows[i] * ROW_DATA_SIZE;
+    hipLaunchKernelGGL(count_outside, dim3(1024), dim3(256), 0, 0, reinterpret_cast<const float *>(last[i]), n,
+                       lo, hi, dbad);
+    HCK(hipGetLastError());
+    checked += n;
+  }
+  HCK(hipMemcpy(&bad, dbad, sizeof bad, hipMemcpyDeviceToHost));
+  HCK(hipFree(dbad));
   const double per = s / clocks;
   const double table_bytes = (double)rows * sizeof(RowData);
-  std::printf("{\"process\": %d, \"processes\": %d, \"rows\": %zu, \"table_bytes\": %.0f, "
-              "\"slack\": %d, \"clocks\": %d, \"ms_per_clock\": %.4f, \"delta_GBps\": %.2f, \"probe\": %.1f}\n",
-              pid, P, rows, table_bytes, slack, clocks, per * 1e3, table_bytes / per / 1e9, probe);
+  std::printf("{\"process\": %d, \"processes\": %d, \"device\": %d, \"rows\": %zu, \"table_bytes\": %.0f, "
+              "\"slack\": %d, \"clocks\": %d, \"ms_per_clock\": %.4f, \"delta_GBps\": %.2f, \"probe\": %.1f, "
+              "\"read_checked\": %zu, \"read_bad\": %llu, \"read_lo\": %.1f, \"read_hi\": %.1f}\n",
+              pid, P, device, rows, table_bytes, slack, clocks, per * 1e3, table_bytes / per / 1e9, probe,
+              checked, bad, lo, hi);
   std::fflush(stdout);
   std::fprintf(stderr, "stats %s\n", ps->GetStats().c_str());
   ps->Shutdown();

@@ -1,0 +1,248 @@
+"""Probe of HIP IPC memory handles between two processes.
+
+libgeeps aborted once with ROCr's "IPC Attach: Invalid IPC handle! %u and %u"
+from hipIpcOpenMemHandle (profiles/r03/e2e/pytest_libgeeps_race.log:379-382),
+in a test whose tables are 2,000 rows x 512 B: every exported buffer was a
+1,024,000-B hipMalloc.  This probe talks to the HIP runtime directly (ctypes on
+libamdhip64, none of libgeeps' wrappers or locks) and asks, per scenario, whether
+a handle still opens, and still maps the exported bytes, when:
+
+  seq        each buffer is opened before the next one is exported;
+  seq_big    the same with 4-MiB buffers;
+  batch      every buffer is exported before the importer opens the first;
+  batch_big  the same with 4-MiB buffers (allocations of their own);
+  twice      one buffer exported twice, the FIRST handle opened afterwards;
+  bidir      both processes export new buffers on one thread while another
+             thread opens the peer's handles, as libgeeps' server and reader
+             threads do (no lock around the runtime's IPC calls).
+  freed      an exported buffer is freed and its address range reused by a
+             new allocation before the importer opens the old handle.
+
+Each scenario runs as two fresh processes (exporter / importer, or two peers)
+that pass handles through files.  Output: one JSON line per scenario with
+ok / failure counts, the allocation addresses (is a small buffer a fragment
+of a shared block?) and the runtime's stderr lines.
+
+Usage: python scripts/probes/ipc_probe.py [scenario ...]
+"""
+from __future__ import annotations
+
+import ctypes
+import faulthandler
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+SMALL = 2000 * 512       # a 2,000-row RowData buffer, as in the failing test
+BIG = 4 << 20
+
+
+class IpcHandle(ctypes.Structure):
+    # bytes, not c_char: a c_char array field reads back cut at its first NUL
+    _fields_ = [("reserved", ctypes.c_ubyte * 64)]
+
+
+def hip():
+    h = ctypes.CDLL("libamdhip64.so")
+    h.hipIpcGetMemHandle.argtypes = [ctypes.POINTER(IpcHandle), ctypes.c_void_p]
+    h.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), IpcHandle, ctypes.c_uint]
+    h.hipIpcCloseMemHandle.argtypes = [ctypes.c_void_p]
+    h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    h.hipFree.argtypes = [ctypes.c_void_p]
+    h.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    h.hipMemGetAddressRange.argtypes = [ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]
+    h.hipGetErrorString.restype = ctypes.c_char_p
+    h.hipDeviceSynchronize.argtypes = []
+    return h
+
+
+def call(h, rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: {h.hipGetErrorString(rc).decode()}")
+
+
+def alloc(h, nbytes, value):
+    p = ctypes.c_void_p()
+    call(h, h.hipMalloc(ctypes.byref(p), nbytes), "hipMalloc")
+    call(h, h.hipMemset(p, value, nbytes), "hipMemset")
+    call(h, h.hipDeviceSynchronize(), "sync")
+    base, size = ctypes.c_void_p(), ctypes.c_size_t()
+    call(h, h.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), p), "range")
+    return p, {"ptr": p.value, "base_is_ptr": base.value == p.value, "range": size.value}
+
+
+def export(h, p):
+    hd = IpcHandle()
+    call(h, h.hipIpcGetMemHandle(ctypes.byref(hd), p), "hipIpcGetMemHandle")
+    return ctypes.string_at(ctypes.addressof(hd), 64)
+
+
+def put(d, name, payload):
+    tmp = os.path.join(d, name + ".tmp")
+    with open(tmp, "wb") as f:
+        f.write(payload)
+    os.rename(tmp, os.path.join(d, name))
+
+
+def get(d, name, timeout=30.0):
+    path = os.path.join(d, name)
+    t0 = time.monotonic()
+    while not os.path.exists(path):
+        if time.monotonic() - t0 > timeout:
+            raise TimeoutError(name)
+        time.sleep(0.001)
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def open_and_check(h, raw, value, nbytes):
+    """Open a handle; return (ok, detail)."""
+    hd = IpcHandle()
+    assert len(raw) == 64
+    ctypes.memmove(ctypes.addressof(hd), raw, 64)
+    p = ctypes.c_void_p()
+    rc = h.hipIpcOpenMemHandle(ctypes.byref(p), hd, 1)  # hipIpcMemLazyEnablePeerAccess
+    if rc != 0:
+        return False, "open: " + h.hipGetErrorString(rc).decode()
+    out = (ctypes.c_ubyte * 16)()
+    for off in (0, nbytes - 16):
+        call(h, h.hipMemcpy(out, ctypes.c_void_p(p.value + off), 16, 2), "D2H")  # DeviceToHost
+        if any(b != value for b in out):
+            h.hipIpcCloseMemHandle(p)
+            return False, f"mapped bytes {list(out)[:4]} at +{off}, exported {value}"
+    call(h, h.hipIpcCloseMemHandle(p), "close")
+    return True, ""
+
+
+# --- roles -------------------------------------------------------------------
+def progress(*a):
+    print(f"[{time.monotonic():.3f}]", *a, file=sys.stderr, flush=True)
+
+
+def exporter(scn, d):
+    faulthandler.dump_traceback_later(20, repeat=True)  # where a hang sits
+    h = hip()
+    n = 16
+    size = BIG if scn.endswith("_big") else SMALL
+    keep, info = [], []
+    if scn == "twice":
+        p, inf = alloc(h, size, 7)
+        keep.append(p)
+        info.append(inf)
+        put(d, "h0", export(h, p))
+        put(d, "h1", export(h, p))
+        put(d, "exported", b"2")
+    elif scn == "freed":
+        for k in range(n):
+            p, inf = alloc(h, size, 1 + k)
+            put(d, f"h{k}", export(h, p))
+            info.append(inf)
+            call(h, h.hipFree(p), "free")
+            q, _ = alloc(h, size, 200)   # likely the same range, new contents
+            keep.append(q)
+        put(d, "exported", str(n).encode())
+    else:
+        for k in range(n):
+            progress("alloc", k)
+            p, inf = alloc(h, size, 1 + k)
+            keep.append(p)
+            info.append(inf)
+            progress("export", k, inf)
+            put(d, f"h{k}", export(h, p))
+            if scn.startswith("seq"):
+                get(d, f"opened{k}")
+        put(d, "exported", str(n).encode())
+    get(d, "done", timeout=60)
+    print(json.dumps({"role": "exporter", "allocs": info}))
+
+
+def importer(scn, d):
+    faulthandler.dump_traceback_later(20, repeat=True)
+    h = hip()
+    n = int(get(d, "exported", timeout=60)) if not scn.startswith("seq") else 16
+    results = []
+    for k in range(n):
+        raw = get(d, f"h{k}")
+        value = 7 if scn == "twice" else 1 + k
+        nbytes = BIG if scn.endswith("_big") else SMALL
+        if scn == "twice" and k == 1:
+            break  # only the first handle, opened after the second export
+        progress("open", k)
+        ok, why = open_and_check(h, raw, value, nbytes)
+        progress("opened", k, ok, why)
+        results.append({"k": k, "ok": ok, "why": why})
+        if scn.startswith("seq"):
+            put(d, f"opened{k}", b"1")
+    put(d, "done", b"1")
+    print(json.dumps({"role": "importer", "results": results}))
+
+
+def peer(scn, d, me):
+    """bidir: export new small buffers on one thread, open the peer's on another."""
+    faulthandler.dump_traceback_later(20, repeat=True)
+    h = hip()
+    other = 1 - me
+    n = 64
+    keep = []
+    errors = []
+
+    def exp():
+        for k in range(n):
+            p, _ = alloc(h, SMALL, (me * 100 + k) % 251 + 1)
+            keep.append(p)
+            put(d, f"p{me}_h{k}", export(h, p))
+
+    def imp():
+        for k in range(n):
+            raw = get(d, f"p{other}_h{k}")
+            ok, why = open_and_check(h, raw, (other * 100 + k) % 251 + 1, SMALL)
+            if not ok:
+                errors.append({"k": k, "why": why})
+
+    t1, t2 = threading.Thread(target=exp), threading.Thread(target=imp)
+    t1.start()
+    t2.start()
+    t1.join()
+    t2.join()
+    put(d, f"p{me}_done", b"1")
+    get(d, f"p{other}_done", timeout=60)
+    print(json.dumps({"role": f"peer{me}", "opened": n, "errors": errors}))
+
+
+def run(scn):
+    d = tempfile.mkdtemp(prefix="ipc_probe_")
+    me = os.path.abspath(__file__)
+    if scn == "bidir":
+        cmds = [[sys.executable, me, "--peer", scn, d, "0"], [sys.executable, me, "--peer", scn, d, "1"]]
+    else:
+        cmds = [[sys.executable, me, "--exporter", scn, d], [sys.executable, me, "--importer", scn, d]]
+    procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for c in cmds]
+    outs = []
+    deadline = time.monotonic() + 45
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=max(1.0, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            o, e = p.communicate()
+        outs.append({"rc": p.returncode, "out": [json.loads(x) for x in o.splitlines() if x.startswith("{")],
+                     "stderr": [x for x in e.splitlines() if x.strip()][-40:]})
+    print(json.dumps({"scenario": scn, "procs": outs}), flush=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--exporter":
+        exporter(sys.argv[2], sys.argv[3])
+    elif len(sys.argv) > 1 and sys.argv[1] == "--importer":
+        importer(sys.argv[2], sys.argv[3])
+    elif len(sys.argv) > 1 and sys.argv[1] == "--peer":
+        peer(sys.argv[2], sys.argv[3], int(sys.argv[4]))
+    else:
+        for scn in sys.argv[1:] or ["seq_big", "seq", "batch_big", "batch", "twice", "bidir", "freed"]:
+            run(scn)

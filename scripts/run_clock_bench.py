@@ -6,7 +6,13 @@ server each) and print one aggregate JSON line.
 Every worker updates every row each clock, so the job reduces P full delta
 tables per clock: aggregate delta rate = P * rows * 512 B / (slowest worker's
 ms per clock).  All processes share the one GPU of the box (HIP_VISIBLE_DEVICES
-is left alone).
+is left alone), unless GEEPS_TEST_SPREAD_DEVICES=1 puts process p on GPU
+p % device_count (one process per GPU, as on an 8-GPU node).
+
+Each worker checks its last Read over every element against the exact sum
+(read_bad = elements outside [0.5 P (K - slack), 0.5 P K]); `read_ok` is true
+when no worker saw one.  The workers' GetStats counters say which data path
+ran: peer buckets staged (nr_peer_staged), refreshes staged or read in place.
 
 With CLOCK_BENCH_PROF=<dir> set, each worker runs under
 ``rocprofv3 --kernel-trace --memory-copy-trace --stats`` into <dir>/p<id>/.
@@ -65,7 +71,7 @@ def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900, extra_en
     # this one-GPU rehearsal in that regime.  (The GPU box exports
     # GPU_MAX_HW_QUEUES=4, so this overrides; CLOCK_BENCH_HW_QUEUES chooses.)
     if P > 2:
-        env["GPU_MAX_HW_QUEUES"] = os.environ.get("CLOCK_BENCH_HW_QUEUES", "2")
+        env["GPU_MAX_HW_QUEUES"] = env.get("CLOCK_BENCH_HW_QUEUES", "2")
     if transport == "tcp":
         env["GEEPS_TRANSPORT"] = "tcp"
     else:
@@ -95,17 +101,32 @@ def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900, extra_en
         if pr.returncode != 0:
             errors.append(f"process {p} rc={pr.returncode}\n{e[-2000:]}")
             continue
-        results.append(json.loads(o.strip().splitlines()[-1]))
+        r = json.loads(o.strip().splitlines()[-1])
+        for line in e.splitlines():
+            if line.startswith("stats "):
+                r["stats"] = json.loads(line[6:])
+        results.append(r)
     if errors:
         raise RuntimeError("\n".join(errors))
     worst = max(r["ms_per_clock"] for r in results)
     table = results[0]["table_bytes"]
-    return {"workers": P, "rows": rows, "table_bytes": table, "slack": slack,
-            "transport": transport, "clocks": clocks, "warmup": warmup,
-            "ms_per_clock_max": worst,
-            "ms_per_clock": [r["ms_per_clock"] for r in results],
-            "aggregate_delta_GBps": round(P * table / (worst * 1e-3) / 1e9, 2),
-            "probe": [r["probe"] for r in results]}
+    out = {"workers": P, "rows": rows, "table_bytes": table, "slack": slack,
+           "transport": transport, "clocks": clocks, "warmup": warmup,
+           "ms_per_clock_max": worst,
+           "ms_per_clock": [r["ms_per_clock"] for r in results],
+           "aggregate_delta_GBps": round(P * table / (worst * 1e-3) / 1e9, 2),
+           "probe": [r["probe"] for r in results],
+           "devices": [r.get("device", 0) for r in results],
+           "read_checked": sum(r.get("read_checked", 0) for r in results),
+           "read_bad": sum(r.get("read_bad", 0) for r in results)}
+    out["read_ok"] = out["read_bad"] == 0 and out["read_checked"] > 0
+    st = [r["stats"] for r in results if "stats" in r]
+    if st:
+        out["nr_peer_staged"] = sum(srv["nr_peer_staged"] for s in st for srv in s["servers"])
+        out["nr_refresh_staged"] = sum(s["client"]["nr_refresh_staged"] for s in st)
+        out["nr_refresh_in_place"] = sum(s["client"]["nr_refresh_in_place"] for s in st)
+        out["nr_read_direct"] = sum(s["client"]["nr_read_direct"] for s in st)
+    return out
 
 
 def main():

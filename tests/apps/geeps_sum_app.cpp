@@ -64,6 +64,19 @@ static float delta(int p, int c, size_t e, bool fl) {
   return (float)(1 + ((p * 7 + c * 3 + e) % 5));  // 1..5
 }
 
+// GEEPS_TEST_ASYNC_READ=<n>: each Read buffer is copied by two kernels on the
+// null stream, queued right after Read and never waited for before PostRead: a
+// plain copy, then one that first sleeps n x s_sleep(127) (~3.4 us each) and
+// copies again.  Both read the buffer before PostRead in stream order, so the
+// two copies must be identical: a direct Read's master version may not go back
+// to its server (which could then rewrite it) before the app's queued device
+// work on it is done.
+__global__ void copy_kernel(float *dst, const float *src, size_t n, int sleeps) {
+  for (int i = 0; i < sleeps; ++i) __builtin_amdgcn_s_sleep(127);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
 #define HCK(x)                                                     \
   do {                                                             \
     hipError_t e_ = (x);                                           \
@@ -121,6 +134,12 @@ int main(int argc, char **argv) {
   cfg.num_comm_channels = channels;
   cfg.read_my_writes = rmw;
   cfg.gpu_memory_capacity = (size_t)1 << 34;
+  // GEEPS_TEST_CAPACITY=<bytes>: a tight capacity with mm_warning_level 2, so
+  // FinishVirtualIteration must refuse (libgeeps has no CPU param-cache tier)
+  if (const char *cap = std::getenv("GEEPS_TEST_CAPACITY")) {
+    cfg.gpu_memory_capacity = std::strtoull(cap, nullptr, 10);
+    cfg.mm_warning_level = 2;
+  }
   GeePs *ps = new GeePs(pid, cfg);
 
   size_t total = 0;
@@ -187,6 +206,16 @@ int main(int argc, char **argv) {
   // PostRead and must not have changed (a direct Read's master version stays
   // pinned while refreshes arrive).
   const bool reread = std::getenv("GEEPS_TEST_REREAD") != nullptr;
+  const char *async_env = std::getenv("GEEPS_TEST_ASYNC_READ");
+  const bool async_read = async_env != nullptr;
+  const int async_sleeps = async_read ? std::atoi(async_env) : 0;
+  float *dev_got = nullptr, *dev_got2 = nullptr;
+  hipStream_t fill_stream = nullptr;  // async mode: fills that do not wait for the null stream
+  if (async_read) {
+    HCK(hipMalloc(&dev_got, n * 4));
+    HCK(hipMalloc(&dev_got2, n * 4));
+    HCK(hipStreamCreateWithFlags(&fill_stream, hipStreamNonBlocking));
+  }
   int bad = 0;
   // PreUpdate -> fill on the device -> [PostRead] -> Update, in declared order.
   auto push = [&](int c, bool post_read) {
@@ -198,8 +227,13 @@ int main(int argc, char **argv) {
         for (size_t v = 0; v < ROW_DATA_SIZE; ++v)
           host[e0 + j * ROW_DATA_SIZE + v] =
               delta(pid, c, e0 + upd_row[l][j] * ROW_DATA_SIZE + v, fl);
-      HCK(hipMemcpy(buf, host.data() + e0, ne * 4, hipMemcpyHostToDevice));
-      if (post_read && reread) {
+      if (async_read) {
+        HCK(hipMemcpyAsync(buf, host.data() + e0, ne * 4, hipMemcpyHostToDevice, fill_stream));
+        HCK(hipStreamSynchronize(fill_stream));
+      } else {
+        HCK(hipMemcpy(buf, host.data() + e0, ne * 4, hipMemcpyHostToDevice));
+      }
+      if (post_read && reread && !async_read) {
         again.resize(ne);
         HCK(hipMemcpy(again.data(), rbufs[l], ne * 4, hipMemcpyDeviceToHost));
         if (std::memcmp(again.data(), got.data() + e0, ne * 4) != 0 && bad < 5) {
@@ -264,7 +298,31 @@ int main(int argc, char **argv) {
       ps->Read(h_read[l], &rbuf);
       rbufs[l] = rbuf;
       const size_t e0 = first[l] * ROW_DATA_SIZE, ne = layer_rows[l] * ROW_DATA_SIZE;
-      HCK(hipMemcpy(got.data() + e0, rbuf, ne * 4, hipMemcpyDeviceToHost));
+      if (async_read) {
+        const float *src = reinterpret_cast<const float *>(rbuf);
+        hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, 0, dev_got + e0, src, ne, 0);
+        hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, 0, dev_got2 + e0, src, ne, async_sleeps);
+        HCK(hipGetLastError());
+      } else {
+        HCK(hipMemcpy(got.data() + e0, rbuf, ne * 4, hipMemcpyDeviceToHost));
+      }
+    }
+    if (async_read) {
+      // PostRead (inside push) while the copies may still run; then both copies
+      // of every buffer must agree
+      push(it, true);
+      HCK(hipDeviceSynchronize());
+      again.resize(n);
+      HCK(hipMemcpy(got.data(), dev_got, n * 4, hipMemcpyDeviceToHost));
+      HCK(hipMemcpy(again.data(), dev_got2, n * 4, hipMemcpyDeviceToHost));
+      for (size_t l = 0; l < L && bad < 5; ++l) {
+        const size_t e0 = first[l] * ROW_DATA_SIZE, ne = layer_rows[l] * ROW_DATA_SIZE;
+        if (std::memcmp(again.data() + e0, got.data() + e0, ne * 4) != 0) {
+          std::fprintf(stderr, "p%d it%d layer %zu: Read buffer changed under device work queued "
+                       "before PostRead\n", pid, it, l);
+          ++bad;
+        }
+      }
     }
     if (slack == 0 && !rmw) {
       const auto &e = sum_through(it - 1);
@@ -285,7 +343,7 @@ int main(int argc, char **argv) {
         }
       }
     }
-    push(it, true);
+    if (!async_read) push(it, true);
     if (use_local) ps->PostLocalAccess(h_local_post);
     jitter();
     ps->Clock();

@@ -734,9 +734,12 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
 def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
     """The plan cache keys on the index pointer but trusts no pointer: the same
     device tensor refilled with another permutation (same size, offsets,
-    limit) must give the new index's sums, not the cached order's; the entry is
-    replaced by a copy of the new index (no sort), the next call builds its
-    sorted order and the one after runs it."""
+    limit) must give the new index's sums, not the cached order's.  The first
+    call with the new content is a steady-state call: its device check finds
+    the change and only the gated op-order form runs (no host round trip); the
+    next call sees the check's host-visible word, drops the entry and keeps a
+    copy of the new index (no sort), the next builds its sorted order and the
+    one after runs it (VERDICT r03 #4)."""
     from geeps_amd import rowops
     rng = np.random.default_rng(99)
     W, n = 128, 40000  # 20 MiB of rows: a cached (unsorted) residual
@@ -752,7 +755,7 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
         ti.copy_(torch.from_numpy(idx))
         e = y.copy()
         oracle.add_rows_from_double_index(e, x, idx, (0, 0), W)
-        for call in range(3):
+        for call in range(4 if round_ else 3):
             ty = T(y, dev)
             rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W)
             torch.cuda.synchronize()
@@ -760,6 +763,43 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
             # one entry: the index's copy and its sorted residual (16 B a row each)
             assert _cache_entries() == (1, 2 * 16 * n), (round_, call)
         prev = idx
+
+
+def test_unplanned_steady_state_does_not_wait_for_the_device(analyzed, dev):
+    """once an index is planned and cached, an unplanned call
+    only queues work (the device check, then both gated outcomes): it must
+    return while the stream is still busy with earlier work, where the
+    round-3 form copied the check's result to the host and synced first.  The
+    results stay bit-exact, for an unchanged index and for one changed in
+    place behind the busy stream."""
+    from geeps_amd import rowops
+    if not hasattr(torch.cuda, "_sleep"):
+        pytest.skip("torch.cuda._sleep unavailable")
+    rng = np.random.default_rng(5)
+    W, n = 128, 40000
+    x = rng.standard_normal(n * W).astype(np.float32)
+    y = rng.standard_normal(n * W).astype(np.float32)
+    idx = np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64)
+    tx, ti = T(x, dev), torch.from_numpy(idx).to(dev)
+    for _ in range(3):  # first sighting, sort, steady state
+        rowops.add_rows_from_double_index_gpu(T(y, dev), tx, ti, n, (0, 0), W, validate=False)
+    torch.cuda.synchronize()
+    for changed in (False, True):
+        idx2 = idx.copy()
+        if changed:
+            idx2[[3, 11], 1] = idx2[[11, 3], 1]
+        e = y.copy()
+        oracle.add_rows_from_double_index(e, x, idx2, (0, 0), W)
+        ty, ti2 = T(y, dev), torch.from_numpy(idx2).to(dev)
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        torch.cuda._sleep(200_000_000)  # ~0.1 s of device time ahead of the call
+        ti.copy_(ti2)  # device to device, stream-ordered behind the sleep
+        rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W, validate=False)
+        busy = not stream.query()
+        torch.cuda.synchronize()
+        assert busy, "the steady-state call waited for the device"
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), changed
 
 
 @pytest.mark.parametrize("kind", ["identity", "permuted", "mixed"])
@@ -1225,8 +1265,10 @@ def test_unplanned_calls_fuzz(analyzed, dev, case):
     its plan cache, on fuzzed indexes (dense runs around the sweep threshold,
     short runs, scattered rows, in shuffled op order), row sizes, offsets and
     num_vals_limit: three scatter-adds (first call in op order, second builds
-    the sorted residual, third runs it), two inits and a gather, each bit for
-    bit against the oracle."""
+    the sorted residual, third runs it behind the device check), then two more
+    after two destinations of the index were swapped in place (the steady
+    state's gated op-order form, then the re-plan), three inits and a gather,
+    each bit for bit against the oracle."""
     from geeps_amd import rowops
     rng = np.random.default_rng(7000 + case)
     W = int(rng.choice([4, 64, 128, 132, 256]))
@@ -1246,10 +1288,23 @@ def test_unplanned_calls_fuzz(analyzed, dev, case):
         rowops.add_rows_from_double_index_gpu(ty, tx, ti, n_op, off, W, limit)
         torch.cuda.synchronize()
         assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add", case, call, W, off, limit)
+    # the same tensor, two destinations swapped (still distinct)
+    idx2 = idx.copy()
+    a, b = rng.choice(n_op, 2, replace=False)
+    idx2[[a, b], 1] = idx2[[b, a], 1]
+    ti.copy_(torch.from_numpy(idx2))
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx2, off, W, limit)
+    for call in range(2):
+        ty = T(y, dev)
+        rowops.add_rows_from_double_index_gpu(ty, tx, ti, n_op, off, W, limit)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("add changed", case, call, W, off, limit)
+    ti.copy_(torch.from_numpy(idx))
     e = y.copy()
     e.reshape(n_cache, W)[idx[:, 1] + off[1]] = 0.0
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
-    for call in range(2):
+    for call in range(3):
         ty = T(y, dev)
         rowops.init_rows_from_double_index_gpu(ty, tx, ti, n_op, off, W, limit)
         torch.cuda.synchronize()

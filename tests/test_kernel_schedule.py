@@ -44,7 +44,10 @@ SWEEP_SHAPES = ([(1, 14, 8, 0, 4)] + [(nb, 7, 1, 0, 8) for nb in range(2, 9)]
 
 @pytest.mark.parametrize("nb,rt,tg,zin,u", SWEEP_SHAPES)
 def test_sweep_kernel_keeps_burst_schedule(asm, nb, rt, tg, zin, u):
-    body = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi{nb}ELi{rt}ELi{tg}ELb{zin}ELi{u}EE")
+    # (the last template argument: GATED = false, the form every launch but
+    # the unplanned calls' steady state uses; GATED = true differs only by the
+    # gate test before this body)
+    body = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi{nb}ELi{rt}ELi{tg}ELb{zin}ELi{u}ELb0EE")
     loads = len(re.findall(r"global_load_dwordx4", body))
     full_drains = len(re.findall(r"s_waitcnt vmcnt\(0\)", body))
     streams = nb if zin else nb + 1
@@ -67,8 +70,22 @@ def test_wave_kernels_fit_their_occupancy(asm):
     limit-straddle path must not index register arrays at run time (that cost
     86-91 more VGPRs and halved the resident blocks; profiles/r02)."""
     for op, max_vgpr in ((0, 168), (1, 128), (3, 128)):  # add, gather, init at 128-float rows
-        # <f4, OP, 32 lanes, 8 rows, flat, MAP 0 (the production tile map)>
-        pat = rf"_ZN12_GLOBAL__N_115row_wave_kernelIDv4_fLi{op}ELi32ELi8ELi0ELi0EEE"
+        # <f4, OP, 32 lanes, 8 rows, flat, MAP 0 (the production tile map), not gated>
+        pat = rf"_ZN12_GLOBAL__N_115row_wave_kernelIDv4_fLi{op}ELi32ELi8ELi0ELi0ELb0EEE"
         name = re.search(rf"^({pat}\S*):", asm, re.M).group(1)
         n = int(re.search(rf"\.set {re.escape(name)}\.num_vgpr, (\d+)", asm).group(1))
         assert n <= max_vgpr, (op, n)
+
+
+@pytest.mark.parametrize("rt,tg,zin", [(14, 8, 0), (6, 4, 1), (6, 4, 0)])
+def test_gated_sweep_kernel_keeps_burst_schedule(asm, rt, tg, zin):
+    """The GATED = true forms (the unplanned calls' steady state, gp_reduce.hip
+    "Device-built plans") run the gate test, then the same body: the same
+    loads, and no more full drains than the plain form."""
+    plain = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi1ELi{rt}ELi{tg}ELb{zin}ELi4ELb0EE")
+    gated = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi1ELi{rt}ELi{tg}ELb{zin}ELi4ELb1EE")
+    for body in (plain, gated):
+        assert "scratch_" not in body
+    assert gated.count("global_load_dwordx4") == plain.count("global_load_dwordx4")
+    drains = lambda b: len(re.findall(r"s_waitcnt vmcnt\(0\)", b))
+    assert drains(gated) <= drains(plain) + 1

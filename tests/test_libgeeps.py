@@ -55,6 +55,15 @@ def test_libgeeps_exports_reference_symbol_set():
     assert not missing, missing
 
 
+def test_capacity_message_names_the_reference_cpu_tier():
+    """libgeeps keeps every row in HBM; past gpu_memory_capacity its message names
+    the reference's CPU placement it does not build (test_capacity_past_hbm_names_the_missing_cpu_tier runs it)."""
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    with open(LIB, "rb") as f:
+        blob = f.read()
+    assert b"no CPU param-cache tier" in blob and b"clientlib-viter.cpp:492-611" in blob
+
+
 def test_app_links_with_public_header_only(tmp_path):
     src = tmp_path / "app.cpp"
     src.write_text('#include "geeps.hpp"\nint main() { GeePsConfig c; (void)c;\n'
@@ -443,6 +452,74 @@ def test_direct_read(dev, P, mode, slack, channels, spec, delay_us):
         assert direct == reads  # one shard, one channel: every Read is direct
     else:
         assert all(d < r for d, r in zip(direct, reads))  # straddling blobs gather
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,slack,delay_us", [(2, 1, 0), (3, 2, 15000)])
+def test_direct_read_release_waits_for_queued_device_reads(dev, P, slack, delay_us):
+    """a direct Read's buffer is a master version, and the
+    app's device work that reads it is queued (null stream) before PostRead
+    and may still run after it.  The app here copies every Read buffer with two
+    null-stream kernels it never waits for before PostRead -- a plain copy,
+    then one that first sleeps ~7 ms -- and requires both copies to agree.  A
+    version replaced meanwhile may go back to its server (which may rewrite
+    it) only after the PostRead's event, so the late copy sees the same rows."""
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    base = _ports(P, 1)
+    extra = {"GEEPS_DIRECT_READ": "1", "GEEPS_TEST_ASYNC_READ": "2000"}
+    if delay_us:
+        extra["GEEPS_TEST_READER_DELAY_US"] = str(delay_us)
+    env = _env("ipc", jitter_us=500, extra=extra)
+    spec = "700,5,900,395"
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), "2000", "10", str(slack), "1", "0", "int",
+                     spec], env) for p in range(P)]
+    st = _stats(_collect(procs, 300))
+    assert all(s["client"]["nr_read_direct"] > 0 for s in st)
+
+
+@pytest.mark.gpu
+def test_direct_read_two_tables_lagging_readers_keep_version_cap_live(dev):
+    """P = 3, slack 1, direct Reads of two tables in one
+    clock, every reader taking refreshes 15 ms late.  A pinned version that a
+    refresh replaces goes back only at PostRead, on the app thread, which may
+    be blocked in a Read of the other table; a client therefore defers at most
+    one version per (server, table) and gathers instead of pinning a second
+    (nr_read_direct_capped).  The servers' version waits must end: no abort
+    (GEEPS_VERSION_WAIT_S = 60 in these tests), every Read within the SSP
+    bounds, and every server within its clients + 2 versions."""
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    P = 3
+    base = _ports(P, 1)
+    extra = {"GEEPS_DIRECT_READ": "1", "GEEPS_TEST_REREAD": "1", "GEEPS_TEST_READER_DELAY_US": "15000"}
+    env = _env("ipc", jitter_us=1500, extra=extra)
+    spec = "600,5,700,300,900,95"
+    rows = sum(int(x) for x in spec.split(","))
+    procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), "16", "1", "1", "0", "int", spec,
+                     "2"], env) for p in range(P)]
+    st = _stats(_collect(procs, 300))
+    print("direct / capped / deferred:", [(s["client"]["nr_read_direct"], s["client"]["nr_read_direct_capped"],
+                                           s["client"]["nr_read_pin_deferred"]) for s in st])
+    assert all(s["client"]["nr_read_direct"] > 0 for s in st)
+    assert all(srv["nr_versions"] <= 2 * (P + 2) for s in st for srv in s["servers"])  # 2 tables
+
+
+@pytest.mark.gpu
+def test_capacity_past_hbm_names_the_missing_cpu_tier(dev):
+    """Optional VERDICT r03 #8: a table past gpu_memory_capacity at
+    mm_warning_level 2 fails in FinishVirtualIteration with a message naming
+    the reference's CPU placement, which libgeeps does not build."""
+    if not os.path.exists(SUM_APP):
+        pytest.skip("geeps_sum_app not built")
+    base = _ports(1, 1)
+    pr = _spawn([SUM_APP, "0", "1", str(base), "512", "2", "0", "1", "0"],
+                _env("ipc", extra={"GEEPS_TEST_CAPACITY": "65536"}))
+    pr.wait(timeout=120)
+    pr.err_file.seek(0)
+    err = pr.err_file.read()
+    assert pr.returncode != 0
+    assert "no CPU param-cache tier" in err and "clientlib-viter.cpp:492-611" in err, err[-2000:]
 
 
 @pytest.mark.gpu
