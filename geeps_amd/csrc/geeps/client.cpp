@@ -35,6 +35,13 @@ double connect_timeout_s() {
 }
 constexpr int kWaitWarnMs = 12000;  // the reference's 12 s timed_wait warnings
 
+// GEEPS_IPC_LOG=1: one stderr line per IPC handle exported or mapped (which
+// buffer, where, how large), on both sides, to audit buffer lifetimes.
+bool ipc_log() {
+  static const bool on = std::getenv("GEEPS_IPC_LOG") != nullptr;
+  return on;
+}
+
 struct PinnedPool {
   std::vector<std::shared_ptr<PinnedArray<float>>> bufs;
   std::shared_ptr<PinnedArray<float>> get(size_t floats) {
@@ -276,6 +283,9 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
           void *p = nullptr;
           GP_CALL(gp_ipc_open_handle(&p, ref.handle));
           mapped[ref.buffer_id] = p;
+          if (ipc_log())
+            std::cerr << "libgeeps ipc map oplog: server " << process_id_ << " ch " << ch.id << " client "
+                      << client_id << " buffer " << ref.buffer_id << " -> " << p << "\n";
         }
         auto it = mapped.find(ref.buffer_id);
         GP_CHECK_MSG(it != mapped.end(), "unmapped oplog buffer " << ref.buffer_id);
@@ -356,6 +366,10 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
           GP_CHECK_MSG(!mapped.count(rv.version), "version " << rv.version << " mapped twice");
           GP_CALL(gp_ipc_open_handle(&ptr, rv.handle));
           mapped[rv.version] = ptr;
+          if (ipc_log())
+            std::cerr << "libgeeps ipc map version: client " << process_id_ << " ch " << ch.id << " server "
+                      << server_id << " table " << h.table_id << " version " << rv.version << " rows "
+                      << rv.num_rows << " -> " << ptr << "\n";
         } else {
           auto it = mapped.find(rv.version);
           GP_CHECK_MSG(it != mapped.end(), "unmapped master version " << rv.version);
@@ -406,6 +420,10 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
     GP_CALL(gp_ipc_get_handle(rv.handle, const_cast<float *>(r.device_rows)));
     rv.has_handle = 1;
     sent.insert(r.version);
+    if (ipc_log())
+      std::cerr << "libgeeps ipc export version: server " << process_id_ << " ch " << ch.id << " client "
+                << client_id << " table " << r.table_id << " version " << r.version << " rows " << r.num_rows
+                << " at " << r.device_rows << "\n";
   }
   sc_read_row_batch_msg_t h{};
   h.cmd = READ_ROW_BATCH;
@@ -981,7 +999,8 @@ std::shared_ptr<DeviceArray<float>> ClientLib::get_oplog(ParamCache &pc, iter_t 
       break;
     }
   if (!buf) {
-    pc.oplog_pool.push_back(std::make_shared<DeviceArray<float>>(pc.num_rows * ROW_DATA_SIZE));
+    // (a same-node server maps it over IPC: a whole allocation)
+    pc.oplog_pool.push_back(std::make_shared<DeviceArray<float>>(pc.num_rows * ROW_DATA_SIZE, kShared));
     buf = pc.oplog_pool.back();
     // a new buffer never shows uninitialised HBM: a direct-oplog PreUpdate
     // hands it to the app, and rows an app leaves unwritten then push zeros
@@ -1167,6 +1186,10 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
         GP_CALL(gp_ipc_get_handle(ref.handle, oplog->data()));
         ref.has_handle = 1;
         (*exported)[s] = 1;
+        if (ipc_log())
+          std::cerr << "libgeeps ipc export oplog: client " << process_id_ << " ch " << ch.id << " server " << s
+                    << " buffer " << ref.buffer_id << " at " << static_cast<void *>(oplog->data()) << " bytes "
+                    << oplog->bytes() << "\n";
       }
       const bool with_keys = !(*keys_sent)[s];
       send_to_server(ch, s, {Part{&h, sizeof h},

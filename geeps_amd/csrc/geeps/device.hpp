@@ -46,12 +46,18 @@ class Event {
   gp_event e_ = nullptr;
 };
 
-// A device (HBM) array of T.
+// A device (HBM) array of T.  `shared`: a buffer peers map over IPC (oplogs,
+// master versions), allocated whole (gp_malloc_device_shared: >= 2 MiB, never a
+// fragment of a block the runtime sub-allocates).
+struct SharedAlloc {};
+constexpr SharedAlloc kShared{};
+
 template <typename T>
 class DeviceArray {
  public:
   DeviceArray() = default;
   explicit DeviceArray(size_t n) { resize(n); }
+  DeviceArray(size_t n, SharedAlloc) : shared_(true) { resize(n); }
   ~DeviceArray() { release(); }
   DeviceArray(const DeviceArray &) = delete;
   DeviceArray &operator=(const DeviceArray &) = delete;
@@ -67,7 +73,10 @@ class DeviceArray {
     release();
     if (n) {
       void *p = nullptr;
-      GP_CALL(gp_malloc_device(&p, n * sizeof(T)));
+      if (shared_)
+        GP_CALL(gp_malloc_device_shared(&p, n * sizeof(T)));
+      else
+        GP_CALL(gp_malloc_device(&p, n * sizeof(T)));
       p_ = static_cast<T *>(p);
     }
     n_ = n;
@@ -80,6 +89,7 @@ class DeviceArray {
   void swap(DeviceArray &o) noexcept {
     std::swap(p_, o.p_);
     std::swap(n_, o.n_);
+    std::swap(shared_, o.shared_);
   }
   T *data() const { return p_; }
   size_t size() const { return n_; }
@@ -88,6 +98,7 @@ class DeviceArray {
  private:
   T *p_ = nullptr;
   size_t n_ = 0;
+  bool shared_ = false;
 };
 
 // Page-locked host memory (the reference's mallocHost, common-util.hpp).

@@ -302,7 +302,8 @@ int TabletServer::free_version(DataTable &t) {
       }
     }
     if (t.versions.size() < (size_t)num_clients_ + 2) {
-      t.versions.push_back(std::make_unique<DeviceArray<float>>(t.row_count * ROW_DATA_SIZE));
+      // (same-node clients map it over IPC: a whole allocation)
+      t.versions.push_back(std::make_unique<DeviceArray<float>>(t.row_count * ROW_DATA_SIZE, kShared));
       t.holders.emplace_back(num_clients_, 0);
       stats_.nr_versions++;
       return (int)t.versions.size() - 1;

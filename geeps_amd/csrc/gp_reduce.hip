@@ -123,16 +123,43 @@ struct BucketPtrs {
 // instantiation runs this test first and takes the Gate as its last argument;
 // GATED = false (the default, every other launch) compiles to the same code as
 // without it (tests/test_kernel_schedule.py checks the sweep kernel's schedule).
+// kGateIfSame: the cached plan's dense runs run only if the index is
+// unchanged.  kGateSelect (row kernels): always run -- on the launch's own
+// index (the cached sorted residual) if unchanged, else on `alt` (the call's
+// own index, its offsets, in op order): one launch serves both outcomes.
+enum GateMode : unsigned { kGateIfSame = 0, kGateSelect = 2 };
 struct Gate {
   const unsigned *word;
   unsigned gen;
-  unsigned run_if_changed;  // 0: the cached plan's launches; 1: the fallback's
+  unsigned mode;
+  const gp_double_index *alt;
+  size_t alt_rows;
+  uint64_t alt_off0, alt_off1;
 };
 
-__device__ __forceinline__ bool gate_closed(const Gate &g) {
-  const unsigned w = __hip_atomic_load(g.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (w == g.gen) != (g.run_if_changed != 0);  // block-uniform
+__device__ __forceinline__ bool gate_changed(const Gate &g) {
+  return __hip_atomic_load(g.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g.gen;  // block-uniform
 }
+
+__device__ __forceinline__ bool gate_closed(const Gate &g) {
+  return g.mode == kGateIfSame && gate_changed(g);
+}
+
+// A row kernel's GATED prologue: exit, or (select) switch to the alternative
+// index when the check found the call's index changed.
+#define GP_ROW_GATE(gate, index, num_rows, off0, off1)  \
+  do {                                                  \
+    if (gate.mode == kGateSelect) {                     \
+      if (gate_changed(gate)) {                         \
+        index = gate.alt;                               \
+        num_rows = gate.alt_rows;                       \
+        off0 = gate.alt_off0;                           \
+        off1 = gate.alt_off1;                           \
+      }                                                 \
+    } else if (gate_closed(gate)) {                     \
+      return;                                           \
+    }                                                   \
+  } while (0)
 
 // hipLaunchKernelGGL of kernel K, or of its GATED form GK with *g last.  C:
 // a compile-time condition for instantiating GK at all (only the forms the
@@ -749,9 +776,7 @@ __global__ __launch_bounds__(kBlock) void row_op_kernel(
     float *__restrict__ y, const float *__restrict__ x,
     const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
     uint64_t off1, size_t row_size, size_t vw, size_t limit, Gate gate = Gate{}) {
-  if constexpr (GATED) {
-    if (gate_closed(gate)) return;
-  }
+  if constexpr (GATED) GP_ROW_GATE(gate, index, num_rows, off0, off1);
   constexpr int kGroups = kBlock / LPR;
   const int lane = threadIdx.x % LPR;
   const size_t group = (size_t)blockIdx.x * kGroups + threadIdx.x / LPR;
@@ -928,9 +953,7 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
     const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
     uint64_t off1, size_t row_size, size_t vw, size_t limit, const SegArg<SEG> seg, Gate gate = Gate{}) {
-  if constexpr (GATED) {
-    if (gate_closed(gate)) return;
-  }
+  if constexpr (GATED) GP_ROW_GATE(gate, index, num_rows, off0, off1);
   static_assert((OP == kAssignTo && (SEG == kFlat || SEG == kSegX)) ||
                     ((OP == kAddFrom || OP == kInitFrom) && SEG == kFlat),
                 "gather (flat / segmented source) or flat scatter-add / init");
@@ -1482,7 +1505,7 @@ constexpr int kScanWaveTiles = 16;   // tiles per wave (17 loads in flight)
 constexpr int kMaxRunStarts = 512;   // run-start entries the scan records
 constexpr int kMaxDeviceRuns = 32;   // dense runs a call sweeps (the longest)
 constexpr size_t kSortMinBytes = 16u << 20;       // smaller residuals keep op order
-constexpr size_t kPlanCacheBytes = 4ull << 30;    // device memory of cached plans (LRU)
+std::atomic<size_t> g_plan_cache_bytes{4ull << 30};  // device memory of cached plans (LRU)
 constexpr size_t kPlanCacheEntries = 256;
 
 struct ScanHeader {
@@ -1617,35 +1640,74 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
 }
 
 // The steady state's check of a planned index seen again: whether every entry
-// still equals the cached copy (32 B read per entry, no tile analysis).  Each
-// thread holds 4 entries' loads in flight.  A wave that saw a difference
+// still equals the kept copy (no tile analysis).  Two forms of the copy:
+//   full     the 16-B entries (32 B read per entry);
+//   compact  when the kept index has id0 = base0 + position and id1 < 2^32
+//            (the reference's op buffers list their rows in order: id0 is
+//            the position, clientlib-viter.cpp:841), only id1 as 4 B: the
+//            check reads 20 B per entry and still compares all 128 bits.
+// Each thread holds 4 entries' loads in flight.  A wave that saw a difference
 // stores this call's generation into the call's gate word (the gated launches
 // behind it read it) and into the entry's host-visible word (the next call
 // drops the entry).  Plain vector stores, idempotent: no atomics needed.
 constexpr int kCmpPerThread = 4;
 constexpr unsigned kGateSlots = 64;  // gate words per entry: calls in flight on one entry
+template <bool COMPACT>
 __global__ __launch_bounds__(kBlock) void index_verify_kernel(const gp_double_index *__restrict__ idx,
-                                                              const gp_double_index *__restrict__ cached, size_t n,
+                                                              const void *__restrict__ kept, size_t n,
+                                                              const uint64_t *__restrict__ base0_word,
                                                               unsigned *__restrict__ gate_word,
                                                               unsigned *__restrict__ host_word, unsigned gen) {
   const size_t step = (size_t)gridDim.x * kBlock * kCmpPerThread;
+  const uint64_t base0 = COMPACT ? *base0_word : 0;
   bool differs = false;
   for (size_t base = (size_t)blockIdx.x * kBlock * kCmpPerThread + threadIdx.x; base < n; base += step) {
     gp_double_index a[kCmpPerThread], b[kCmpPerThread];
+    uint32_t c[kCmpPerThread];
 #pragma unroll
     for (int k = 0; k < kCmpPerThread; ++k) {  // clamped, unconditional: all loads in flight
       const size_t e = base + (size_t)k * kBlock;
       const size_t ec = e < n ? e : n - 1;
       a[k] = idx[ec];
-      b[k] = cached[ec];
+      if constexpr (COMPACT)
+        c[k] = static_cast<const uint32_t *>(kept)[ec];
+      else
+        b[k] = static_cast<const gp_double_index *>(kept)[ec];
     }
 #pragma unroll
-    for (int k = 0; k < kCmpPerThread; ++k) differs |= (a[k].id0 != b[k].id0) | (a[k].id1 != b[k].id1);
+    for (int k = 0; k < kCmpPerThread; ++k) {
+      if constexpr (COMPACT) {
+        const size_t ec = base + (size_t)k * kBlock < n ? base + (size_t)k * kBlock : n - 1;
+        differs |= (a[k].id0 != base0 + ec) | (a[k].id1 != (uint64_t)c[k]);
+      } else {
+        differs |= (a[k].id0 != b[k].id0) | (a[k].id1 != b[k].id1);
+      }
+    }
   }
   if (__any(differs) && (threadIdx.x & 63) == 0) {
     __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// The compact copy of an index (built with its sorted residual, on the second
+// call): id1 as 4 B per entry and base0 = id0 of entry 0; `host_broken` set
+// when the index is not of that shape (then the full copy stays in use).
+__global__ __launch_bounds__(kBlock) void compact_copy_kernel(const gp_double_index *__restrict__ idx, size_t n,
+                                                              uint32_t *__restrict__ id1_out,
+                                                              uint64_t *__restrict__ base0_out,
+                                                              unsigned *__restrict__ host_broken) {
+  const uint64_t base0 = idx[0].id0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *base0_out = base0;
+  bool bad = false;
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += stride) {
+    const gp_double_index v = idx[e];
+    bad |= (v.id0 != base0 + e) | ((v.id1 >> 32) != 0);
+    id1_out[e] = (uint32_t)v.id1;
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0)
+    __hip_atomic_store(host_broken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Residual rows of a call: up to kMaxDeviceRuns + 1 entry ranges, passed by
@@ -1806,11 +1868,18 @@ struct CachedPlan {
   size_t resid = 0;
   std::vector<DevRun> runs;    // with `sorted`: the index's dense runs (the rest is the residual)
   // with `sorted`, the steady state's gate: kGateSlots device words (call
-  // generation g uses word g % kGateSlots), the host-visible "the index
-  // changed" word, and the generation counter (0 never used)
+  // generation g uses word g % kGateSlots) then the compact copy's base0 (8
+  // B), the host-visible "the index changed" word, and the generation counter
+  // (0 never used)
   std::shared_ptr<DevBuf> gate;
   std::shared_ptr<PinnedWord> changed;
   std::atomic<unsigned> gen{0};
+  // with `sorted`: the compact copy (id1 as 4 B, index_verify_kernel), whether
+  // the index has that shape (host-visible, set by compact_copy_kernel), and
+  // what the host knows of it: -1 not yet (the build may still run), 0 no, 1 yes
+  std::shared_ptr<DevBuf> compact;
+  std::shared_ptr<PinnedWord> compact_broken;
+  std::atomic<int> compact_state{-1};
   hipEvent_t ready = nullptr;  // recorded once copy (and sorted) are built, on the building stream
   uint64_t last_use = 0;
   size_t bytes = 0;
@@ -1819,6 +1888,7 @@ struct CachedPlan {
     return sorted ? static_cast<const gp_double_index *>(sorted->p) : nullptr;
   }
   unsigned *gate_words() const { return static_cast<unsigned *>(gate->p); }
+  uint64_t *base0_word() const { return reinterpret_cast<uint64_t *>(gate_words() + kGateSlots); }
   ~CachedPlan() {
     if (!ready) return;
     int cur = -1;
@@ -1866,7 +1936,9 @@ void cache_insert(std::shared_ptr<CachedPlan> p) {
       for (auto &q : g_plan_cache) b += q->bytes;
       return b;
     };
-    while (g_plan_cache.size() > 1 && (g_plan_cache.size() > kPlanCacheEntries || total() > kPlanCacheBytes)) {
+    const size_t cap = g_plan_cache_bytes.load(std::memory_order_relaxed);
+    // (the newest entry stays even past the cap, unless the cap is 0)
+    while (g_plan_cache.size() > (cap ? 1u : 0u) && (g_plan_cache.size() > kPlanCacheEntries || total() > cap)) {
       auto lru = std::min_element(g_plan_cache.begin(), g_plan_cache.end(),
                                   [](const auto &a, const auto &b) { return a->last_use < b->last_use; });
       evicted.push_back(*lru);
@@ -1915,11 +1987,22 @@ int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_doub
   else
     p->sorted = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
   if (rc != GP_OK) return rc;
-  p->gate = std::make_shared<DevBuf>(kGateSlots * sizeof(unsigned), key.device, &rc);
+  p->gate = std::make_shared<DevBuf>(kGateSlots * sizeof(unsigned) + sizeof(uint64_t), key.device, &rc);
   if (rc != GP_OK) return rc;
   p->changed = std::make_shared<PinnedWord>(key.device, &rc);
   if (rc != GP_OK) return rc;
+  p->compact = std::make_shared<DevBuf>(key.n * sizeof(uint32_t), key.device, &rc);
+  if (rc != GP_OK) return rc;
+  p->compact_broken = std::make_shared<PinnedWord>(key.device, &rc);
+  if (rc != GP_OK) return rc;
+  p->bytes += key.n * sizeof(uint32_t);
   GP_HIP_TRY(hipMemsetAsync(p->gate->p, 0, kGateSlots * sizeof(unsigned), s));
+  {
+    const size_t g = std::max<size_t>(1, std::min((key.n + kBlock - 1) / kBlock, (size_t)num_cus() * 8));
+    hipLaunchKernelGGL(compact_copy_kernel, dim3((unsigned)g), dim3(kBlock), 0, s, idx, key.n,
+                       static_cast<uint32_t *>(p->compact->p), p->base0_word(), p->compact_broken->p);
+    GP_HIP_TRY(hipGetLastError());
+  }
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
   uint32_t *kv = nullptr;  // keys, values, sorted keys, sorted values
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&kv), 4 * resid * sizeof(uint32_t), s));
@@ -1986,18 +2069,34 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     unsigned gen = ++cached->gen;
     if (gen == 0) gen = ++cached->gen;  // 0 is the gate words' initial value
     unsigned *word = cached->gate_words() + gen % kGateSlots;
+    // the compact copy once its build is known to have finished (never waits)
+    int compact = cached->compact_state.load(std::memory_order_acquire);
+    if (compact < 0) {
+      const hipError_t q = hipEventQuery(cached->ready);
+      if (q == hipSuccess) {
+        compact = cached->compact_broken->load() ? 0 : 1;
+        cached->compact_state.store(compact, std::memory_order_release);
+      } else {
+        (void)hipGetLastError();  // "not ready" is not this call's error
+      }
+    }
     const size_t per_block = (size_t)kBlock * kCmpPerThread;
     const size_t grid = std::max<size_t>(1, std::min((n + per_block - 1) / per_block, (size_t)num_cus() * 8));
-    hipLaunchKernelGGL(index_verify_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, cached->copy_ptr(), n,
-                       word, cached->changed->p, gen);
+    if (compact == 1)
+      hipLaunchKernelGGL(index_verify_kernel<true>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx,
+                         cached->compact->p, n, cached->base0_word(), word, cached->changed->p, gen);
+    else
+      hipLaunchKernelGGL(index_verify_kernel<false>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx,
+                         cached->copy_ptr(), n, cached->base0_word(), word, cached->changed->p, gen);
     GP_HIP_TRY(hipGetLastError());
-    const Gate same{word, gen, 0}, changed{word, gen, 1};
+    // dense runs only if unchanged; one row launch for both outcomes: the
+    // sorted residual if unchanged, else every row of the call in op order
+    const Gate same{word, gen, kGateIfSame, nullptr, 0, 0, 0};
+    const Gate select{word, gen, kGateSelect, idx, n, off.id0, off.id1};
     int rc = launch_runs(cached->runs, &same);
     if (rc != GP_OK) return rc;
-    rc = launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
-                           /*sorted=*/true, &same);
-    if (rc != GP_OK) return rc;
-    return launch_row_op<OP>(y, x, idx, n, off, W, limit, s, /*sorted=*/false, &changed);
+    return launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
+                             /*sorted=*/true, &select);
   }
   const size_t scan_bytes = kScanWordsOff + groups * kScanWords * sizeof(uint64_t);
   char *ws = nullptr;
@@ -2168,6 +2267,24 @@ int gp_unplanned_cache_entries(size_t *entries, size_t *bytes) {
   *entries = g_plan_cache.size();
   *bytes = 0;
   for (auto &p : g_plan_cache) *bytes += p->bytes;
+  return GP_OK;
+}
+
+int gp_set_unplanned_cache_bytes(size_t max_bytes) {
+  g_plan_cache_bytes.store(max_bytes, std::memory_order_relaxed);
+  std::vector<std::shared_ptr<CachedPlan>> evicted;  // freed outside the lock
+  {
+    std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+    size_t total = 0;
+    for (auto &p : g_plan_cache) total += p->bytes;
+    while (!g_plan_cache.empty() && total > max_bytes) {
+      auto lru = std::min_element(g_plan_cache.begin(), g_plan_cache.end(),
+                                  [](const auto &a, const auto &b) { return a->last_use < b->last_use; });
+      total -= (*lru)->bytes;
+      evicted.push_back(*lru);
+      g_plan_cache.erase(lru);
+    }
+  }
   return GP_OK;
 }
 
@@ -2485,6 +2602,23 @@ int gp_malloc_device(void **ptr, size_t bytes) {
   return GP_OK;
 }
 
+// The HIP runtime sub-allocates device memory below 2 MiB from shared 2-MiB
+// blocks (two 1,024,000-B hipMallocs land at offsets 0 and 1,024,000 of one
+// block: scripts/probes/ipc_probe.py).  Exporting such a fragment over IPC
+// failed intermittently on MI355X (hipIpcGetMemHandle "invalid argument" in
+// one of six runs of 64 exports; ROCr's "IPC Attach: Invalid IPC handle" in
+// a libgeeps run with 1-MB buffers), whole allocations never did.  A buffer
+// meant for IPC is therefore an allocation of its own: at least 2 MiB, a
+// multiple of 2 MiB.
+constexpr size_t kIpcBlock = 2u << 20;
+
+int gp_malloc_device_shared(void **ptr, size_t bytes) {
+  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
+  *ptr = nullptr;
+  if (bytes == 0) return GP_OK;
+  return gp_malloc_device(ptr, (bytes + kIpcBlock - 1) / kIpcBlock * kIpcBlock);
+}
+
 int gp_free_device(void *ptr) {
   if (ptr) GP_HIP_TRY(hipFree(ptr));
   return GP_OK;
@@ -2596,6 +2730,19 @@ static std::mutex g_ipc_mu;
 int gp_ipc_get_handle(void *handle_out, void *device_base) {
   if (!handle_out || !device_base) return set_error(GP_ERR_INVALID, "null pointer");
   std::lock_guard<std::mutex> lk(g_ipc_mu);
+  // a handle names a whole allocation: an interior pointer would map the
+  // allocation's base in the peer, at the wrong rows
+  void *base = nullptr;
+  size_t bytes = 0;
+  GP_HIP_TRY(hipMemGetAddressRange(&base, &bytes, device_base));
+  if (base != device_base || bytes < kIpcBlock) {
+    char msg[200];
+    std::snprintf(msg, sizeof msg,
+                  "IPC export of %p: %s (allocation %p, %zu B); allocate it with gp_malloc_device_shared",
+                  device_base, base != device_base ? "not an allocation base" : "a sub-2-MiB fragment", base,
+                  bytes);
+    return set_error(GP_ERR_INVALID, msg);
+  }
   hipIpcMemHandle_t h;
   GP_HIP_TRY(hipIpcGetMemHandle(&h, device_base));
   std::memset(handle_out, 0, GP_IPC_HANDLE_BYTES);

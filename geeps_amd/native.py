@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 10  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 11  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -66,6 +66,7 @@ _SIGNATURES = {
     "gp_set_unplanned_min_bytes": (_i, [_sz]),
     "gp_unplanned_cache_clear": (_i, []),
     "gp_unplanned_cache_entries": (_i, [_c.POINTER(_sz), _c.POINTER(_sz)]),
+    "gp_set_unplanned_cache_bytes": (_i, [_sz]),
     "gp_scatter_add_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
@@ -96,6 +97,7 @@ _SIGNATURES = {
     "gp_set_device": (_i, [_i]),
     "gp_get_device": (_i, [_c.POINTER(_i)]),
     "gp_malloc_device": (_i, [_c.POINTER(_vp), _sz]),
+    "gp_malloc_device_shared": (_i, [_c.POINTER(_vp), _sz]),
     "gp_free_device": (_i, [_vp]),
     "gp_malloc_host": (_i, [_c.POINTER(_vp), _sz]),
     "gp_free_host": (_i, [_vp]),

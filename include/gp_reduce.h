@@ -14,7 +14,11 @@
  *     loops overflow past 2^31 elements: src/common/gpu-util/mkl_alternate.hpp:62,
  *     src/common/gpu-util/device_alternate.hpp:31-54);
  *   - calls are asynchronous on the given stream (the reference synchronises
- *     after every launch: src/common/row-op-util.cu:141); the caller syncs;
+ *     after every launch: src/common/row-op-util.cu:141); the caller syncs.
+ *     The one exception: a large unplanned row call (gp_scatter_add_rows and
+ *     kin, >= gp_set_unplanned_min_bytes) waits for its stream once on the
+ *     first two calls with an index (the device scan's summary); from the
+ *     third call with the same index on it is asynchronous too (ABI 11);
  *   - errors are returned as a status code (0 = GP_OK) with a thread-local
  *     message from gp_last_error(), instead of a glog FATAL abort
  *     (src/common/gpu-util/device_alternate.hpp:16-28).  The C++ layer above
@@ -42,7 +46,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 10
+#define GP_ABI_VERSION 11
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -71,10 +75,13 @@ int gp_set_unplanned_min_bytes(size_t min_bytes);
  * order once and keeps, for later calls with the same index (same pointer,
  * size, offsets, row size and limit, and the same content, which every such
  * call checks entry for entry on the device), a copy of the index and its
- * rows in destination order: 32 B of HBM per row, at most 4 GiB and 256
- * indexes, least recently used first out.  Clear it, or read its size. */
+ * rows in destination order (+ a 4-B compact copy of each entry's id1 once
+ * sorted): 32-36 B of HBM per row, at most 256 indexes and
+ * gp_set_unplanned_cache_bytes() of HBM (default 4 GiB; 0 keeps nothing),
+ * least recently used first out.  Clear it, read its size, or bound it. */
 int gp_unplanned_cache_clear(void);
 int gp_unplanned_cache_entries(size_t *entries, size_t *bytes);
+int gp_set_unplanned_cache_bytes(size_t max_bytes);
 
 /* ---------------------------------------------------------------------------
  * Row operations (client side).  Element (row r, value v) lives at
@@ -97,11 +104,13 @@ int gp_unplanned_cache_entries(size_t *entries, size_t *bytes);
  * plan themselves on the device (ABI 10): one pass over the index finds its
  * dense runs (moved like a row plan's, by the phase-separated sum kernels) and
  * whether the other rows' destinations ascend; if they do not, the rows run in
- * op order and a destination-sorted copy is kept for the next call with the
- * same index (gp_unplanned_cache_clear).  Such a call waits for the stream
- * once, for the index summary, as the reference's call waits at its end
- * (row-op-util.cu:141); smaller calls are fully asynchronous.  Same results
- * either way. */
+ * op order and the next call with the same index builds a destination-sorted
+ * copy of them (gp_unplanned_cache_clear).  These first two calls wait for the
+ * stream once, for the index summary, as the reference's call waits at its end
+ * (row-op-util.cu:141).  Later calls with the same index (ABI 11) do not: the
+ * device compares the index with the kept copy and runs the sorted form if it
+ * is unchanged, the op-order form if not, with no host round trip.  Smaller
+ * calls are fully asynchronous.  Same results every way. */
 int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
                         size_t num_rows, gp_double_index offset,
                         size_t row_size, size_t num_vals_limit, gp_stream s);
@@ -358,6 +367,12 @@ int gp_get_device(int *device);
  * contiguous first (steadier HBM rates for the streaming sums), plain
  * otherwise or when no contiguous range is left. */
 int gp_malloc_device(void **ptr, size_t bytes);
+/* A device buffer that may be exported over IPC (gp_ipc_get_handle): an
+ * allocation of its own, rounded up to a multiple of 2 MiB.  The runtime
+ * sub-allocates smaller device buffers from shared 2-MiB blocks, and exporting
+ * such a fragment is unreliable (ABI 11).  Free with
+ * gp_free_device. */
+int gp_malloc_device_shared(void **ptr, size_t bytes);
 int gp_free_device(void *ptr);
 int gp_malloc_host(void **ptr, size_t bytes); /* pinned (mallocHost) */
 int gp_free_host(void *ptr);
@@ -381,8 +396,10 @@ int gp_stream_wait_event(gp_stream s, gp_event e);
 int gp_device_pci_bus_id(int device, char *buf, int len);
 
 /* Inter-process device memory (same node; xGMI between MI355X devices):
- * export a hipMalloc'd allocation BASE as an opaque 64-byte handle, map a
- * peer's handle into this process (peer access enabled lazily), unmap. */
+ * export an allocation BASE of at least 2 MiB (gp_malloc_device_shared; an
+ * interior pointer or a sub-2-MiB fragment is refused with GP_ERR_INVALID) as
+ * an opaque 64-byte handle, map a peer's handle into this process (peer access
+ * enabled lazily), unmap. */
 #define GP_IPC_HANDLE_BYTES 64
 int gp_ipc_get_handle(void *handle_out, void *device_base);
 int gp_ipc_open_handle(void **device_ptr, const void *handle);

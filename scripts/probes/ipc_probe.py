@@ -17,6 +17,19 @@ a handle still opens, and still maps the exported bytes, when:
              threads do (no lock around the runtime's IPC calls).
   freed      an exported buffer is freed and its address range reused by a
              new allocation before the importer opens the old handle.
+  keep       as batch, but the importer keeps every mapping open (libgeeps
+             never closes a peer's oplog or version mapping while it runs);
+  mt_open    the importer opens the handles from 2 threads at once (pairs
+             of fragments of one 2-MiB block), keeping every mapping open,
+             no lock: libgeeps' reader threads of two channels and its
+             server-side reader threads map a peer's buffers concurrently;
+  mt_export  the exporter allocates and exports from 2 threads at once.
+  stress_frag / stress_whole
+             256 buffers of 1,024,000 B (fragments: two share a 2-MiB block)
+             or of 2 MiB (whole allocations, as gp_malloc_device_shared
+             makes them), each exported; failed exports are counted, not
+             raised; the importer maps the rest from 2 threads, keeping every
+             mapping open.  Failure counts per side.
 
 Each scenario runs as two fresh processes (exporter / importer, or two peers)
 that pass handles through files.  Output: one JSON line per scenario with
@@ -101,8 +114,8 @@ def get(d, name, timeout=30.0):
         return f.read()
 
 
-def open_and_check(h, raw, value, nbytes):
-    """Open a handle; return (ok, detail)."""
+def open_and_check(h, raw, value, nbytes, keep=False):
+    """Open a handle; return (ok, detail).  keep: leave the mapping open."""
     hd = IpcHandle()
     assert len(raw) == 64
     ctypes.memmove(ctypes.addressof(hd), raw, 64)
@@ -116,7 +129,8 @@ def open_and_check(h, raw, value, nbytes):
         if any(b != value for b in out):
             h.hipIpcCloseMemHandle(p)
             return False, f"mapped bytes {list(out)[:4]} at +{off}, exported {value}"
-    call(h, h.hipIpcCloseMemHandle(p), "close")
+    if not keep:
+        call(h, h.hipIpcCloseMemHandle(p), "close")
     return True, ""
 
 
@@ -138,6 +152,46 @@ def exporter(scn, d):
         put(d, "h0", export(h, p))
         put(d, "h1", export(h, p))
         put(d, "exported", b"2")
+    elif scn == "mt_export":
+        n = 64
+        out = [None] * n
+
+        def work(t):
+            for k in range(t, n, 2):
+                p, inf = alloc(h, size, 1 + k % 250)
+                keep.append(p)
+                out[k] = export(h, p)
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        for k in range(n):
+            put(d, f"h{k}", out[k])
+        put(d, "exported", str(n).encode())
+    elif scn.startswith("stress"):
+        n = 256
+        size = SMALL if scn == "stress_frag" else 2 << 20
+        fails = []
+        for k in range(n):
+            p, inf = alloc(h, size, 1 + k % 250)
+            keep.append(p)
+            try:
+                raw = export(h, p)
+            except RuntimeError as exc:
+                fails.append({"k": k, "why": str(exc), "ptr_mod_2MiB": inf["ptr"] % (2 << 20)})
+                raw = b""
+            put(d, f"h{k}", raw)
+        put(d, "exported", str(n).encode())
+        info.append({"export_failures": fails})
+    elif scn == "mt_open":
+        n = 64
+        for k in range(n):
+            p, inf = alloc(h, size, 1 + k % 250)
+            keep.append(p)
+            info.append(inf)
+            put(d, f"h{k}", export(h, p))
+        put(d, "exported", str(n).encode())
     elif scn == "freed":
         for k in range(n):
             p, inf = alloc(h, size, 1 + k)
@@ -167,6 +221,28 @@ def importer(scn, d):
     h = hip()
     n = int(get(d, "exported", timeout=60)) if not scn.startswith("seq") else 16
     results = []
+    if scn in ("mt_open", "mt_export") or scn.startswith("stress"):
+        raws = [get(d, f"h{k}") for k in range(n)]
+        nbytes = SMALL if scn != "stress_whole" else 2 << 20
+        go = threading.Barrier(2)
+
+        def work(t):
+            go.wait()
+            for k in range(t, n, 2):
+                if not raws[k]:
+                    continue  # its export failed
+                ok, why = open_and_check(h, raws[k], 1 + k % 250, nbytes, keep=True)
+                results.append({"k": k, "ok": ok, "why": why})
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(1 if scn == "mt_export" else 2)]
+        if scn == "mt_export":
+            go = threading.Barrier(1)
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        put(d, "done", b"1")
+        print(json.dumps({"role": "importer", "results": results}))
+        return
     for k in range(n):
         raw = get(d, f"h{k}")
         value = 7 if scn == "twice" else 1 + k
@@ -174,7 +250,7 @@ def importer(scn, d):
         if scn == "twice" and k == 1:
             break  # only the first handle, opened after the second export
         progress("open", k)
-        ok, why = open_and_check(h, raw, value, nbytes)
+        ok, why = open_and_check(h, raw, value, nbytes, keep=scn == "keep")
         progress("opened", k, ok, why)
         results.append({"k": k, "ok": ok, "why": why})
         if scn.startswith("seq"):
@@ -244,5 +320,6 @@ if __name__ == "__main__":
     elif len(sys.argv) > 1 and sys.argv[1] == "--peer":
         peer(sys.argv[2], sys.argv[3], int(sys.argv[4]))
     else:
-        for scn in sys.argv[1:] or ["seq_big", "seq", "batch_big", "batch", "twice", "bidir", "freed"]:
+        for scn in sys.argv[1:] or ["seq_big", "seq", "batch_big", "batch", "twice", "bidir", "freed", "keep",
+                                    "mt_open", "mt_export"]:
             run(scn)

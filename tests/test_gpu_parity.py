@@ -731,7 +731,8 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
     assert np.array_equal(bits(to.cpu().numpy()), bits(e)), ("gather", kind, W)
 
 
-def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
+@pytest.mark.parametrize("id0", ["position", "permuted"])
+def test_unplanned_plan_cache_checks_index_content(analyzed, dev, id0):
     """The plan cache keys on the index pointer but trusts no pointer: the same
     device tensor refilled with another permutation (same size, offsets,
     limit) must give the new index's sums, not the cached order's.  The first
@@ -739,7 +740,9 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
     the change and only the gated op-order form runs (no host round trip); the
     next call sees the check's host-visible word, drops the entry and keeps a
     copy of the new index (no sort), the next builds its sorted order and the
-    one after runs it (VERDICT r03 #4)."""
+    one after runs it.  id0 "position" (the op buffer's rows
+    in order, as the reference lists them) is checked against the compact
+    copy (id1 only), a permuted id0 against the full copy."""
     from geeps_amd import rowops
     rng = np.random.default_rng(99)
     W, n = 128, 40000  # 20 MiB of rows: a cached (unsorted) residual
@@ -748,7 +751,8 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
     tx = T(x, dev)
     ti = torch.empty((n, 2), dtype=torch.int64, device=dev)
     for round_ in range(3):
-        idx = np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64)
+        src = np.arange(n) if id0 == "position" else rng.permutation(n)
+        idx = np.stack([src, rng.permutation(n)], 1).astype(np.int64)
         if round_ == 2:  # one swapped pair: a single differing entry
             idx = prev.copy()
             idx[[5, n - 7], 1] = idx[[n - 7, 5], 1]
@@ -760,9 +764,39 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev):
             rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W)
             torch.cuda.synchronize()
             assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), (round_, call)
-            # one entry: the index's copy and its sorted residual (16 B a row each)
-            assert _cache_entries() == (1, 2 * 16 * n), (round_, call)
+            # one entry: the index's copy and its sorted residual (16 B a row
+            # each), once sorted also the compact copy (4 B a row)
+            assert _cache_entries() in ((1, 2 * 16 * n), (1, 2 * 16 * n + 4 * n)), (round_, call)
         prev = idx
+
+
+def test_unplanned_cache_capacity_bound(analyzed, dev):
+    """gp_set_unplanned_cache_bytes (ABI 11): the plan cache's HBM
+    is bounded by the caller.  At 0 nothing is kept (every call plans afresh,
+    in op order) and the sums stay exact; the default bound afterwards caches
+    again."""
+    from geeps_amd import native, rowops
+    rng = np.random.default_rng(11)
+    W, n = 128, 40000
+    x = rng.standard_normal(n * W).astype(np.float32)
+    y = rng.standard_normal(n * W).astype(np.float32)
+    idx = np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64)
+    tx, ti = T(x, dev), torch.from_numpy(idx).to(dev)
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, (0, 0), W)
+    try:
+        native.check(native.lib().gp_set_unplanned_cache_bytes(0), "gp_set_unplanned_cache_bytes")
+        for call in range(3):
+            ty = T(y, dev)
+            rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W)
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), call
+            assert _cache_entries() == (0, 0), call
+    finally:
+        native.check(native.lib().gp_set_unplanned_cache_bytes(4 << 30), "gp_set_unplanned_cache_bytes")
+    rowops.add_rows_from_double_index_gpu(T(y, dev), tx, ti, n, (0, 0), W)
+    torch.cuda.synchronize()
+    assert _cache_entries()[0] == 1
 
 
 def test_unplanned_steady_state_does_not_wait_for_the_device(analyzed, dev):

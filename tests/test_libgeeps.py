@@ -522,20 +522,45 @@ def test_capacity_past_hbm_names_the_missing_cpu_tier(dev):
     assert "no CPU param-cache tier" in err and "clientlib-viter.cpp:492-611" in err, err[-2000:]
 
 
+def _one_process_per_gpu(P, extra):
+    """configs[4]'s per-blob AlexNet table, slack 1, process p on GPU p % count
+    (GEEPS_TEST_SPREAD_DEVICES=1), every Read checked; returns the stats."""
+    rows, spec = _layer_spec(ALEXNET_BLOBS)
+    outs = _run_app_layers(P, rows, spec, clocks=4, slack=1, timeout=600, transport="ipc",
+                           extra_env=dict({"GEEPS_TEST_SPREAD_DEVICES": "1"}, **extra))
+    return _stats(outs)
+
+
 @pytest.mark.gpu
 def test_one_process_per_gpu(dev):
-    """One process per GPU (process p on device p % count), as on an 8-GPU
-    node: peers' buckets cross xGMI by the staged peer copy and refreshes are
-    read in place from the other GPUs' master versions.  Needs 2+ GPUs."""
+    """configs[2] / [4] through the drop-in, one process per GPU as on an 8-GPU
+    node (P = min(GPUs, 8)): the AlexNet table's per-blob ops over P shards at
+    slack 1.  With the defaults across GPUs, a peer's bucket is peer-copied
+    into the server's HBM over xGMI before the sum (nr_peer_staged) and a
+    peer server's refreshed shard is peer-copied into the client's cache once
+    per refresh (nr_refresh_staged); same-process shards are read in place.
+    Needs 2+ GPUs; test_one_process_per_gpu_rehearsal runs the same path on
+    one GPU."""
     import torch
     n = torch.cuda.device_count()
     if n < 2:
-        pytest.skip("one GPU on this box")
-    P = min(n, 4)
-    outs = _run_app(P, rows=1200, clocks=8, slack=1, channels=1, rmw=0, transport="ipc",
-                    extra_env={"GEEPS_TEST_SPREAD_DEVICES": "1"})
-    for s in _stats(outs):
+        pytest.skip("one GPU on this box (see test_one_process_per_gpu_rehearsal)")
+    for s in _one_process_per_gpu(min(n, 8), {}):
         assert all(srv["nr_peer_staged"] > 0 for srv in s["servers"])
+        assert s["client"]["nr_refresh_staged"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 4])
+def test_one_process_per_gpu_rehearsal(dev, P):
+    """The same configs[2] / [4] run with the cross-GPU data paths forced on
+    (GEEPS_STAGE_PEER_UPDATES=1, GEEPS_STAGE_PEER_REFRESH=1): on a one-GPU box
+    every process lands on GPU 0 and the staged copies are peer copies within
+    it, so the code an 8-GPU node runs (VERDICT r03 #2) runs here too."""
+    st = _one_process_per_gpu(P, {"GEEPS_STAGE_PEER_UPDATES": "1", "GEEPS_STAGE_PEER_REFRESH": "1"})
+    for s in st:
+        assert all(srv["nr_peer_staged"] > 0 for srv in s["servers"])
+        assert s["client"]["nr_refresh_staged"] > 0
 
 
 @pytest.mark.gpu
