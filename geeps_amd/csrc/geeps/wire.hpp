@@ -51,6 +51,7 @@
 #include <vector>
 
 #include "geeps-user-defined-types.hpp"
+#include "gp_reduce.h"
 
 // Clock value of a table nobody has clocked yet, and the largest clock
 // (src/common/internal-config.hpp:34-36).
@@ -111,7 +112,7 @@ struct sc_read_row_batch_msg_t {
 // HBM; TCP carries only these small control frames.
 // ---------------------------------------------------------------------------
 constexpr command_t kCmdRefreshAck = 101;  // client -> server: master version released
-constexpr uint32_t kIpcHandleBytes = 64;
+constexpr uint32_t kIpcHandleBytes = GP_IPC_HANDLE_BYTES;  // the C-ABI's opaque handle
 
 // 4th part of a CLOCK_WITH_UPDATES_BATCH whose rows stay in the client's oplog.
 // The RowKey part is sent on the first such message per (server, table) only:

@@ -33,8 +33,10 @@
 // Wave64 throughout: 256-thread workgroups = 4 waves, one per SIMD.
 
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -123,11 +125,15 @@ struct BucketPtrs {
 // instantiation runs this test first and takes the Gate as its last argument;
 // GATED = false (the default, every other launch) compiles to the same code as
 // without it (tests/test_kernel_schedule.py checks the sweep kernel's schedule).
-// kGateIfSame: the cached plan's dense runs run only if the index is
-// unchanged.  kGateSelect (row kernels): always run -- on the launch's own
-// index (the cached sorted residual) if unchanged, else on `alt` (the call's
-// own index, its offsets, in op order): one launch serves both outcomes.
-enum GateMode : unsigned { kGateIfSame = 0, kGateSelect = 2 };
+// kGateIfSame: run only if the word does not hold this call's generation (the
+// index is unchanged, the inverse map is sound); kGateIfChanged: only if it
+// does.  kGateSelect (row kernels): always run -- on the launch's own rows
+// (the cached sorted residual or inverse map) if unchanged, else on `alt` (the
+// call's own index, its offsets, in op order): one launch serves both.
+// `inv` (row_wave_kernel only): the launch walks destination rows 0 ..
+// num_rows - 1 through an inverse map, inv[to] = entry << 32 | from, ~0 = no
+// row (the unplanned calls' inverse plan), instead of reading `index`.
+enum GateMode : unsigned { kGateIfSame = 0, kGateIfChanged = 1, kGateSelect = 2 };
 struct Gate {
   const unsigned *word;
   unsigned gen;
@@ -135,6 +141,7 @@ struct Gate {
   const gp_double_index *alt;
   size_t alt_rows;
   uint64_t alt_off0, alt_off1;
+  const uint64_t *inv;
 };
 
 __device__ __forceinline__ bool gate_changed(const Gate &g) {
@@ -142,7 +149,7 @@ __device__ __forceinline__ bool gate_changed(const Gate &g) {
 }
 
 __device__ __forceinline__ bool gate_closed(const Gate &g) {
-  return g.mode == kGateIfSame && gate_changed(g);
+  return g.mode != kGateSelect && (g.mode == kGateIfSame) == gate_changed(g);
 }
 
 // A row kernel's GATED prologue: exit, or (select) switch to the alternative
@@ -953,7 +960,19 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     float *__restrict__ y, const float *__restrict__ x,
     const gp_double_index *__restrict__ index, size_t num_rows, uint64_t off0,
     uint64_t off1, size_t row_size, size_t vw, size_t limit, const SegArg<SEG> seg, Gate gate = Gate{}) {
-  if constexpr (GATED) GP_ROW_GATE(gate, index, num_rows, off0, off1);
+  const uint64_t *inv = nullptr;  // GATED: the inverse map walked instead of `index`
+  if constexpr (GATED) {
+    if (gate.mode == kGateSelect && gate_changed(gate)) {
+      index = gate.alt;
+      num_rows = gate.alt_rows;
+      off0 = gate.alt_off0;
+      off1 = gate.alt_off1;
+    } else if (gate_closed(gate)) {
+      return;
+    } else {
+      inv = gate.inv;
+    }
+  }
   static_assert((OP == kAssignTo && (SEG == kFlat || SEG == kSegX)) ||
                     ((OP == kAddFrom || OP == kInitFrom) && SEG == kFlat),
                 "gather (flat / segmented source) or flat scatter-add / init");
@@ -1003,17 +1022,29 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
     mdst = reinterpret_cast<uint64_t>(y + to * row_size);
     mwhole = ((OP == kAssignTo ? to : from) + 1) * row_size <= limit;
   };
+  // entry r of the rows walked: the index's, or (inverse map) destination row
+  // r and its source, offsets applied; a row the map does not list is dead
+  auto load = [&](size_t r, bool &live) {
+    if constexpr (GATED) {
+      if (inv) {
+        const uint64_t v = inv[r];
+        live = live && v != ~0ull;
+        return gp_double_index{v & 0xffffffffu, r};
+      }
+    }
+    return index[r];
+  };
   {
-    const bool live = t + wl < num_rows;
+    bool live = t + wl < num_rows;
     gp_double_index ix = {0, 0};
-    if (live) ix = index[t + wl];
+    if (live) ix = load(t + wl, live);
     resolve(ix, live);
   }
   for (; t < r1; t += lstride) {
     const size_t nr = t + lstride + wl;  // next tile's entry, in flight meanwhile
-    const bool nlive = MAP == 2 ? t + lstride < r1 && nr < num_rows : nr < num_rows;
+    bool nlive = MAP == 2 ? t + lstride < r1 && nr < num_rows : nr < num_rows;
     gp_double_index nix = {0, 0};
-    if (nlive) nix = index[nr];
+    if (nlive) nix = load(nr, nlive);
     const size_t rows_here = num_rows - t < 64 ? num_rows - t : 64;
     for (int i0 = 0; i0 < kRowsPerGroup; i0 += kRPG) {
       uint64_t sp[kRPG], dp[kRPG];
@@ -1025,6 +1056,7 @@ __global__ __launch_bounds__(kBlock) void row_wave_kernel(
         live[k] = (size_t)rt < rows_here;
         sp[k] = shfl64(msrc, rt);
         dp[k] = shfl64(mdst, rt);
+        if constexpr (GATED) live[k] = live[k] && dp[k] != 0;  // (an inverse map's unlisted row)
         all_whole = all_whole && (!live[k] || __shfl(mwhole, rt, 64));
       }
       if (all_whole) {  // group-uniform
@@ -1505,6 +1537,7 @@ constexpr int kScanWaveTiles = 16;   // tiles per wave (17 loads in flight)
 constexpr int kMaxRunStarts = 512;   // run-start entries the scan records
 constexpr int kMaxDeviceRuns = 32;   // dense runs a call sweeps (the longest)
 constexpr size_t kSortMinBytes = 16u << 20;       // smaller residuals keep op order
+constexpr size_t kInvSpread = 4;  // an inverse map may span up to 4 x its rows (+ 1 Mi)
 std::atomic<size_t> g_plan_cache_bytes{4ull << 30};  // device memory of cached plans (LRU)
 constexpr size_t kPlanCacheEntries = 256;
 
@@ -1754,6 +1787,59 @@ __global__ __launch_bounds__(kBlock) void residual_gather_kernel(const gp_double
   }
 }
 
+// The inverse map of a call's residual (the unplanned calls' inverse plan):
+// inv[to] = entry << 32 | from, offsets applied, over destination rows 0 ..
+// D - 1 (~0 = no residual row goes there; the caller fills it first).  Plain
+// stores: destinations are distinct by the calls' precondition, and
+// inverse_check_kernel then proves it (a repeated destination keeps one
+// entry's word, so another entry finds its own missing).  A source row past
+// 2^32 (a 4-B field) or a repeated destination stores this call's
+// generation into the gate word and the host-visible word: the map is then
+// unsound, the gated op-order launches run instead, and the next call drops
+// the plan.
+template <int OP>
+__global__ __launch_bounds__(kBlock) void inverse_scatter_kernel(const gp_double_index *__restrict__ idx, EntryRanges rr,
+                                                                 uint64_t off0, uint64_t off1,
+                                                                 uint64_t *__restrict__ inv,
+                                                                 unsigned *__restrict__ gate_word,
+                                                                 unsigned *__restrict__ host_word, unsigned gen) {
+  const size_t total = rr.pre[rr.count];
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  bool bad = false;
+  for (size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x; k < total; k += stride) {
+    const size_t e = range_entry(rr, k);
+    uint64_t f, t;
+    row_endpoints<OP>(idx[e], off0, off1, f, t);
+    bad |= (f >> 32) != 0;
+    inv[t] = ((uint64_t)e << 32) | (f & 0xffffffffu);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) {
+    __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <int OP>
+__global__ __launch_bounds__(kBlock) void inverse_check_kernel(const gp_double_index *__restrict__ idx, EntryRanges rr,
+                                                               uint64_t off0, uint64_t off1,
+                                                               const uint64_t *__restrict__ inv,
+                                                               unsigned *__restrict__ gate_word,
+                                                               unsigned *__restrict__ host_word, unsigned gen) {
+  const size_t total = rr.pre[rr.count];
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  bool bad = false;
+  for (size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x; k < total; k += stride) {
+    const size_t e = range_entry(rr, k);
+    uint64_t f, t;
+    row_endpoints<OP>(idx[e], off0, off1, f, t);
+    bad |= inv[t] != (((uint64_t)e << 32) | (f & 0xffffffffu));
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) {
+    __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Thread-local pinned landing buffer for the scan summary (a call's D2H is
 // complete, after its sync, before the same thread issues the next).
 struct PinnedScratch {
@@ -1803,20 +1889,23 @@ struct PlanKey {
   }
 };
 
-// Device memory freed with hipFree (which waits for the device, so kernels
-// already queued on it finish first) on the device it came from.
+// Device memory of a plan-cache entry, from the device's stream-ordered pool
+// (hipMallocAsync on the building call's stream: the pool keeps what it was
+// given, keep_pool_memory, so a first call's allocations do not stall it).
+// Freed only after the device is idle (~CachedPlan waits for it first),
+// back to the pool.
 struct DevBuf {
   void *p = nullptr;
   int device = 0;
-  DevBuf(size_t bytes, int dev, int *rc) : device(dev) {
-    *rc = hipMalloc(&p, bytes) == hipSuccess ? GP_OK : set_error(GP_ERR_HIP, "plan cache hipMalloc");
+  DevBuf(size_t bytes, int dev, hipStream_t s, int *rc) : device(dev) {
+    *rc = hipMallocAsync(&p, bytes, s) == hipSuccess ? GP_OK : set_error(GP_ERR_HIP, "plan cache hipMallocAsync");
   }
   ~DevBuf() {
     if (!p) return;
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != device) (void)hipSetDevice(device);
-    (void)hipFree(p);
+    (void)hipFreeAsync(p, nullptr);
     if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
   }
   DevBuf(const DevBuf &) = delete;
@@ -1827,27 +1916,51 @@ struct DevRun {
   uint64_t e0, rows, from, to;  // first entry, rows, endpoints of the first entry
 };
 
-// A host-visible word in pinned (fine-grained, coherent) host memory that a
-// kernel may store to.  Freed only after the device is idle: a check still in
-// flight may write it.
+// Host-visible words in pinned (fine-grained, coherent) host memory that
+// kernels store to: 64-B slots of one slab allocated once per process and
+// never freed (a check still in flight may write a slot; a slot is reused
+// only after its entry waited for the device, ~CachedPlan).
+struct PinnedSlots {
+  std::mutex mu;
+  char *base = nullptr;
+  std::vector<unsigned *> free_slots;
+  static constexpr size_t kSlots = 4096;
+  unsigned *take(int *rc) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!base) {
+      void *q = nullptr;
+      if (hipHostMalloc(&q, kSlots * 64, hipHostMallocCoherent) != hipSuccess || !q) {
+        *rc = set_error(GP_ERR_HIP, "plan cache hipHostMalloc");
+        return nullptr;
+      }
+      base = static_cast<char *>(q);
+      for (size_t i = kSlots; i-- > 0;) free_slots.push_back(reinterpret_cast<unsigned *>(base + 64 * i));
+    }
+    if (free_slots.empty()) {
+      *rc = set_error(GP_ERR_HIP, "plan cache: no host-visible slot left");
+      return nullptr;
+    }
+    unsigned *w = free_slots.back();
+    free_slots.pop_back();
+    *rc = GP_OK;
+    return w;
+  }
+  void give(unsigned *w) {
+    std::lock_guard<std::mutex> lk(mu);
+    free_slots.push_back(w);
+  }
+};
+PinnedSlots g_pinned_slots;
+
 struct PinnedWord {
   unsigned *p = nullptr;
   int device = 0;
   PinnedWord(int dev, int *rc) : device(dev) {
-    void *q = nullptr;
-    *rc = hipHostMalloc(&q, 64, hipHostMallocCoherent) == hipSuccess ? GP_OK
-                                                                      : set_error(GP_ERR_HIP, "plan cache hipHostMalloc");
-    p = static_cast<unsigned *>(q);
+    p = g_pinned_slots.take(rc);
     if (p) __atomic_store_n(p, 0u, __ATOMIC_RELEASE);
   }
   ~PinnedWord() {
-    if (!p) return;
-    int cur = -1;
-    (void)hipGetDevice(&cur);
-    if (cur != device) (void)hipSetDevice(device);
-    (void)hipDeviceSynchronize();
-    (void)hipHostFree(p);
-    if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
+    if (p) g_pinned_slots.give(p);
   }
   unsigned load() const { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
   PinnedWord(const PinnedWord &) = delete;
@@ -1880,6 +1993,10 @@ struct CachedPlan {
   std::shared_ptr<DevBuf> compact;
   std::shared_ptr<PinnedWord> compact_broken;
   std::atomic<int> compact_state{-1};
+  // an inverse plan (instead of `sorted`): the residual as an inverse map over
+  // destination rows 0 .. inv_rows - 1 (inverse_scatter_kernel)
+  std::shared_ptr<DevBuf> inv;
+  size_t inv_rows = 0;
   hipEvent_t ready = nullptr;  // recorded once copy (and sorted) are built, on the building stream
   uint64_t last_use = 0;
   size_t bytes = 0;
@@ -1887,13 +2004,24 @@ struct CachedPlan {
   const gp_double_index *sorted_ptr() const {
     return sorted ? static_cast<const gp_double_index *>(sorted->p) : nullptr;
   }
+  bool planned() const { return sorted || inv; }  // a steady-state entry
+  const uint64_t *inv_ptr() const { return static_cast<const uint64_t *>(inv->p); }
   unsigned *gate_words() const { return static_cast<unsigned *>(gate->p); }
   uint64_t *base0_word() const { return reinterpret_cast<uint64_t *>(gate_words() + kGateSlots); }
+  // Kernels of a call may still run on the device when an entry goes (it is
+  // dropped or evicted on the host): wait for them before any member frees
+  // what they read or write.
+  bool frees_memory() const {
+    auto last = [](const auto &b) { return b && b.use_count() == 1; };
+    return last(copy) || last(sorted) || last(spare) || last(gate) || last(compact) || last(inv) || changed ||
+           compact_broken;
+  }
   ~CachedPlan() {
     if (!ready) return;
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != key.device) (void)hipSetDevice(key.device);
+    if (frees_memory()) (void)hipDeviceSynchronize();
     (void)hipEventDestroy(ready);
     if (cur >= 0 && cur != key.device) (void)hipSetDevice(cur);
   }
@@ -1955,14 +2083,91 @@ int cache_first_sighting(const PlanKey &key, const gp_double_index *idx, size_t 
   p->resid = resid;
   p->bytes = (key.n + resid) * sizeof(gp_double_index);
   int rc = GP_OK;
-  p->copy = std::make_shared<DevBuf>(key.n * sizeof(gp_double_index), key.device, &rc);
+  p->copy = std::make_shared<DevBuf>(key.n * sizeof(gp_double_index), key.device, s, &rc);
   if (rc != GP_OK) return rc;
-  p->spare = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
+  p->spare = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, s, &rc);
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
   GP_HIP_TRY(hipMemcpyAsync(p->copy->p, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
   GP_HIP_TRY(hipEventRecord(p->ready, s));
   cache_insert(std::move(p));
+  return GP_OK;
+}
+
+// What a steady-state entry needs besides its plan: the gate words, the
+// host-visible "changed" word, and the compact copy of the index (built on s).
+int steady_state_setup(CachedPlan *p, const gp_double_index *idx, hipStream_t s) {
+  const PlanKey &key = p->key;
+  int rc = GP_OK;
+  p->gate = std::make_shared<DevBuf>(kGateSlots * sizeof(unsigned) + sizeof(uint64_t), key.device, s, &rc);
+  if (rc != GP_OK) return rc;
+  p->changed = std::make_shared<PinnedWord>(key.device, &rc);
+  if (rc != GP_OK) return rc;
+  p->compact = std::make_shared<DevBuf>(key.n * sizeof(uint32_t), key.device, s, &rc);
+  if (rc != GP_OK) return rc;
+  p->compact_broken = std::make_shared<PinnedWord>(key.device, &rc);
+  if (rc != GP_OK) return rc;
+  p->bytes += key.n * sizeof(uint32_t);
+  GP_HIP_TRY(hipMemsetAsync(p->gate->p, 0, kGateSlots * sizeof(unsigned), s));
+  const size_t g = std::max<size_t>(1, std::min((key.n + kBlock - 1) / kBlock, (size_t)num_cus() * 8));
+  hipLaunchKernelGGL(compact_copy_kernel, dim3((unsigned)g), dim3(kBlock), 0, s, idx, key.n,
+                     static_cast<uint32_t *>(p->compact->p), p->base0_word(), p->compact_broken->p);
+  GP_HIP_TRY(hipGetLastError());
+  return GP_OK;
+}
+
+// The first call with an index whose residual has no ascending order: the
+// inverse plan (for rows of up to 128 floats, destinations below 2^32 and not
+// too sparse, kInvSpread).  It keeps a copy of the index (for the steady
+// state's check), builds the inverse map of the residual on s (fill, scatter,
+// check: generation `*gen` marks it unsound) and returns the entry; the caller
+// launches the map's rows gated on soundness and the op-order residual gated
+// on the opposite.
+template <int OP>
+int cache_inverse_plan(const PlanKey &key, const gp_double_index *idx, const EntryRanges &rr,
+                       const std::vector<DevRun> &runs, size_t inv_rows, hipStream_t s,
+                       std::shared_ptr<CachedPlan> *built, unsigned *gen) {
+  auto p = std::make_shared<CachedPlan>();
+  p->key = key;
+  p->resid = rr.pre[rr.count];
+  p->runs = runs;
+  p->inv_rows = inv_rows;
+  p->bytes = key.n * sizeof(gp_double_index) + inv_rows * sizeof(uint64_t);
+  int rc = GP_OK;
+  p->copy = std::make_shared<DevBuf>(key.n * sizeof(gp_double_index), key.device, s, &rc);
+  if (rc != GP_OK) return rc;
+  p->inv = std::make_shared<DevBuf>(inv_rows * sizeof(uint64_t), key.device, s, &rc);
+  if (rc != GP_OK) return rc;
+  rc = steady_state_setup(p.get(), idx, s);
+  if (rc != GP_OK) return rc;
+  GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+  GP_HIP_TRY(hipMemcpyAsync(p->copy->p, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
+  GP_HIP_TRY(hipMemsetAsync(p->inv->p, 0xff, inv_rows * sizeof(uint64_t), s));
+  *gen = ++p->gen;
+  unsigned *word = p->gate_words() + *gen % kGateSlots;
+  const size_t grid = std::max<size_t>(1, std::min((p->resid + kBlock - 1) / kBlock, (size_t)num_cus() * 8));
+  uint64_t *inv = static_cast<uint64_t *>(p->inv->p);
+  hipLaunchKernelGGL(inverse_scatter_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, rr, key.off0,
+                     key.off1, inv, word, p->changed->p, *gen);
+  hipLaunchKernelGGL(inverse_check_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, rr, key.off0,
+                     key.off1, inv, word, p->changed->p, *gen);
+  GP_HIP_TRY(hipGetLastError());
+  GP_HIP_TRY(hipEventRecord(p->ready, s));
+  *built = p;
+  cache_insert(std::move(p));
+  return GP_OK;
+}
+
+// The inverse plan's rows: row_wave_kernel walking destination rows 0 ..
+// inv_rows - 1 through the map (Gate::inv), offsets already applied.
+template <int OP>
+int launch_inverse_rows(float *y, const float *x, const CachedPlan &p, size_t W, size_t limit, hipStream_t s,
+                        Gate g) {
+  g.inv = p.inv_ptr();
+  // (`index` is not read in this form: the map's pointer stands in for it)
+  launch_row_op_t<f4, 4, OP, kFlat>(y, x, reinterpret_cast<const gp_double_index *>(p.inv_ptr()), p.inv_rows, 0, 0,
+                                    W, limit, SegArg<kFlat>{}, /*sorted=*/true, s, &g);
+  GP_HIP_TRY(hipGetLastError());
   return GP_OK;
 }
 
@@ -1985,24 +2190,10 @@ int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_doub
   if (seen->spare)
     p->sorted = seen->spare;  // written only here: no call reads a copy-only entry's spare
   else
-    p->sorted = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, &rc);
+    p->sorted = std::make_shared<DevBuf>(resid * sizeof(gp_double_index), key.device, s, &rc);
   if (rc != GP_OK) return rc;
-  p->gate = std::make_shared<DevBuf>(kGateSlots * sizeof(unsigned) + sizeof(uint64_t), key.device, &rc);
+  rc = steady_state_setup(p.get(), idx, s);
   if (rc != GP_OK) return rc;
-  p->changed = std::make_shared<PinnedWord>(key.device, &rc);
-  if (rc != GP_OK) return rc;
-  p->compact = std::make_shared<DevBuf>(key.n * sizeof(uint32_t), key.device, &rc);
-  if (rc != GP_OK) return rc;
-  p->compact_broken = std::make_shared<PinnedWord>(key.device, &rc);
-  if (rc != GP_OK) return rc;
-  p->bytes += key.n * sizeof(uint32_t);
-  GP_HIP_TRY(hipMemsetAsync(p->gate->p, 0, kGateSlots * sizeof(unsigned), s));
-  {
-    const size_t g = std::max<size_t>(1, std::min((key.n + kBlock - 1) / kBlock, (size_t)num_cus() * 8));
-    hipLaunchKernelGGL(compact_copy_kernel, dim3((unsigned)g), dim3(kBlock), 0, s, idx, key.n,
-                       static_cast<uint32_t *>(p->compact->p), p->base0_word(), p->compact_broken->p);
-    GP_HIP_TRY(hipGetLastError());
-  }
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
   uint32_t *kv = nullptr;  // keys, values, sorted keys, sorted values
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&kv), 4 * resid * sizeof(uint32_t), s));
@@ -2038,7 +2229,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   std::shared_ptr<CachedPlan> cached = OP == kAssignTo ? nullptr : cache_find(key);
   // a steady-state call since the last host look found the index changed: the
   // entry is stale, plan this call afresh (scan, host round trip)
-  if (cached && cached->sorted && cached->changed->load() != 0) {
+  if (cached && cached->planned() && cached->changed->load() != 0) {
     cache_drop(cached);
     cached.reset();
   }
@@ -2060,7 +2251,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     }
     return (int)GP_OK;
   };
-  if (cached && cached->sorted) {
+  if (cached && cached->planned()) {
     // The steady state: a planned index seen again.  Check it against the copy
     // and launch both outcomes behind the check, each gated on its result:
     // the cached dense runs and sorted residual (unchanged), or this call's
@@ -2091,10 +2282,11 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     GP_HIP_TRY(hipGetLastError());
     // dense runs only if unchanged; one row launch for both outcomes: the
     // sorted residual if unchanged, else every row of the call in op order
-    const Gate same{word, gen, kGateIfSame, nullptr, 0, 0, 0};
-    const Gate select{word, gen, kGateSelect, idx, n, off.id0, off.id1};
+    const Gate same{word, gen, kGateIfSame, nullptr, 0, 0, 0, nullptr};
+    const Gate select{word, gen, kGateSelect, idx, n, off.id0, off.id1, nullptr};
     int rc = launch_runs(cached->runs, &same);
     if (rc != GP_OK) return rc;
+    if (cached->inv) return launch_inverse_rows<OP>(y, x, *cached, W, limit, s, select);
     return launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
                              /*sorted=*/true, &select);
   }
@@ -2205,6 +2397,27 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   // it (one radix sort, about what sorting saves in one call) and runs it
   const bool sortable = OP != kAssignTo && !ascending && resid * W * sizeof(float) >= kSortMinBytes &&
                         max_dst < (1ull << 32) && n < (1ull << 32);
+  // the inverse plan: rows of up to 128 floats (the wave kernel's shapes),
+  // destinations not too sparse for a map over 0 .. max_dst
+  const size_t inv_rows = (size_t)max_dst + 1;
+  const bool inverse = sortable && !cached && W / 4 <= 32 && inv_rows <= kInvSpread * resid + (1u << 20);
+  if (inverse) {
+    std::shared_ptr<CachedPlan> built;
+    unsigned gen = 0;
+    int rc = cache_inverse_plan<OP>(key, idx, rr, runs, inv_rows, s, &built, &gen);
+    if (rc != GP_OK) return rc;
+    unsigned *word = built->gate_words() + gen % kGateSlots;
+    // the map's rows if it is sound, else the residual in op order (as the
+    // calls before ABI 11 ran it)
+    rc = launch_inverse_rows<OP>(y, x, *built, W, limit, s, Gate{word, gen, kGateIfSame, nullptr, 0, 0, 0, nullptr});
+    if (rc != GP_OK) return rc;
+    const Gate unsound{word, gen, kGateIfChanged, nullptr, 0, 0, 0, nullptr};
+    for (uint32_t i = 0; i < rr.count; ++i) {
+      rc = launch_row_op<OP>(y, x, idx + rr.lo[i], rr.hi[i] - rr.lo[i], off, W, limit, s, ascending, &unsound);
+      if (rc != GP_OK) return rc;
+    }
+    return GP_OK;
+  }
   if (sortable && cached && !cached->sorted && cached->resid == resid) {
     std::shared_ptr<CachedPlan> built;
     const int rc = cache_second_sighting<OP>(cached, idx, rr, runs, max_dst, s, &built);
@@ -2602,21 +2815,47 @@ int gp_malloc_device(void **ptr, size_t bytes) {
   return GP_OK;
 }
 
-// The HIP runtime sub-allocates device memory below 2 MiB from shared 2-MiB
-// blocks (two 1,024,000-B hipMallocs land at offsets 0 and 1,024,000 of one
-// block: scripts/probes/ipc_probe.py).  Exporting such a fragment over IPC
-// failed intermittently on MI355X (hipIpcGetMemHandle "invalid argument" in
-// one of six runs of 64 exports; ROCr's "IPC Attach: Invalid IPC handle" in
-// a libgeeps run with 1-MB buffers), whole allocations never did.  A buffer
-// meant for IPC is therefore an allocation of its own: at least 2 MiB, a
-// multiple of 2 MiB.
+// A buffer meant for IPC (gp_ipc_get_handle) is an allocation of its own,
+// rounded up to a multiple of 2 MiB, whose last kIpcTagBytes hold a tag that
+// the export writes and every mapping checks.  On MI355X (ROCm 7.2,
+// scripts/probes/ipc_probe.py) a process's FIRST device allocation could not
+// always be exported: in some runs hipIpcGetMemHandle refused it ("invalid
+// argument", persistently), in one run the export succeeded and the peer's
+// mapping held other memory, not the exported bytes; every later allocation
+// exported and mapped correctly in thousands of tries.  libgeeps' one failure
+// of this kind (ROCr "IPC Attach: Invalid IPC handle! X and Y", round 3) was
+// on the mapping side.  The tag turns a mapping of the wrong memory into a
+// loud error instead of silently wrong rows.
 constexpr size_t kIpcBlock = 2u << 20;
+constexpr size_t kIpcTagBytes = 256;  // the tag's slot at the end of the allocation
+
+static std::mutex g_ipc_prime_mu;
+static bool g_ipc_primed[kMaxDevices];  // g_ipc_prime_mu
 
 int gp_malloc_device_shared(void **ptr, size_t bytes) {
   if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
   *ptr = nullptr;
   if (bytes == 0) return GP_OK;
-  return gp_malloc_device(ptr, (bytes + kIpcBlock - 1) / kIpcBlock * kIpcBlock);
+  // Before a device's first shareable buffer: one throwaway export, so no
+  // real buffer is the process's first export (or older than it) -- the
+  // buffers the probe saw fail (not yet validated on its own: that run's box
+  // was lost)
+  int dev = 0;
+  GP_HIP_TRY(hipGetDevice(&dev));
+  if (dev >= 0 && dev < kMaxDevices) {
+    std::lock_guard<std::mutex> lk(g_ipc_prime_mu);
+    if (!g_ipc_primed[dev]) {
+      g_ipc_primed[dev] = true;
+      void *d = nullptr;
+      if (hipMalloc(&d, kIpcBlock) == hipSuccess) {
+        hipIpcMemHandle_t h;
+        (void)hipIpcGetMemHandle(&h, d);
+        (void)hipFree(d);
+      }
+      (void)hipGetLastError();  // a refused throwaway export is expected, not this call's error
+    }
+  }
+  return gp_malloc_device(ptr, (bytes + kIpcTagBytes + kIpcBlock - 1) / kIpcBlock * kIpcBlock);
 }
 
 int gp_free_device(void *ptr) {
@@ -2716,16 +2955,44 @@ int gp_device_pci_bus_id(int device, char *buf, int len) {
   return GP_OK;
 }
 
-static_assert(sizeof(hipIpcMemHandle_t) <= GP_IPC_HANDLE_BYTES, "IPC handle size");
+// The handle as it crosses the C-ABI: the runtime's handle, then where the
+// allocation's tag lies (bytes from its base) and the tag itself.
+struct IpcHandleOut {
+  hipIpcMemHandle_t h;
+  uint64_t tag_offset;
+  uint64_t tag[2];
+};
+static_assert(sizeof(IpcHandleOut) <= GP_IPC_HANDLE_BYTES, "IPC handle size");
+constexpr uint64_t kIpcTagMagic = 0x6770495043746167ull;  // "gpIPCtag"
 
-// One process's IPC calls run one at a time.  libgeeps exports and maps from
-// several threads (a server thread exporting master versions, reader threads
-// mapping a peer's versions and oplogs).  One GPU run saw hipIpcOpenMemHandle
-// reject a handle once ("IPC Attach: Invalid IPC handle",
-// profiles/r03/e2e/pytest_libgeeps_race.log, test_shuffled_update_rows) and not
-// in any rerun; a concurrent call is not proven to be the cause, so this lock
-// is a precaution (the calls run once per buffer).
+// One process's IPC calls run one at a time (libgeeps exports and maps from
+// several threads: server threads export master versions, reader threads map
+// a peer's versions and oplogs); they run once per buffer.
 static std::mutex g_ipc_mu;
+static hipStream_t g_ipc_stream[kMaxDevices];  // g_ipc_mu: the tag copies' stream per device
+
+static int ipc_stream(hipStream_t *s) {
+  int dev = 0;
+  GP_HIP_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) return set_error(GP_ERR_INVALID, "device id out of range");
+  if (!g_ipc_stream[dev]) GP_HIP_TRY(hipStreamCreateWithFlags(&g_ipc_stream[dev], hipStreamNonBlocking));
+  *s = g_ipc_stream[dev];
+  return GP_OK;
+}
+
+// The allocation's tag: the same for every export of it, distinct per process,
+// allocation and size.
+static void ipc_tag(const void *base, size_t bytes, uint64_t tag[2]) {
+  static const uint64_t salt = [] {
+    uint64_t x = (uint64_t)getpid() * 0x9e3779b97f4a7c15ull;
+    x ^= (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    return x;
+  }();
+  uint64_t h = salt ^ (reinterpret_cast<uintptr_t>(base) * 0xbf58476d1ce4e5b9ull) ^ (bytes * 0x94d049bb133111ebull);
+  h ^= h >> 31;
+  tag[0] = kIpcTagMagic;
+  tag[1] = h;
+}
 
 int gp_ipc_get_handle(void *handle_out, void *device_base) {
   if (!handle_out || !device_base) return set_error(GP_ERR_INVALID, "null pointer");
@@ -2735,27 +3002,58 @@ int gp_ipc_get_handle(void *handle_out, void *device_base) {
   void *base = nullptr;
   size_t bytes = 0;
   GP_HIP_TRY(hipMemGetAddressRange(&base, &bytes, device_base));
-  if (base != device_base || bytes < kIpcBlock) {
+  if (base != device_base || bytes < kIpcBlock || bytes % kIpcBlock) {
     char msg[200];
     std::snprintf(msg, sizeof msg,
                   "IPC export of %p: %s (allocation %p, %zu B); allocate it with gp_malloc_device_shared",
-                  device_base, base != device_base ? "not an allocation base" : "a sub-2-MiB fragment", base,
-                  bytes);
+                  device_base, base != device_base ? "not an allocation base" : "not a gp_malloc_device_shared buffer",
+                  base, bytes);
     return set_error(GP_ERR_INVALID, msg);
   }
-  hipIpcMemHandle_t h;
-  GP_HIP_TRY(hipIpcGetMemHandle(&h, device_base));
+  IpcHandleOut out{};
+  out.tag_offset = bytes - kIpcTagBytes;
+  ipc_tag(base, bytes, out.tag);
+  hipStream_t s = nullptr;
+  if (const int rc = ipc_stream(&s); rc != GP_OK) return rc;
+  GP_HIP_TRY(hipMemcpyAsync(static_cast<char *>(base) + out.tag_offset, out.tag, sizeof out.tag,
+                            hipMemcpyHostToDevice, s));
+  GP_HIP_TRY(hipStreamSynchronize(s));
+  GP_HIP_TRY(hipIpcGetMemHandle(&out.h, device_base));
   std::memset(handle_out, 0, GP_IPC_HANDLE_BYTES);
-  std::memcpy(handle_out, &h, sizeof h);
+  std::memcpy(handle_out, &out, sizeof out);
   return GP_OK;
 }
 
 int gp_ipc_open_handle(void **device_ptr, const void *handle) {
   if (!device_ptr || !handle) return set_error(GP_ERR_INVALID, "null pointer");
-  hipIpcMemHandle_t h;
-  std::memcpy(&h, handle, sizeof h);
+  IpcHandleOut in;
+  std::memcpy(&in, handle, sizeof in);
+  if (in.tag[0] != kIpcTagMagic) return set_error(GP_ERR_INVALID, "not a gp_ipc_get_handle handle");
   std::lock_guard<std::mutex> lk(g_ipc_mu);
-  GP_HIP_TRY(hipIpcOpenMemHandle(device_ptr, h, hipIpcMemLazyEnablePeerAccess));
+  void *p = nullptr;
+  GP_HIP_TRY(hipIpcOpenMemHandle(&p, in.h, hipIpcMemLazyEnablePeerAccess));
+  // the mapping must hold the exporter's tag where the exporter wrote it
+  uint64_t got[2] = {0, 0};
+  hipStream_t s = nullptr;
+  int rc = ipc_stream(&s);
+  if (rc == GP_OK && (hipMemcpyAsync(got, static_cast<char *>(p) + in.tag_offset, sizeof got, hipMemcpyDeviceToHost,
+                                     s) != hipSuccess ||
+                      hipStreamSynchronize(s) != hipSuccess))
+    rc = set_error(GP_ERR_HIP, "reading the IPC mapping's tag failed");
+  if (rc == GP_OK && (got[0] != in.tag[0] || got[1] != in.tag[1])) {
+    char msg[240];
+    std::snprintf(msg, sizeof msg,
+                  "IPC mapping %p does not hold the exporter's tag at +%llu (read %016llx %016llx, expected "
+                  "%016llx %016llx): the runtime mapped other memory than the exported buffer",
+                  p, (unsigned long long)in.tag_offset, (unsigned long long)got[0], (unsigned long long)got[1],
+                  (unsigned long long)in.tag[0], (unsigned long long)in.tag[1]);
+    rc = set_error(GP_ERR_HIP, msg);
+  }
+  if (rc != GP_OK) {
+    (void)hipIpcCloseMemHandle(p);
+    return rc;
+  }
+  *device_ptr = p;
   return GP_OK;
 }
 

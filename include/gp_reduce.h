@@ -368,9 +368,8 @@ int gp_get_device(int *device);
  * otherwise or when no contiguous range is left. */
 int gp_malloc_device(void **ptr, size_t bytes);
 /* A device buffer that may be exported over IPC (gp_ipc_get_handle): an
- * allocation of its own, rounded up to a multiple of 2 MiB.  The runtime
- * sub-allocates smaller device buffers from shared 2-MiB blocks, and exporting
- * such a fragment is unreliable (ABI 11).  Free with
+ * allocation of its own, at least `bytes` + 256 rounded up to a multiple of
+ * 2 MiB; its last 256 bytes hold the export's tag (ABI 11).  Free with
  * gp_free_device. */
 int gp_malloc_device_shared(void **ptr, size_t bytes);
 int gp_free_device(void *ptr);
@@ -396,11 +395,13 @@ int gp_stream_wait_event(gp_stream s, gp_event e);
 int gp_device_pci_bus_id(int device, char *buf, int len);
 
 /* Inter-process device memory (same node; xGMI between MI355X devices):
- * export an allocation BASE of at least 2 MiB (gp_malloc_device_shared; an
- * interior pointer or a sub-2-MiB fragment is refused with GP_ERR_INVALID) as
- * an opaque 64-byte handle, map a peer's handle into this process (peer access
- * enabled lazily), unmap. */
-#define GP_IPC_HANDLE_BYTES 64
+ * export the BASE of a gp_malloc_device_shared buffer (anything else is
+ * refused with GP_ERR_INVALID) as an opaque handle, map a peer's handle into
+ * this process (peer access enabled lazily), unmap.  ABI 11: the export
+ * writes a tag into the buffer's spare end and the handle carries it; a
+ * mapping that does not hold it (the runtime mapped other memory) fails with
+ * GP_ERR_HIP instead of handing out wrong rows. */
+#define GP_IPC_HANDLE_BYTES 96
 int gp_ipc_get_handle(void *handle_out, void *device_base);
 int gp_ipc_open_handle(void **device_ptr, const void *handle);
 int gp_ipc_close_handle(void *device_ptr);

@@ -30,6 +30,17 @@ a handle still opens, and still maps the exported bytes, when:
              makes them), each exported; failed exports are counted, not
              raised; the importer maps the rest from 2 threads, keeping every
              mapping open.  Failure counts per side.
+  retry      64 whole buffers exported right after the process's first HIP
+             calls; a failed export is retried every 20 ms (up to 50 times):
+             attempts per buffer, and how long after the first try it worked;
+  late       the same, but the process first sleeps 3 s after its first
+             device allocation: does the failure need a young process?
+  warm       as late, but the process's first device allocation is a 4-MiB
+             buffer that is never exported: is it the first allocation?
+  primed     as late, but a throwaway 2-MiB buffer is allocated and exported
+             (its failure ignored) before the first real buffer is
+             allocated: is it a buffer allocated before the process's first
+             export (gp_malloc_device_shared primes so)?
 
 Each scenario runs as two fresh processes (exporter / importer, or two peers)
 that pass handles through files.  Output: one JSON line per scenario with
@@ -184,6 +195,39 @@ def exporter(scn, d):
             put(d, f"h{k}", raw)
         put(d, "exported", str(n).encode())
         info.append({"export_failures": fails})
+    elif scn in ("retry", "late", "warm", "primed"):
+        n = 64
+        size = 2 << 20
+        first = True
+        primed_ok = None
+        if scn in ("warm", "primed"):
+            dummy, _ = alloc(h, 4 << 20 if scn == "warm" else 2 << 20, 0)
+            keep.append(dummy)
+            if scn == "primed":
+                try:
+                    export(h, dummy)
+                    primed_ok = True
+                except RuntimeError:
+                    primed_ok = False
+        attempts = []
+        for k in range(n):
+            p, inf = alloc(h, size, 1 + k % 250)
+            keep.append(p)
+            if first and scn in ("late", "warm", "primed"):
+                time.sleep(3.0)
+            first = False
+            t0 = time.monotonic()
+            for a in range(1, 51):
+                try:
+                    raw = export(h, p)
+                    break
+                except RuntimeError:
+                    raw = b""
+                    time.sleep(0.02)
+            attempts.append({"k": k, "attempts": a, "ok": bool(raw), "ms": round((time.monotonic() - t0) * 1e3, 1)})
+            put(d, f"h{k}", raw)
+        put(d, "exported", str(n).encode())
+        info.append({"retries": [x for x in attempts if x["attempts"] > 1], "primed_export_ok": primed_ok})
     elif scn == "mt_open":
         n = 64
         for k in range(n):
@@ -221,9 +265,9 @@ def importer(scn, d):
     h = hip()
     n = int(get(d, "exported", timeout=60)) if not scn.startswith("seq") else 16
     results = []
-    if scn in ("mt_open", "mt_export") or scn.startswith("stress"):
+    if scn in ("mt_open", "mt_export", "retry", "late", "warm", "primed") or scn.startswith("stress"):
         raws = [get(d, f"h{k}") for k in range(n)]
-        nbytes = SMALL if scn != "stress_whole" else 2 << 20
+        nbytes = 2 << 20 if scn in ("stress_whole", "retry", "late", "warm", "primed") else SMALL
         go = threading.Barrier(2)
 
         def work(t):

@@ -41,6 +41,7 @@ FAMILIES = [
     ("row / gather plans (libgeeps Update / Read) vs oracle", "test_gpu_parity",
      ("test_row_plan", "test_gather_plan")),
     ("C-ABI from C99 vs oracle", "test_gpu_parity", ("test_c_abi_consumer",)),
+    ("IPC buffers between processes through the C-ABI (tagged mappings)", "test_ipc", ("test_",)),
     ("libgeeps end to end (other process / consistency cases)", "test_libgeeps", ("test_",)),
     ("wire path: libgeeps ZMTP/3.0 ROUTER vs a stock libzmq ROUTER (CPU)", "test_zmtp", ("test_",)),
     ("oracle vs golden vectors + layout vs reference headers (CPU)", "", ("test_",)),

@@ -691,9 +691,10 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
     y = rng.standard_normal(n_cache * W).astype(np.float32)
     ti = torch.from_numpy(idx).to(dev)
     tx = T(x, dev)
-    # add, three times: the first call runs in op order and (unsorted
-    # residual) leaves a copy of the index, the second builds and runs the
-    # destination-sorted residual, the third runs it from the cache
+    # add, three times: the first call plans (an unsorted residual of rows up
+    # to 128 floats: the inverse map, built and run; wider rows: op order and
+    # a copy of the index, the second call then builds and runs the
+    # destination-sorted residual), later calls run the plan from the cache
     e = y.copy()
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
     for call in range(3):
@@ -735,14 +736,15 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
 def test_unplanned_plan_cache_checks_index_content(analyzed, dev, id0):
     """The plan cache keys on the index pointer but trusts no pointer: the same
     device tensor refilled with another permutation (same size, offsets,
-    limit) must give the new index's sums, not the cached order's.  The first
-    call with the new content is a steady-state call: its device check finds
-    the change and only the gated op-order form runs (no host round trip); the
-    next call sees the check's host-visible word, drops the entry and keeps a
-    copy of the new index (no sort), the next builds its sorted order and the
-    one after runs it.  id0 "position" (the op buffer's rows
-    in order, as the reference lists them) is checked against the compact
-    copy (id1 only), a permuted id0 against the full copy."""
+    limit) must give the new index's sums, not the cached plan's.  The first
+    call with an index builds its inverse plan (a map over destination rows)
+    and runs it; later calls are steady-state calls.  The first with new
+    content finds the change with its device check and only the gated
+    op-order form runs (no host round trip); the next sees the check's
+    host-visible word, drops the entry and plans the new index afresh
+    (VERDICT r03 #4).  id0 "position" (the op buffer's rows in order, as the
+    reference lists them) is checked against the compact copy (id1 only), a
+    permuted id0 against the full copy."""
     from geeps_amd import rowops
     rng = np.random.default_rng(99)
     W, n = 128, 40000  # 20 MiB of rows: a cached (unsorted) residual
@@ -764,9 +766,9 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev, id0):
             rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W)
             torch.cuda.synchronize()
             assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), (round_, call)
-            # one entry: the index's copy and its sorted residual (16 B a row
-            # each), once sorted also the compact copy (4 B a row)
-            assert _cache_entries() in ((1, 2 * 16 * n), (1, 2 * 16 * n + 4 * n)), (round_, call)
+            # one entry: the index's copy (16 B a row) and its plan: the
+            # inverse map (8 B a destination row) and the compact copy (4 B)
+            assert _cache_entries() == (1, 28 * n), (round_, call)
         prev = idx
 
 
@@ -1298,8 +1300,9 @@ def test_unplanned_calls_fuzz(analyzed, dev, case):
     """The reference binding's unplanned calls through the device plan and
     its plan cache, on fuzzed indexes (dense runs around the sweep threshold,
     short runs, scattered rows, in shuffled op order), row sizes, offsets and
-    num_vals_limit: three scatter-adds (first call in op order, second builds
-    the sorted residual, third runs it behind the device check), then two more
+    num_vals_limit: three scatter-adds (the first builds the plan: an inverse
+    map at up to 128 floats a row, else op order and, on the second call, the
+    sorted residual; later ones run it behind the device check), then two more
     after two destinations of the index were swapped in place (the steady
     state's gated op-order form, then the re-plan), three inits and a gather,
     each bit for bit against the oracle."""
