@@ -3032,10 +3032,24 @@ int gp_ipc_open_handle(void **device_ptr, const void *handle) {
   std::lock_guard<std::mutex> lk(g_ipc_mu);
   void *p = nullptr;
   GP_HIP_TRY(hipIpcOpenMemHandle(&p, in.h, hipIpcMemLazyEnablePeerAccess));
-  // the mapping must hold the exporter's tag where the exporter wrote it
+  // the mapping must span the tag (else it is not the exported allocation:
+  // refused without reading past it) and hold the exporter's tag there
   uint64_t got[2] = {0, 0};
   hipStream_t s = nullptr;
   int rc = ipc_stream(&s);
+  void *mbase = nullptr;
+  size_t mbytes = 0;
+  const bool ranged = hipMemGetAddressRange(&mbase, &mbytes, p) == hipSuccess;
+  if (!ranged) (void)hipGetLastError();  // no range for this mapping: the tag check below still runs
+  const uintptr_t from_base = reinterpret_cast<uintptr_t>(p) - reinterpret_cast<uintptr_t>(mbase);
+  if (rc == GP_OK && ranged && (from_base > mbytes || mbytes - from_base < in.tag_offset + sizeof got)) {
+    char msg[200];
+    std::snprintf(msg, sizeof msg,
+                  "IPC mapping %p spans %zu B from %p, short of the exporter's tag at +%llu: the runtime mapped "
+                  "other memory than the exported buffer",
+                  p, mbytes, mbase, (unsigned long long)in.tag_offset);
+    rc = set_error(GP_ERR_HIP, msg);
+  }
   if (rc == GP_OK && (hipMemcpyAsync(got, static_cast<char *>(p) + in.tag_offset, sizeof got, hipMemcpyDeviceToHost,
                                      s) != hipSuccess ||
                       hipStreamSynchronize(s) != hipSuccess))
