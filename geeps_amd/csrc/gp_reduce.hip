@@ -375,7 +375,7 @@ void launch_phased(float *out, const float *in, const BucketPtrs &b, size_t n4_t
                    const PhasePlan &p, hipStream_t s, const Gate *g = nullptr) {
   const size_t G = (size_t)num_cus();
   for (size_t l = 0; l < p.launches; ++l)
-    GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_phased_kernel<NB, RT, BAL, ZIN>),
+    GP_LAUNCH_GATED(NB <= 1, g, (bucket_sum_phased_kernel<NB, RT, BAL, ZIN>),
                     (bucket_sum_phased_kernel<NB, RT, BAL, ZIN, true>), dim3((unsigned)G), dim3(kBlock), s,
                     reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b, n4_tiles,
                     l * (size_t)p.per_launch, p.tiles);
@@ -541,7 +541,7 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     using SS = SweepShape<NB, ZIN>;
     const SweepSplit sp = sweep_split<NB, ZIN>(n / 4 / kPhaseTile * kPhaseTile);
     for (size_t c = 0; c < sp.big; ++c)
-      GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN, SS::U>),
+      GP_LAUNCH_GATED(NB <= 1, g, (bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN, SS::U>),
                       (bucket_sum_sweep_kernel<NB, SS::RT, SS::TG, ZIN, SS::U, true>), dim3((unsigned)G),
                       dim3(kBlock), s, reinterpret_cast<f4 *>(out), reinterpret_cast<const f4 *>(in), b,
                       n / 4, c);
@@ -549,7 +549,7 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     if constexpr (!SS::kOne) {
       const BucketPtrs bo = offset_buckets<NB>(b, done);
       for (size_t c = 0; c < sp.small; ++c)
-        GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN>),
+        GP_LAUNCH_GATED(NB <= 1, g, (bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN>),
                         (bucket_sum_sweep_kernel<NB, kSweepRT, kSweepTG, ZIN, kPhaseU, true>), dim3((unsigned)G),
                         dim3(kBlock), s, reinterpret_cast<f4 *>(out + done),
                         reinterpret_cast<const f4 *>(ZIN ? nullptr : in + done), bo, (n - done) / 4, c);
@@ -579,7 +579,7 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     const size_t tiles = (n4 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
     const size_t cap = G * kPerCU;
     const size_t grid = tiles < cap ? tiles : cap;
-    GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_vec_kernel<NB, U, ZIN>), (bucket_sum_vec_kernel<NB, U, ZIN, true>),
+    GP_LAUNCH_GATED(NB <= 1, g, (bucket_sum_vec_kernel<NB, U, ZIN>), (bucket_sum_vec_kernel<NB, U, ZIN, true>),
                     dim3((unsigned)grid), dim3(kBlock), s, reinterpret_cast<f4 *>(out + done),
                     reinterpret_cast<const f4 *>(in_at), offset_buckets<NB>(b, done), n4);
     done += n4 * 4;
@@ -589,7 +589,7 @@ int launch_bucket_sum_nb(float *out, const float *in, const BucketPtrs &b,
     const size_t rem = n - done;
     size_t grid = (rem + kBlock - 1) / kBlock;
     if (grid > G * kBlocksPerCU) grid = G * kBlocksPerCU;
-    GP_LAUNCH_GATED(NB == 1, g, (bucket_sum_scalar_kernel<NB, ZIN>), (bucket_sum_scalar_kernel<NB, ZIN, true>),
+    GP_LAUNCH_GATED(NB <= 1, g, (bucket_sum_scalar_kernel<NB, ZIN>), (bucket_sum_scalar_kernel<NB, ZIN, true>),
                     dim3((unsigned)grid), dim3(kBlock), s, out + done, in_at, offset_buckets<NB>(b, done), rem);
   }
   GP_HIP_TRY(hipGetLastError());
@@ -1132,8 +1132,8 @@ void launch_row_op_lpr(float *y, const float *x, const gp_double_index *idx,
                        size_t limit, const SegArg<SEG> &seg, bool sorted, hipStream_t s,
                        const Gate *g) {
   constexpr bool kWaveShape = VEC == 4 && LPR <= 32;
-  // the unplanned calls' steady state gates its flat scatter-add / init launches
-  constexpr bool kGatable = SEG == kFlat && (OP == kAddFrom || OP == kInitFrom);
+  // the unplanned calls' steady state gates its flat launches
+  constexpr bool kGatable = SEG == kFlat;
   constexpr bool kWaveGather = OP == kAssignTo && (SEG == kFlat || SEG == kSegX);
   constexpr bool kWaveScatter = (OP == kAddFrom || OP == kInitFrom) && SEG == kFlat;
   if constexpr (kWaveShape && (kWaveGather || kWaveScatter)) {
@@ -1997,6 +1997,11 @@ struct CachedPlan {
   // destination rows 0 .. inv_rows - 1 (inverse_scatter_kernel)
   std::shared_ptr<DevBuf> inv;
   size_t inv_rows = 0;
+  // a ranges plan (a gather, or a residual whose destinations ascend): the
+  // residual is the call's own index over these entry ranges, in call order
+  bool ranges = false;
+  bool ascending = false;
+  EntryRanges rr{};
   hipEvent_t ready = nullptr;  // recorded once copy (and sorted) are built, on the building stream
   uint64_t last_use = 0;
   size_t bytes = 0;
@@ -2004,7 +2009,7 @@ struct CachedPlan {
   const gp_double_index *sorted_ptr() const {
     return sorted ? static_cast<const gp_double_index *>(sorted->p) : nullptr;
   }
-  bool planned() const { return sorted || inv; }  // a steady-state entry
+  bool planned() const { return sorted || inv || ranges; }  // a steady-state entry
   const uint64_t *inv_ptr() const { return static_cast<const uint64_t *>(inv->p); }
   unsigned *gate_words() const { return static_cast<unsigned *>(gate->p); }
   uint64_t *base0_word() const { return reinterpret_cast<uint64_t *>(gate_words() + kGateSlots); }
@@ -2158,6 +2163,31 @@ int cache_inverse_plan(const PlanKey &key, const gp_double_index *idx, const Ent
   return GP_OK;
 }
 
+// A plan that is the call's dense runs and residual ranges (a gather, or a
+// residual already in destination order, or too short to sort): kept with a
+// copy of the index (and its compact copy) for the steady state.
+int cache_ranges_plan(const PlanKey &key, const gp_double_index *idx, const EntryRanges &rr,
+                      const std::vector<DevRun> &runs, bool ascending, hipStream_t s) {
+  auto p = std::make_shared<CachedPlan>();
+  p->key = key;
+  p->resid = rr.pre[rr.count];
+  p->runs = runs;
+  p->ranges = true;
+  p->ascending = ascending;
+  p->rr = rr;
+  p->bytes = key.n * sizeof(gp_double_index);
+  int rc = GP_OK;
+  p->copy = std::make_shared<DevBuf>(key.n * sizeof(gp_double_index), key.device, s, &rc);
+  if (rc != GP_OK) return rc;
+  rc = steady_state_setup(p.get(), idx, s);
+  if (rc != GP_OK) return rc;
+  GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+  GP_HIP_TRY(hipMemcpyAsync(p->copy->p, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
+  GP_HIP_TRY(hipEventRecord(p->ready, s));
+  cache_insert(std::move(p));
+  return GP_OK;
+}
+
 // The inverse plan's rows: row_wave_kernel walking destination rows 0 ..
 // inv_rows - 1 through the map (Gate::inv), offsets already applied.
 template <int OP>
@@ -2226,7 +2256,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   int dev = 0;
   GP_HIP_TRY(hipGetDevice(&dev));
   const PlanKey key{dev, OP, reinterpret_cast<uintptr_t>(idx), n, W, limit, off.id0, off.id1};
-  std::shared_ptr<CachedPlan> cached = OP == kAssignTo ? nullptr : cache_find(key);
+  std::shared_ptr<CachedPlan> cached = cache_find(key);
   // a steady-state call since the last host look found the index changed: the
   // entry is stale, plan this call afresh (scan, host round trip)
   if (cached && cached->planned() && cached->changed->load() != 0) {
@@ -2246,7 +2276,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
       else if constexpr (OP == kInitFrom)
         rc = launch_bucket_sum_nb<1, true>(yr, nullptr, b, r.rows * W, s, g);
       else
-        rc = launch_bucket_sum_nb<0>(yr, x + r.from * W, BucketPtrs{}, r.rows * W, s);
+        rc = launch_bucket_sum_nb<0>(yr, x + r.from * W, BucketPtrs{}, r.rows * W, s, g);
       if (rc != GP_OK) return rc;
     }
     return (int)GP_OK;
@@ -2287,6 +2317,23 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     int rc = launch_runs(cached->runs, &same);
     if (rc != GP_OK) return rc;
     if (cached->inv) return launch_inverse_rows<OP>(y, x, *cached, W, limit, s, select);
+    if (cached->ranges) {
+      // the residual is the call's own index over the kept ranges, in call
+      // order: the first range's launch selects (all the call's rows if the
+      // index changed), the others run only if it did not; with no residual,
+      // the op-order form alone, gated on a change
+      const EntryRanges &rr = cached->rr;
+      if (rr.count == 0) {
+        const Gate changed{word, gen, kGateIfChanged, nullptr, 0, 0, 0, nullptr};
+        return launch_row_op<OP>(y, x, idx, n, off, W, limit, s, /*sorted=*/false, &changed);
+      }
+      for (uint32_t i = 0; i < rr.count; ++i) {
+        rc = launch_row_op<OP>(y, x, idx + rr.lo[i], rr.hi[i] - rr.lo[i], off, W, limit, s, cached->ascending,
+                               i == 0 ? &select : &same);
+        if (rc != GP_OK) return rc;
+      }
+      return GP_OK;
+    }
     return launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
                              /*sorted=*/true, &select);
   }
@@ -2379,7 +2426,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     add(at, n);
   }
   const size_t resid = rr.pre[rr.count];
-  if (resid == 0) return GP_OK;
+  if (resid == 0) return cached ? GP_OK : cache_ranges_plan(key, idx, rr, runs, true, s);  // all dense runs
   // destinations already (mostly) ascending: the call's order is the sorted one
   size_t resid_tiles = 0, asc_tiles = 0;
   for (uint32_t i = 0; i < rr.count; ++i) {
@@ -2431,6 +2478,10 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   }
   // first sighting: remember the content, so the next call can tell it is the same
   if (sortable && !cached) return cache_first_sighting(key, idx, resid, s);
+  // nothing to sort (a gather, ascending destinations, a short residual): the
+  // plan is the runs and the residual ranges themselves, kept for the steady
+  // state's check-and-run without a scan
+  if (!sortable && !cached) return cache_ranges_plan(key, idx, rr, runs, ascending, s);
   return GP_OK;
 }
 

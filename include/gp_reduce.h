@@ -70,13 +70,14 @@ const char *gp_last_error(void);
  * bytes; default 64 MiB; SIZE_MAX: never).  Process-wide; for tests and
  * measurement. */
 int gp_set_unplanned_min_bytes(size_t min_bytes);
-/* The unplanned calls' plan cache (ABI 10): a large scatter-add / init whose
- * rows outside dense runs are not in ascending destination order runs in op
- * order once and keeps, for later calls with the same index (same pointer,
- * size, offsets, row size and limit, and the same content, which every such
- * call checks entry for entry on the device), a copy of the index and its
- * rows in destination order (+ a 4-B compact copy of each entry's id1 once
- * sorted): 32-36 B of HBM per row, at most 256 indexes and
+/* The unplanned calls' plan cache (ABI 10, 11): a large call keeps its plan
+ * for later calls with the same index (same pointer, size, offsets, row size
+ * and limit, and the same content, which every such call checks entry for
+ * entry on the device): a copy of the index and a 4-B compact copy of each
+ * entry's id1, its dense runs and its residual -- as an inverse map over
+ * destination rows or in destination order when a scatter's residual is
+ * unsorted, else as ranges of the index itself: 20-36 B of HBM per row, at
+ * most 256 indexes and
  * gp_set_unplanned_cache_bytes() of HBM (default 4 GiB; 0 keeps nothing),
  * least recently used first out.  Clear it, read its size, or bound it. */
 int gp_unplanned_cache_clear(void);

@@ -712,12 +712,11 @@ def test_unplanned_device_plan_matches_oracle(analyzed, dev, kind, W, limit_frac
         rowops.init_rows_from_double_index_gpu(ty, tx, ti, n, off, W, limit)
         torch.cuda.synchronize()
         assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", kind, W, call)
-    # only an unsorted residual of >= 16 MiB is cached: "permuted" at 128 and
-    # 1024 floats, "runs" at 1024 (its ~9,100 scattered rows); "identity" and
-    # "sorted" residuals ascend, the rest are short
-    expect = 1 if (kind == "permuted" and W >= 128) or (kind == "runs" and W == 1024) else 0
-    assert cached_add == expect, (kind, W)
-    assert _cache_entries()[0] == 2 * cached_add
+    # every large call keeps its plan (ABI 11): an inverse map or sorted
+    # residual for an unsorted residual of >= 16 MiB ("permuted" at 128 and
+    # 1024 floats, "runs" at 1024), else its runs and residual ranges
+    assert cached_add == 1, (kind, W)
+    assert _cache_entries()[0] == 2
     # gather with the index's roles swapped: y[id0] = x[id1]
     gidx = np.ascontiguousarray(idx[:, ::-1]) if kind != "sorted" else idx
     g_out = int(gidx[:, 0].max()) + 1 + off[0]
