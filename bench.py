@@ -748,16 +748,21 @@ def libgeeps_multi_gpu_leg(n_gpus, rows, W, clocks=5, warmup=2, alex_clocks=10, 
     base_env = {"GEEPS_TEST_SPREAD_DEVICES": "1"}
     if gpus >= n_gpus:  # one process per GPU: the default hardware queues
         base_env["CLOCK_BENCH_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES", "4")
+    failed = None
     for table, nrows, slack, ck in (("1Mx1024", rd_rows, 0, clocks), ("alexnet", ALEXNET_ROWS, 1, alex_clocks)):
         if table not in tables:
             continue
         for path, env in PEER_PATHS.items():
             key = f"{table}_{path}"
+            if failed:  # one failure (or hang) ends the leg: the headline must not wait on it
+                out[key] = {"skipped": f"after {failed} failed"}
+                continue
             try:
-                r = mod.run(n_gpus, nrows, ck, warmup, slack, "ipc", timeout=300,
+                r = mod.run(n_gpus, nrows, ck, warmup, slack, "ipc", timeout=150,
                             extra_env=dict(base_env, **env))
-            except Exception as exc:  # report, keep the other cases
+            except Exception as exc:  # report it, skip the rest
                 out[key] = {"error": f"{type(exc).__name__}: {str(exc)[-800:]}"}
+                failed = key
                 continue
             out[key] = {"rows": nrows, "slack": slack, "ms_per_clock": r["ms_per_clock_max"],
                         "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],

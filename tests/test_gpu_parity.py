@@ -1303,8 +1303,9 @@ def test_unplanned_calls_fuzz(analyzed, dev, case):
     map at up to 128 floats a row, else op order and, on the second call, the
     sorted residual; later ones run it behind the device check), then two more
     after two destinations of the index were swapped in place (the steady
-    state's gated op-order form, then the re-plan), three inits and a gather,
-    each bit for bit against the oracle."""
+    state's gated op-order form, then the re-plan), three inits, and three
+    gathers plus two after a swap of two sources (the ranges plan's steady
+    state and its select launch), each bit for bit against the oracle."""
     from geeps_amd import rowops
     rng = np.random.default_rng(7000 + case)
     W = int(rng.choice([4, 64, 128, 132, 256]))
@@ -1345,11 +1346,22 @@ def test_unplanned_calls_fuzz(analyzed, dev, case):
         rowops.init_rows_from_double_index_gpu(ty, tx, ti, n_op, off, W, limit)
         torch.cuda.synchronize()
         assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), ("init", case, call, W, off, limit)
+    # gathers: the first plans (runs and residual ranges), later ones run it
+    # behind the device check; then two sources swapped in place
     dst = rng.standard_normal(n_x * W).astype(np.float32)
-    e = dst.copy()
-    oracle.assign_rows_to_double_index(e, y, idx, off, W, limit)
-    td = T(dst, dev)
-    rowops.assign_rows_to_double_index_gpu(td, T(y, dev), ti, n_op, off, W, limit)
-    torch.cuda.synchronize()
-    assert np.array_equal(bits(td.cpu().numpy()), bits(e)), ("gather", case, W, off, limit)
+    ty = T(y, dev)
+    for changed in (False, True):
+        if changed:
+            gidx = idx.copy()
+            gidx[[a, b], 1] = gidx[[b, a], 1]
+            ti.copy_(torch.from_numpy(gidx))
+        else:
+            gidx = idx
+        e = dst.copy()
+        oracle.assign_rows_to_double_index(e, y, gidx, off, W, limit)
+        for call in range(3 if not changed else 2):
+            td = T(dst, dev)
+            rowops.assign_rows_to_double_index_gpu(td, ty, ti, n_op, off, W, limit)
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(td.cpu().numpy()), bits(e)), ("gather", changed, call, case, W, off, limit)
 
