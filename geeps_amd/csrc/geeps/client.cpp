@@ -318,6 +318,10 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       }
       ch.server->release_all(client_id);
       ch.server->post_shutdown(client_id);
+      // its last frame, kCmdReaderDone, comes once it has handled this
+      // server's SHUTDOWN (shutdown()): this process waits for it
+      continue;
+    } else if (cmd == kCmdReaderDone) {
       break;
     } else {
       GP_CHECK_MSG(false, "server received unknown command " << (int)cmd);
@@ -342,7 +346,14 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
     if (!recv_frame(fd, parts, scratch, alloc, &buf)) break;
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
-    if (cmd == SHUTDOWN) break;  // the server will send nothing more
+    if (cmd == SHUTDOWN) {
+      // The server sends nothing more.  Every frame it sent is handled; once
+      // no queued device work reads its memory, say so: it waits for that
+      // before its process exits and frees what its handles named.
+      GP_CALL(gp_device_synchronize());
+      reader_done_to_server(ch, server_id);
+      break;
+    }
     if (reader_delay_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(reader_delay_us_));
     GP_CHECK((parts.size() == 3 || parts.size() == 4) &&
              parts[0].size == sizeof(sc_read_row_batch_msg_t));
@@ -449,13 +460,22 @@ void ClientLib::send_to_server(Channel &ch, uint32_t s, const std::vector<Part> 
 
 // The reader thread releases a master version it no longer reads.  The last
 // refresh can land after the app thread already sent SHUTDOWN (the server then
-// stops reading that socket, and its SHUTDOWN handling released every hold),
+// reads nothing but kCmdReaderDone there, and its SHUTDOWN handling released
+// every hold),
 // so such a release is dropped, not sent.
 void ClientLib::ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a) {
   std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
   if (ch.server_shut[s]) return;
   GP_CHECK_MSG(send_frame(ch.server_fd[s], {Part{&a, sizeof a}}),
                "refresh ACK to server " << s << " failed");
+}
+
+void ClientLib::reader_done_to_server(Channel &ch, uint32_t s) {
+  std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
+  cs_clock_msg_t h{};
+  h.cmd = kCmdReaderDone;
+  h.client_id = process_id_;
+  GP_CHECK_MSG(send_frame(ch.server_fd[s], {Part{&h, sizeof h}}), "reader-done to server " << s << " failed");
 }
 
 void ClientLib::give_back(Channel &ch, uint32_t s, uint32_t table, int v) {
@@ -1389,8 +1409,12 @@ std::string ClientLib::json_stats() {
 }
 
 // Shutdown handshake: every client tells every server it is done; a server
-// acknowledges all clients once all have; each process then tears down.  A peer
-// therefore never sees a connection close while it still expects a message.
+// acknowledges all clients once all have; each client's reader, having handled
+// that acknowledgement (and every frame before it), answers with
+// kCmdReaderDone; each process tears down once its readers of both kinds are
+// done.  A peer therefore never sees a connection close while it still expects
+// a message, and no process frees a buffer whose IPC handle a peer has yet to
+// open.
 void ClientLib::shutdown() {
   if (stopping_.exchange(true)) return;
   for (auto &chp : channels_) {

@@ -184,8 +184,9 @@ struct Channel {
   // app thread (pushes) and the reader thread (refresh ACKs) both write to it
   std::vector<int> server_fd;
   std::vector<std::unique_ptr<std::mutex>> server_send_mu;
-  // set (under server_send_mu[s]) once SHUTDOWN went to server s: nothing may
-  // follow it on that socket, so late refresh ACKs are dropped
+  // set (under server_send_mu[s]) once SHUTDOWN went to server s: nothing but
+  // the reader's kCmdReaderDone may follow it on that socket, so late refresh
+  // ACKs are dropped
   std::vector<char> server_shut;
   std::vector<std::thread> client_readers;
   PinnedArray<float> send_buf;
@@ -274,6 +275,8 @@ class ClientLib {
   bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r, bool *held);
   void send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts);
   void ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a);
+  // the reader of server s's frames has handled its SHUTDOWN (kCmdReaderDone)
+  void reader_done_to_server(Channel &ch, uint32_t s);
   // hand master version v of server s's shard of `table` back to that server
   void give_back(Channel &ch, uint32_t s, uint32_t table, int v);
 

@@ -112,6 +112,12 @@ struct sc_read_row_batch_msg_t {
 // HBM; TCP carries only these small control frames.
 // ---------------------------------------------------------------------------
 constexpr command_t kCmdRefreshAck = 101;  // client -> server: master version released
+// client -> server, the last frame on a connection: the client's reader has
+// handled the server's SHUTDOWN and every frame before it (each version handle
+// they named is mapped), and no device work of the client still reads the
+// server's memory.  The server's process outlives this: a handle opened after
+// its exporter exited is refused ("Invalid IPC handle ... and 0").
+constexpr command_t kCmdReaderDone = 102;
 constexpr uint32_t kIpcHandleBytes = GP_IPC_HANDLE_BYTES;  // the C-ABI's opaque handle
 
 // 4th part of a CLOCK_WITH_UPDATES_BATCH whose rows stay in the client's oplog.
