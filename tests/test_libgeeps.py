@@ -638,6 +638,14 @@ def test_randomized_configurations(dev, case):
     transport = rng.choice(["ipc", "ipc", "tcp"])
     if rng.random() < 0.5:  # direct reads, each buffer re-read before its PostRead
         extra.update(GEEPS_DIRECT_READ="1", GEEPS_TEST_REREAD="1")
+    # (round 4; drawn last so the earlier draws give round 3's cases) slow
+    # reader threads (refreshes and shutdown frames queue up behind them), and
+    # with direct reads the app's device reads of each Read buffer left queued
+    # past PostRead (~0.7 ms each)
+    if rng.random() < 0.25:
+        extra["GEEPS_TEST_READER_DELAY_US"] = str(rng.choice([2000, 15000]))
+    if rng.random() < 0.5 and "GEEPS_DIRECT_READ" in extra:
+        extra["GEEPS_TEST_ASYNC_READ"] = "200"
     desc = dict(P=P, slack=slack, channels=channels, rmw=rmw, tables=tables, local=local, mode=mode,
                 layers=layers, transport=transport, **extra)
     print("config", desc)
