@@ -4,7 +4,9 @@ Checks, against the oracle applying every client's whole-table delta in client
 order 0..N-1 (the reference server's arrival order), that:
   * the a2a exchange + client-order apply + all-gather refresh is bit-exact and
     every rank ends with the identical full table;
-  * the reduce-scatter exchange is within fp32 tolerance (ring order);
+  * the reduce-scatter exchange is bit-exact against its own association at 2
+    ranks (a two-term sum per shard) and within fp32 tolerance of the client-order
+    sum (ring order at 8 ranks);
   * uneven partitions (num_rows % world != 0) use the reference rule
     (clientlib-viter.cpp:674-682) and round-trip through the padded gather.
 """
@@ -33,6 +35,14 @@ def _expected(num_rows, W, num_clients, steps):
     return m
 
 
+def _expected_rs_two_ranks(num_rows, W, num_clients, steps):
+    m = np.zeros(num_rows * W, np.float32)
+    for step in range(steps):
+        d = [oracle.synthetic_delta(c + 100 * step, num_rows * W) for c in range(num_clients)]
+        oracle.apply_updates(m, [d[2 * j] + d[2 * j + 1] for j in range(num_clients // 2)])
+    return m
+
+
 @pytest.mark.parametrize("world,num_rows,W,clients,exchange,steps", [
     (2, 64, 16, 4, "a2a", 2),
     (2, 37, 12, 2, "a2a", 3),     # uneven rows: 19 + 18
@@ -54,6 +64,14 @@ def test_sharded_reduction(tmp_path, world, num_rows, W, clients, exchange, step
     assert hosted == list(range(clients))
     if exchange == "a2a":
         assert np.array_equal(tables[0].view(np.uint32), e.view(np.uint32))
+    elif world == 2:
+        # two ranks: each shard's reduce-scatter adds exactly two deltas, and a
+        # two-term fp32 sum is the same in either order, so the rs form is
+        # pinned bit for bit: master += (d[2j] + d[2j+1]) for hosted slot j
+        assert np.array_equal(tables[0].view(np.uint32), _expected_rs_two_ranks(num_rows, W, clients, steps)
+                              .view(np.uint32))
+        np.testing.assert_allclose(tables[0], e, rtol=0,
+                                   atol=clients * steps * np.finfo(np.float32).eps * (0.5 * clients * steps + 1))
     else:
         # per element: |err| <= (N*steps) ulps of the largest partial sum
         tol = clients * steps * np.finfo(np.float32).eps * (0.5 * clients * steps + 1)
