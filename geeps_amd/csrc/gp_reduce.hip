@@ -1679,18 +1679,30 @@ __global__ __launch_bounds__(kBlock) void index_scan_kernel(const gp_double_inde
 //            (the reference's op buffers list their rows in order: id0 is
 //            the position, clientlib-viter.cpp:841), only id1 as 4 B: the
 //            check reads 20 B per entry and still compares all 128 bits.
-// Each thread holds 4 entries' loads in flight.  A wave that saw a difference
-// stores this call's generation into the call's gate word (the gated launches
-// behind it read it) and into the entry's host-visible word (the next call
-// drops the entry).  Plain vector stores, idempotent: no atomics needed.
+// Each thread holds 4 entries' loads in flight.  A difference puts this
+// call's generation into the call's gate word (the gated launches behind it
+// read it) and into the entry's host-visible word (the next call drops the
+// entry), through flag_once.
 constexpr int kCmpPerThread = 4;
 constexpr unsigned kGateSlots = 64;  // gate words per entry: calls in flight on one entry
+
+// A launch's finding (an index changed, a map unsound, a copy not compact):
+// `dev_word` := v for the kernels behind it, and `host_word` := v for the
+// host, at most one atomic per block and one host write per launch -- the
+// block whose exchange changed the device word writes it.  (A store per wave
+// to the host-visible word crosses the bus each time: a launch that found
+// differences everywhere took 1.06 ms instead of 25 us.)  Every thread of the
+// block calls it: `hit` is reduced over the block.
+__device__ __forceinline__ void flag_once(bool hit, unsigned *dev_word, unsigned *host_word, unsigned v) {
+  if (!__syncthreads_or(hit) || threadIdx.x != 0) return;
+  if (__hip_atomic_exchange(dev_word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != v)
+    __hip_atomic_store(host_word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 template <bool COMPACT>
-__global__ __launch_bounds__(kBlock) void index_verify_kernel(const gp_double_index *__restrict__ idx,
-                                                              const void *__restrict__ kept, size_t n,
-                                                              const uint64_t *__restrict__ base0_word,
-                                                              unsigned *__restrict__ gate_word,
-                                                              unsigned *__restrict__ host_word, unsigned gen) {
+__device__ __forceinline__ void index_verify(const gp_double_index *__restrict__ idx, const void *__restrict__ kept,
+                                             size_t n, const uint64_t *__restrict__ base0_word,
+                                             unsigned *__restrict__ gate_word, unsigned *__restrict__ host_word,
+                                             unsigned gen) {
   const size_t step = (size_t)gridDim.x * kBlock * kCmpPerThread;
   const uint64_t base0 = COMPACT ? *base0_word : 0;
   bool differs = false;
@@ -1717,19 +1729,38 @@ __global__ __launch_bounds__(kBlock) void index_verify_kernel(const gp_double_in
       }
     }
   }
-  if (__any(differs) && (threadIdx.x & 63) == 0) {
-    __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  flag_once(differs, gate_word, host_word, gen);
+}
+
+// FORM 0: against the full copy, 1: the compact copy, 2: whichever the
+// entry has, by compact_copy_kernel's `broken` flag (read on the device: the
+// host may not know it yet, and an entry may keep no full copy of a compact
+// index, copy_if_broken_kernel).
+template <int FORM>
+__global__ __launch_bounds__(kBlock) void index_verify_kernel(const gp_double_index *__restrict__ idx,
+                                                              const gp_double_index *__restrict__ full,
+                                                              const uint32_t *__restrict__ compact, size_t n,
+                                                              const uint64_t *__restrict__ base0_word,
+                                                              unsigned *__restrict__ gate_word,
+                                                              unsigned *__restrict__ host_word, unsigned gen,
+                                                              const unsigned *__restrict__ broken) {
+  bool use_compact = FORM == 1;
+  if constexpr (FORM == 2) use_compact = __hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  if (use_compact)
+    index_verify<true>(idx, compact, n, base0_word, gate_word, host_word, gen);
+  else
+    index_verify<false>(idx, full, n, base0_word, gate_word, host_word, gen);
 }
 
 // The compact copy of an index (built with its sorted residual, on the second
-// call): id1 as 4 B per entry and base0 = id0 of entry 0; `host_broken` set
+// call): id1 as 4 B per entry and base0 = id0 of entry 0; `host_broken` and
+// `dev_broken` (a device word the next kernels read) set
 // when the index is not of that shape (then the full copy stays in use).
 __global__ __launch_bounds__(kBlock) void compact_copy_kernel(const gp_double_index *__restrict__ idx, size_t n,
                                                               uint32_t *__restrict__ id1_out,
                                                               uint64_t *__restrict__ base0_out,
-                                                              unsigned *__restrict__ host_broken) {
+                                                              unsigned *__restrict__ host_broken,
+                                                              unsigned *__restrict__ dev_broken) {
   const uint64_t base0 = idx[0].id0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *base0_out = base0;
   bool bad = false;
@@ -1739,8 +1770,18 @@ __global__ __launch_bounds__(kBlock) void compact_copy_kernel(const gp_double_in
     bad |= (v.id0 != base0 + e) | ((v.id1 >> 32) != 0);
     id1_out[e] = (uint32_t)v.id1;
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0)
-    __hip_atomic_store(host_broken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  flag_once(bad, dev_broken, host_broken, 1u);
+}
+
+// The full copy of an index whose steady state checks the compact copy:
+// written only if compact_copy_kernel (earlier on the stream) found the index
+// not of the compact shape, the one case index_verify_kernel<false> reads it.
+__global__ __launch_bounds__(kBlock) void copy_if_broken_kernel(const gp_double_index *__restrict__ idx, size_t n,
+                                                                gp_double_index *__restrict__ out,
+                                                                const unsigned *__restrict__ broken) {
+  if (__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += stride) out[e] = idx[e];
 }
 
 // Residual rows of a call: up to kMaxDeviceRuns + 1 entry ranges, passed by
@@ -1791,12 +1832,12 @@ __global__ __launch_bounds__(kBlock) void residual_gather_kernel(const gp_double
 // inv[to] = entry << 32 | from, offsets applied, over destination rows 0 ..
 // D - 1 (~0 = no residual row goes there; the caller fills it first).  Plain
 // stores: destinations are distinct by the calls' precondition, and
-// inverse_check_kernel then proves it (a repeated destination keeps one
-// entry's word, so another entry finds its own missing).  A source row past
-// 2^32 (a 4-B field) or a repeated destination stores this call's
-// generation into the gate word and the host-visible word: the map is then
-// unsound, the gated op-order launches run instead, and the next call drops
-// the plan.
+// inverse_count_kernel then proves it (a repeated destination leaves fewer
+// listed rows than residual entries).  A source row past 2^32 (a 4-B field)
+// or a repeated destination stores this call's generation into the gate word
+// and the host-visible word: the map is then unsound, the gated op-order
+// launches run instead, and the next call drops the plan.  (A compare-and-swap
+// scatter that checks as it goes measured 2.5x the plain scatter.)
 template <int OP>
 __global__ __launch_bounds__(kBlock) void inverse_scatter_kernel(const gp_double_index *__restrict__ idx, EntryRanges rr,
                                                                  uint64_t off0, uint64_t off1,
@@ -1813,28 +1854,43 @@ __global__ __launch_bounds__(kBlock) void inverse_scatter_kernel(const gp_double
     bad |= (f >> 32) != 0;
     inv[t] = ((uint64_t)e << 32) | (f & 0xffffffffu);
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) {
-    __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  flag_once(bad, gate_word, host_word, gen);
 }
 
-template <int OP>
-__global__ __launch_bounds__(kBlock) void inverse_check_kernel(const gp_double_index *__restrict__ idx, EntryRanges rr,
-                                                               uint64_t off0, uint64_t off1,
-                                                               const uint64_t *__restrict__ inv,
+// Whether the inverse map lists exactly `expected` rows (the residual's
+// entries): one sequential pass over it (8 loads in flight per thread), a
+// block sum, one atomic add per block (a launch of about one block per CU:
+// per-wave atomics on one address measured 254 us); the last block to finish
+// compares and, on a shortfall (a repeated destination), marks the map
+// unsound as inverse_scatter_kernel does.
+constexpr int kCountPerThread = 8;
+__global__ __launch_bounds__(kBlock) void inverse_count_kernel(const uint64_t *__restrict__ inv, size_t rows,
+                                                               uint64_t expected, unsigned long long *counters,
                                                                unsigned *__restrict__ gate_word,
                                                                unsigned *__restrict__ host_word, unsigned gen) {
-  const size_t total = rr.pre[rr.count];
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  bool bad = false;
-  for (size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x; k < total; k += stride) {
-    const size_t e = range_entry(rr, k);
-    uint64_t f, t;
-    row_endpoints<OP>(idx[e], off0, off1, f, t);
-    bad |= inv[t] != (((uint64_t)e << 32) | (f & 0xffffffffu));
+  const size_t step = (size_t)gridDim.x * kBlock * kCountPerThread;
+  unsigned listed = 0;
+  for (size_t base = (size_t)blockIdx.x * kBlock * kCountPerThread + threadIdx.x; base < rows; base += step) {
+    uint64_t v[kCountPerThread];
+#pragma unroll
+    for (int k = 0; k < kCountPerThread; ++k) {
+      const size_t r = base + (size_t)k * kBlock;
+      v[k] = r < rows ? inv[r] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kCountPerThread; ++k) listed += v[k] != ~0ull;
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) {
+  for (int o = 32; o > 0; o >>= 1) listed += __shfl_xor(listed, o, 64);
+  __shared__ unsigned wave_sum[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) wave_sum[threadIdx.x / 64] = listed;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  unsigned long long block = 0;
+  for (int w = 0; w < kBlock / 64; ++w) block += wave_sum[w];
+  __hip_atomic_fetch_add(&counters[0], block, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__hip_atomic_fetch_add(&counters[1], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x - 1ull)
+    return;
+  if (__hip_atomic_load(&counters[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != expected) {
     __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -2013,6 +2069,11 @@ struct CachedPlan {
   const uint64_t *inv_ptr() const { return static_cast<const uint64_t *>(inv->p); }
   unsigned *gate_words() const { return static_cast<unsigned *>(gate->p); }
   uint64_t *base0_word() const { return reinterpret_cast<uint64_t *>(gate_words() + kGateSlots); }
+  // compact_copy_kernel's "not of the compact shape", for the device's kernels
+  // (every block of a launch reading the host-visible word costs ~1 ms)
+  unsigned *dev_broken_word() const { return reinterpret_cast<unsigned *>(base0_word() + 1); }
+  // inverse_count_kernel's listed-row count and finished-wave count
+  unsigned long long *count_words() const { return reinterpret_cast<unsigned long long *>(base0_word() + 2); }
   // Kernels of a call may still run on the device when an entry goes (it is
   // dropped or evicted on the host): wait for them before any member frees
   // what they read or write.
@@ -2100,11 +2161,15 @@ int cache_first_sighting(const PlanKey &key, const gp_double_index *idx, size_t 
 }
 
 // What a steady-state entry needs besides its plan: the gate words, the
-// host-visible "changed" word, and the compact copy of the index (built on s).
-int steady_state_setup(CachedPlan *p, const gp_double_index *idx, hipStream_t s) {
+// host-visible "changed" word, and the compact copy of the index (built on s);
+// with `copy_if_broken`, also the full copy into p->copy, written only if the
+// index is not of the compact shape (else nothing reads it).
+int steady_state_setup(CachedPlan *p, const gp_double_index *idx, hipStream_t s, bool copy_if_broken = false) {
   const PlanKey &key = p->key;
   int rc = GP_OK;
-  p->gate = std::make_shared<DevBuf>(kGateSlots * sizeof(unsigned) + sizeof(uint64_t), key.device, s, &rc);
+  // gate words, base0, broken, the inverse map's two counters
+  constexpr size_t kGateBytes = kGateSlots * sizeof(unsigned) + 4 * sizeof(uint64_t);
+  p->gate = std::make_shared<DevBuf>(kGateBytes, key.device, s, &rc);
   if (rc != GP_OK) return rc;
   p->changed = std::make_shared<PinnedWord>(key.device, &rc);
   if (rc != GP_OK) return rc;
@@ -2113,19 +2178,24 @@ int steady_state_setup(CachedPlan *p, const gp_double_index *idx, hipStream_t s)
   p->compact_broken = std::make_shared<PinnedWord>(key.device, &rc);
   if (rc != GP_OK) return rc;
   p->bytes += key.n * sizeof(uint32_t);
-  GP_HIP_TRY(hipMemsetAsync(p->gate->p, 0, kGateSlots * sizeof(unsigned), s));
+  GP_HIP_TRY(hipMemsetAsync(p->gate->p, 0, kGateBytes, s));
   const size_t g = std::max<size_t>(1, std::min((key.n + kBlock - 1) / kBlock, (size_t)num_cus() * 8));
   hipLaunchKernelGGL(compact_copy_kernel, dim3((unsigned)g), dim3(kBlock), 0, s, idx, key.n,
-                     static_cast<uint32_t *>(p->compact->p), p->base0_word(), p->compact_broken->p);
+                     static_cast<uint32_t *>(p->compact->p), p->base0_word(), p->compact_broken->p,
+                     p->dev_broken_word());
+  if (copy_if_broken)
+    hipLaunchKernelGGL(copy_if_broken_kernel, dim3((unsigned)g), dim3(kBlock), 0, s, idx, key.n,
+                       static_cast<gp_double_index *>(p->copy->p), p->dev_broken_word());
   GP_HIP_TRY(hipGetLastError());
   return GP_OK;
 }
 
 // The first call with an index whose residual has no ascending order: the
 // inverse plan (for rows of up to 128 floats, destinations below 2^32 and not
-// too sparse, kInvSpread).  It keeps a copy of the index (for the steady
-// state's check), builds the inverse map of the residual on s (fill, scatter,
-// check: generation `*gen` marks it unsound) and returns the entry; the caller
+// too sparse, kInvSpread).  It keeps the index's compact copy (or full copy)
+// for the steady state's check, builds the inverse map of the residual on s
+// (fill, scatter, count: generation `*gen` marks it unsound)
+// and returns the entry; the caller
 // launches the map's rows gated on soundness and the op-order residual gated
 // on the opposite.
 template <int OP>
@@ -2143,10 +2213,9 @@ int cache_inverse_plan(const PlanKey &key, const gp_double_index *idx, const Ent
   if (rc != GP_OK) return rc;
   p->inv = std::make_shared<DevBuf>(inv_rows * sizeof(uint64_t), key.device, s, &rc);
   if (rc != GP_OK) return rc;
-  rc = steady_state_setup(p.get(), idx, s);
+  rc = steady_state_setup(p.get(), idx, s, /*copy_if_broken=*/true);
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
-  GP_HIP_TRY(hipMemcpyAsync(p->copy->p, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
   GP_HIP_TRY(hipMemsetAsync(p->inv->p, 0xff, inv_rows * sizeof(uint64_t), s));
   *gen = ++p->gen;
   unsigned *word = p->gate_words() + *gen % kGateSlots;
@@ -2154,8 +2223,10 @@ int cache_inverse_plan(const PlanKey &key, const gp_double_index *idx, const Ent
   uint64_t *inv = static_cast<uint64_t *>(p->inv->p);
   hipLaunchKernelGGL(inverse_scatter_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, rr, key.off0,
                      key.off1, inv, word, p->changed->p, *gen);
-  hipLaunchKernelGGL(inverse_check_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, rr, key.off0,
-                     key.off1, inv, word, p->changed->p, *gen);
+  const size_t cper = (size_t)kBlock * kCountPerThread;
+  const size_t cgrid = std::max<size_t>(1, std::min((inv_rows + cper - 1) / cper, (size_t)num_cus()));
+  hipLaunchKernelGGL(inverse_count_kernel, dim3((unsigned)cgrid), dim3(kBlock), 0, s, inv, inv_rows,
+                     (uint64_t)p->resid, p->count_words(), word, p->changed->p, *gen);
   GP_HIP_TRY(hipGetLastError());
   GP_HIP_TRY(hipEventRecord(p->ready, s));
   *built = p;
@@ -2179,10 +2250,9 @@ int cache_ranges_plan(const PlanKey &key, const gp_double_index *idx, const Entr
   int rc = GP_OK;
   p->copy = std::make_shared<DevBuf>(key.n * sizeof(gp_double_index), key.device, s, &rc);
   if (rc != GP_OK) return rc;
-  rc = steady_state_setup(p.get(), idx, s);
+  rc = steady_state_setup(p.get(), idx, s, /*copy_if_broken=*/true);
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
-  GP_HIP_TRY(hipMemcpyAsync(p->copy->p, idx, key.n * sizeof(gp_double_index), hipMemcpyDeviceToDevice, s));
   GP_HIP_TRY(hipEventRecord(p->ready, s));
   cache_insert(std::move(p));
   return GP_OK;
@@ -2290,7 +2360,8 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     unsigned gen = ++cached->gen;
     if (gen == 0) gen = ++cached->gen;  // 0 is the gate words' initial value
     unsigned *word = cached->gate_words() + gen % kGateSlots;
-    // the compact copy once its build is known to have finished (never waits)
+    // the check's form once the host knows the compact copy's build finished
+    // (never waits); until then the device reads the build's flag (FORM 2)
     int compact = cached->compact_state.load(std::memory_order_acquire);
     if (compact < 0) {
       const hipError_t q = hipEventQuery(cached->ready);
@@ -2303,12 +2374,12 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     }
     const size_t per_block = (size_t)kBlock * kCmpPerThread;
     const size_t grid = std::max<size_t>(1, std::min((n + per_block - 1) / per_block, (size_t)num_cus() * 8));
-    if (compact == 1)
-      hipLaunchKernelGGL(index_verify_kernel<true>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx,
-                         cached->compact->p, n, cached->base0_word(), word, cached->changed->p, gen);
-    else
-      hipLaunchKernelGGL(index_verify_kernel<false>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx,
-                         cached->copy_ptr(), n, cached->base0_word(), word, cached->changed->p, gen);
+    auto verify = compact == 1   ? &index_verify_kernel<1>
+                  : compact == 0 ? &index_verify_kernel<0>
+                                 : &index_verify_kernel<2>;
+    hipLaunchKernelGGL(verify, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, cached->copy_ptr(),
+                       static_cast<const uint32_t *>(cached->compact->p), n, cached->base0_word(), word,
+                       cached->changed->p, gen, cached->dev_broken_word());
     GP_HIP_TRY(hipGetLastError());
     // dense runs only if unchanged; one row launch for both outcomes: the
     // sorted residual if unchanged, else every row of the call in op order
