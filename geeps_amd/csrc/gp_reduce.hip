@@ -2093,6 +2093,11 @@ struct CachedPlan {
   }
 };
 
+// gp_unplanned_stats_get's counters, in its field order
+enum UnplannedStat { kScans, kSteadyCalls, kStaleDrops, kInversePlans, kSortedPlans, kRangesPlans, kNumStats };
+std::atomic<uint64_t> g_unplanned_stats[kNumStats];
+inline void count_stat(UnplannedStat k) { g_unplanned_stats[k].fetch_add(1, std::memory_order_relaxed); }
+
 std::mutex g_plan_cache_mu;
 std::vector<std::shared_ptr<CachedPlan>> g_plan_cache;  // g_plan_cache_mu
 uint64_t g_plan_cache_tick = 0;                          // g_plan_cache_mu
@@ -2230,6 +2235,7 @@ int cache_inverse_plan(const PlanKey &key, const gp_double_index *idx, const Ent
   GP_HIP_TRY(hipGetLastError());
   GP_HIP_TRY(hipEventRecord(p->ready, s));
   *built = p;
+  count_stat(kInversePlans);
   cache_insert(std::move(p));
   return GP_OK;
 }
@@ -2254,6 +2260,7 @@ int cache_ranges_plan(const PlanKey &key, const gp_double_index *idx, const Entr
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
   GP_HIP_TRY(hipEventRecord(p->ready, s));
+  count_stat(kRangesPlans);
   cache_insert(std::move(p));
   return GP_OK;
 }
@@ -2312,6 +2319,7 @@ int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_doub
   if (rc != GP_OK) return rc;
   GP_HIP_TRY(hipEventRecord(p->ready, s));
   *built = p;
+  count_stat(kSortedPlans);
   cache_insert(std::move(p));
   return GP_OK;
 }
@@ -2330,6 +2338,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
   // a steady-state call since the last host look found the index changed: the
   // entry is stale, plan this call afresh (scan, host round trip)
   if (cached && cached->planned() && cached->changed->load() != 0) {
+    count_stat(kStaleDrops);
     cache_drop(cached);
     cached.reset();
   }
@@ -2357,6 +2366,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     // the cached dense runs and sorted residual (unchanged), or this call's
     // rows in op order (changed; as a first call runs its residual).  Exactly
     // one does any work; nothing waits for the host.
+    count_stat(kSteadyCalls);
     unsigned gen = ++cached->gen;
     if (gen == 0) gen = ++cached->gen;  // 0 is the gate words' initial value
     unsigned *word = cached->gate_words() + gen % kGateSlots;
@@ -2408,6 +2418,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
     return launch_row_op<OP>(y, x, cached->sorted_ptr(), cached->resid, gp_double_index{0, 0}, W, limit, s,
                              /*sorted=*/true, &select);
   }
+  count_stat(kScans);
   const size_t scan_bytes = kScanWordsOff + groups * kScanWords * sizeof(uint64_t);
   char *ws = nullptr;
   GP_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), scan_bytes, s));
@@ -2593,6 +2604,14 @@ int gp_unplanned_cache_clear(void) {
     std::lock_guard<std::mutex> lk(g_plan_cache_mu);
     gone.swap(g_plan_cache);
   }
+  return GP_OK;
+}
+
+int gp_unplanned_stats_get(gp_unplanned_stats *out) {
+  if (!out) return set_error(GP_ERR_INVALID, "null pointer");
+  uint64_t *f[kNumStats] = {&out->scans,         &out->steady_calls, &out->stale_drops,
+                            &out->inverse_plans, &out->sorted_plans, &out->ranges_plans};
+  for (int k = 0; k < kNumStats; ++k) *f[k] = g_unplanned_stats[k].load(std::memory_order_relaxed);
   return GP_OK;
 }
 

@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 11  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 12  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -55,6 +55,13 @@ class SumPlan(ctypes.Structure):
                 ("sweep_tile_kib", ctypes.c_int)]
 
 
+class UnplannedStats(ctypes.Structure):
+    """``gp_unplanned_stats``: what the unplanned calls' planning did (ABI 12)."""
+
+    _fields_ = [(n, ctypes.c_uint64) for n in ("scans", "steady_calls", "stale_drops", "inverse_plans",
+                                                "sorted_plans", "ranges_plans")]
+
+
 _c = ctypes
 _vp = _c.c_void_p
 _sz = _c.c_size_t
@@ -67,6 +74,7 @@ _SIGNATURES = {
     "gp_unplanned_cache_clear": (_i, []),
     "gp_unplanned_cache_entries": (_i, [_c.POINTER(_sz), _c.POINTER(_sz)]),
     "gp_set_unplanned_cache_bytes": (_i, [_sz]),
+    "gp_unplanned_stats_get": (_i, [_c.POINTER(UnplannedStats)]),
     "gp_scatter_add_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
     "gp_scatter_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz, _vp]),
@@ -151,6 +159,13 @@ def lib() -> ctypes.CDLL:
             raise ImportError("geeps_amd: libgp_reduce.so ABI version mismatch")
         _lib = handle
         return _lib
+
+
+def unplanned_stats() -> dict:
+    """gp_unplanned_stats_get as a dict (process-wide counters since start)."""
+    st = UnplannedStats()
+    check(lib().gp_unplanned_stats_get(ctypes.byref(st)), "gp_unplanned_stats_get")
+    return {name: getattr(st, name) for name, _ in UnplannedStats._fields_}
 
 
 def check(rc: int, what: str = "") -> None:

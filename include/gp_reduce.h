@@ -46,7 +46,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 11
+#define GP_ABI_VERSION 12
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -83,6 +83,19 @@ int gp_set_unplanned_min_bytes(size_t min_bytes);
 int gp_unplanned_cache_clear(void);
 int gp_unplanned_cache_entries(size_t *entries, size_t *bytes);
 int gp_set_unplanned_cache_bytes(size_t max_bytes);
+/* What the unplanned calls' planning did since the process started (ABI 12;
+ * process-wide counters, for tests and measurement). */
+typedef struct gp_unplanned_stats {
+  uint64_t scans;         /* calls that scanned their index (a first call, a re-plan) */
+  uint64_t steady_calls;  /* calls that ran a kept plan behind the device check */
+  uint64_t stale_drops;   /* kept plans dropped: a check found the index changed, or
+                             the inverse map built for it was unsound (a repeated
+                             destination, a source row past 2^32) */
+  uint64_t inverse_plans; /* inverse maps built (first calls) */
+  uint64_t sorted_plans;  /* destination-sorted residuals built (second calls) */
+  uint64_t ranges_plans;  /* ranges plans kept (first calls) */
+} gp_unplanned_stats;
+int gp_unplanned_stats_get(gp_unplanned_stats *out);
 
 /* ---------------------------------------------------------------------------
  * Row operations (client side).  Element (row r, value v) lives at
@@ -102,16 +115,18 @@ int gp_set_unplanned_cache_bytes(size_t max_bytes);
  * destination): destination rows index[r].id1 are distinct within one call.
  * `index` is a DEVICE pointer.  num_rows == 0 is a no-op.
  * Calls of at least gp_set_unplanned_min_bytes() of rows (default 64 MiB)
- * plan themselves on the device (ABI 10): one pass over the index finds its
+ * plan themselves on the device (ABI 10-12): one pass over the index finds its
  * dense runs (moved like a row plan's, by the phase-separated sum kernels) and
- * whether the other rows' destinations ascend; if they do not, the rows run in
- * op order and the next call with the same index builds a destination-sorted
- * copy of them (gp_unplanned_cache_clear).  These first two calls wait for the
+ * whether the other rows' destinations ascend; if they do not, rows of up to
+ * 128 floats go through an inverse map over destination rows, built by the
+ * same call (wider rows: op order, and the next call with the same index
+ * builds a destination-sorted copy of them).  A first call waits for the
  * stream once, for the index summary, as the reference's call waits at its end
  * (row-op-util.cu:141).  Later calls with the same index (ABI 11) do not: the
- * device compares the index with the kept copy and runs the sorted form if it
- * is unchanged, the op-order form if not, with no host round trip.  Smaller
- * calls are fully asynchronous.  Same results every way. */
+ * device compares the index with the kept copy and runs the kept plan if it is
+ * unchanged, the op-order form if not, with no host round trip.  Smaller
+ * calls are fully asynchronous.  Same results every way
+ * (gp_unplanned_cache_clear, gp_unplanned_stats_get). */
 int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
                         size_t num_rows, gp_double_index offset,
                         size_t row_size, size_t num_vals_limit, gp_stream s);

@@ -744,7 +744,8 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev, id0):
     (VERDICT r03 #4).  id0 "position" (the op buffer's rows in order, as the
     reference lists them) is checked against the compact copy (id1 only), a
     permuted id0 against the full copy."""
-    from geeps_amd import rowops
+    from geeps_amd import native, rowops
+    s0 = native.unplanned_stats()
     rng = np.random.default_rng(99)
     W, n = 128, 40000  # 20 MiB of rows: a cached (unsorted) residual
     x = rng.standard_normal(n * W).astype(np.float32)
@@ -769,6 +770,47 @@ def test_unplanned_plan_cache_checks_index_content(analyzed, dev, id0):
             # inverse map (8 B a destination row) and the compact copy (4 B)
             assert _cache_entries() == (1, 28 * n), (round_, call)
         prev = idx
+    # what ran (gp_unplanned_stats_get): 3 first calls (the first sighting and
+    # one re-plan per change), each building an inverse map; the other 8 calls
+    # steady, 2 of which found the change and had their plan dropped by the
+    # call after them
+    s1 = native.unplanned_stats()
+    d = {k: s1[k] - s0[k] for k in s1}
+    assert d == {"scans": 3, "steady_calls": 8, "stale_drops": 2, "inverse_plans": 3, "sorted_plans": 0,
+                 "ranges_plans": 0}, d
+
+
+def test_unplanned_repeated_destination_marks_the_inverse_map_unsound(analyzed, dev):
+    """A destination listed twice breaks the calls' precondition (the
+    reference's kernel races on it, row-op-util.cu:109-125): the inverse map
+    can list only one of the two entries.  inverse_count_kernel finds fewer
+    listed rows than entries, the gated op-order form runs instead of the
+    map's walk, and the next call drops the plan and plans afresh
+    (gp_unplanned_stats_get).  The repeated entries' source rows are zero
+    here, so the sums are the same whatever order the racing adds land in,
+    and exact."""
+    from geeps_amd import native, rowops
+    rng = np.random.default_rng(17)
+    W, n = 128, 40000
+    idx = np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64)
+    a = rng.choice(n, 64, replace=False)
+    b, c = a[:32], a[32:]
+    idx[c, 1] = idx[b, 1]  # 32 destinations listed twice
+    x = rng.standard_normal(n * W).astype(np.float32)
+    x.reshape(n, W)[idx[a, 0]] = 0.0
+    y = rng.standard_normal(n * W).astype(np.float32)
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, (0, 0), W)
+    tx, ti = T(x, dev), torch.from_numpy(idx).to(dev)
+    s0 = native.unplanned_stats()
+    for call in range(2):
+        ty = T(y, dev)
+        rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W, validate=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), call
+    s1 = native.unplanned_stats()
+    d = {k: s1[k] - s0[k] for k in s1}
+    assert d["inverse_plans"] == 2 and d["scans"] == 2 and d["stale_drops"] == 1 and d["steady_calls"] == 0, d
 
 
 def test_unplanned_cache_capacity_bound(analyzed, dev):
