@@ -459,25 +459,25 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
             writes = R * 512
             launches, other, share, kernel_id = 1, 0, 1.0, None
             # the unplanned calls plan themselves on the device (gp_reduce.h,
-            # ABI 10): an index scan, then the sweep forms for dense runs and
-            # the row kernels for the rest; a scatter's unsorted rest runs in op
-            # order on the first call with an index (`first_call_ms`), the
-            # second call sorts it by destination and runs that
-            # (`second_call_ms`), later calls run the plan cache's sorted copy
-            # (`avg_ms`, the reference reusing each op's DoubleIndex every clock).  The
-            # time includes the scan and the call's one stream sync, as the
-            # reference's call syncs too.
-            scan = "index_scan_kernel + "
+            # ABI 10-12): the first call with an index (`first_call_ms`) scans
+            # it (one stream sync, as the reference's call syncs too), runs
+            # its dense runs through the sweep forms and the rest through the
+            # row kernels -- a scatter's unsorted rest through an inverse map
+            # it builds -- and keeps the plan; later calls (`second_call_ms`,
+            # `avg_ms`: the reference reusing each op's DoubleIndex every
+            # clock) run it behind the device check, with no host round trip.
+            # `plan_stats`: gp_unplanned_stats_get over this leg's calls.
+            scan = "index_verify_kernel + "
             if name == "scatter_add":
                 fn = lambda: rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                    validate=False)
                 kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity"
-                                 else "row_wave_kernel (cached sorted residual)")
+                                 else "row_wave_kernel (the kept inverse map)")
             elif name == "scatter_init":
                 fn = lambda: rowops.init_rows_from_double_index_gpu(y, x, idx, R, (0, 0), 128, R * 128,
                                                                     validate=False)
                 kernel = scan + ("bucket_sum_sweep_kernel" if kind == "identity"
-                                 else "row_wave_kernel (cached sorted residual)")
+                                 else "row_wave_kernel (the kept inverse map)")
             elif name == "gather":
                 fn = lambda: rowops.assign_rows_to_double_index_gpu(x, y, idx, R, (0, 0), 128, R * 128,
                                                                     validate=False)
@@ -513,15 +513,19 @@ def rowops_leg(rows, W, dev, reps=5, indexes=("random", "identity"), only=None, 
                 else:
                     kernel = "row_wave_kernel"
             first_ms = second_ms = None
+            s0 = native.unplanned_stats()
             if not planned:  # the first and second calls with this index on their own
                 native.check(native.lib().gp_unplanned_cache_clear(), "gp_unplanned_cache_clear")
                 first_ms = _time_calls(fn, 1, stream, warmup=False)
                 second_ms = _time_calls(fn, 1, stream, warmup=False)
             avg = _time_calls(fn, reps, stream)
+            s1 = native.unplanned_stats()
             gbps = nbytes / (avg / 1e3) / 1e9
             leg = {"avg_ms": round(avg, 4), "GBps": round(gbps, 1),
                    "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes": nbytes, "kernel": kernel,
                    "launches": launches, "avg_launch_ms": round(avg * share / launches, 5)}
+            if not planned:
+                leg["plan_stats"] = {k: s1[k] - s0[k] for k in s1}
             if first_ms is not None:
                 leg["first_call_ms"] = round(first_ms, 4)
                 leg["first_call_frac"] = round(nbytes / (first_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
