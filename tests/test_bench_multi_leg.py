@@ -1,0 +1,77 @@
+"""bench.py --gpus N's drop-in leg, control flow only (CPU): rank 0 runs the
+one-process-per-GPU libgeeps leg while every other rank waits on a file store
+without touching a GPU, then all ranks go on.
+The leg itself is stubbed here (it needs N GPUs); a leg that raises still
+releases the other ranks and is reported, not fatal."""
+import multiprocessing as mp
+import os
+import socket
+import sys
+import time
+from types import SimpleNamespace
+
+import pytest
+
+from conftest import REPO
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, fail, out):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_PORT=str(port))
+    sys.path.insert(0, REPO)
+    import bench
+
+    def leg(n, rows, W):
+        time.sleep(1.0)  # the other ranks must still be waiting
+        if fail:
+            raise RuntimeError("stub leg failed")
+        return {"processes": n, "rows": rows, "W": W, "done_at": time.time()}
+
+    bench.libgeeps_multi_gpu_leg = leg
+    args = SimpleNamespace(no_e2e=False, no_multi_e2e=False, rows=1024, width=8)
+    res = bench.pre_gpu_multi_leg(args, "nccl")
+    out.put((rank, res, time.time()))
+
+
+@pytest.mark.parametrize("world,fail", [(2, False), (4, False), (2, True)])
+def test_rank0_runs_the_leg_while_the_others_wait(world, fail):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, fail, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, res, t = q.get(timeout=120)
+        got[rank] = (res, t)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res0, _ = got[0]
+    if fail:
+        assert "stub leg failed" in res0["error"]
+    else:
+        assert res0["processes"] == world and res0["rows"] == 1024 and res0["W"] == 8
+        for r in range(1, world):
+            assert got[r][0] is None
+            assert got[r][1] >= res0["done_at"]  # released only after the leg finished
+
+
+def test_world_one_and_other_backends_skip_the_leg():
+    sys.path.insert(0, REPO)
+    import bench
+    args = SimpleNamespace(no_e2e=False, no_multi_e2e=False, rows=1024, width=8)
+    assert bench.pre_gpu_multi_leg(args, "nccl") is None  # WORLD_SIZE unset: N = 1
+    os.environ["WORLD_SIZE"] = "2"
+    try:
+        assert bench.pre_gpu_multi_leg(args, "gloo") is None
+        assert bench.pre_gpu_multi_leg(SimpleNamespace(no_e2e=False, no_multi_e2e=True, rows=1, width=1),
+                                       "nccl") is None
+    finally:
+        del os.environ["WORLD_SIZE"]
