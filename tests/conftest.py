@@ -26,7 +26,8 @@ FAMILIES = [
      "test_libgeeps", ("test_one_process_per_gpu_rehearsal",)),
     ("configs[2] 8 shards: RCCL-shaped exchange (gloo ranks) + one process per GPU", "",
      ("test_sharded_reduction", "test_bench_multirank_flow", "test_one_process_per_gpu",
-      "test_world_one_is_local", "test_hosting_requires_divisible_clients")),
+      "test_world_one_is_local", "test_hosting_requires_divisible_clients",
+      "test_rank0_runs_the_leg", "test_world_one_and_other_backends")),
     ("configs[3] Inception CIFAR-10 table, 2 workers", "test_libgeeps",
      ("test_config4_inception_cifar_two_workers",)),
     ("configs[4] AlexNet table, 8 workers x 8 shards, staleness 1", "test_libgeeps",
@@ -34,10 +35,11 @@ FAMILIES = [
     ("north star: 8-way 1M x 1024 sum, full size vs oracle/torch", "test_gpu_parity",
      ("test_full_size_8way_bucket_sum",)),
     ("bucket sum (server apply_updates) vs oracle", "test_gpu_parity",
-     ("test_bucket_sum", "test_golden_bucket", "test_gpu_add_and_zero")),
+     ("test_bucket_sum", "test_golden_bucket", "test_gpu_add_and_zero", "test_sum_past_the_reference")),
     ("row ops, unplanned C-ABI (add_rows_from_double_index_gpu ...) vs oracle", "test_gpu_parity",
      ("test_rowop", "test_golden_rowops", "test_scatter_init", "test_segmented", "test_side_stream",
-      "test_out_of_range", "test_empty_calls", "test_full_size_scatter_add", "test_unplanned")),
+      "test_out_of_range", "test_empty_calls", "test_full_size_scatter_add", "test_unplanned",
+      "test_row_ops_past_the_reference")),
     ("row / gather plans (libgeeps Update / Read) vs oracle", "test_gpu_parity",
      ("test_row_plan", "test_gather_plan")),
     ("C-ABI from C99 vs oracle", "test_gpu_parity", ("test_c_abi_consumer",)),

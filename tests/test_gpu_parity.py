@@ -486,6 +486,59 @@ def test_full_size_scatter_add_permuted(dev):
     assert torch.equal(y, y0)
 
 
+@pytest.mark.slow
+def test_sum_past_the_reference_int_range(dev):
+    """The reference's sum takes an `int` element count (cpu_add<float>, CHECK_GT
+    n > 0, math_functions.cpp:132-136; CUDA_KERNEL_LOOP's int index,
+    device_alternate.hpp:31-54), so one call stops short of 2^31 elements.  The
+    C-ABI's counts are size_t: a 2-bucket sum over 2^31 + 4,099 floats (8 GiB
+    per buffer, a ragged tail through the tile-major and scalar forms) is
+    bit-exact against torch fp32 in client order over every element."""
+    from geeps_amd import rowops
+    n = (1 << 31) + 4099
+    g = torch.Generator(device=dev)
+    g.manual_seed(31)
+    buckets = [torch.rand(n, generator=g, device=dev) - 0.5 for _ in range(2)]
+    master = torch.rand(n, generator=g, device=dev) - 0.5
+    expect = master.clone()
+    for b in buckets:
+        expect += b
+    rowops.bucket_sum_apply(master, buckets)
+    torch.cuda.synchronize()
+    assert torch.equal(master.view(torch.int32), expect.view(torch.int32))
+
+
+@pytest.mark.slow
+def test_row_ops_past_the_reference_int_range(dev):
+    """2^24 + 7 RowData rows = 2^31 + 896 floats per side, past the
+    reference kernels' int element index (row-op-util.cu's CUDA_KERNEL_LOOP):
+    the unplanned scatter-add on a random permutation (its first call builds
+    the inverse map, the second runs it behind the device check) and the
+    gather with the roles swapped, every row against torch on integer-valued
+    data (exact)."""
+    from geeps_amd import rowops
+    R, W = (1 << 24) + 7, 128
+    g = torch.Generator(device=dev)
+    g.manual_seed(24)
+    perm = torch.randperm(R, generator=g, device=dev)
+    idx = torch.stack([torch.arange(R, device=dev), perm], 1).contiguous()
+    x = torch.randint(-64, 64, (R * W,), generator=g, device=dev).float()
+    y = torch.randint(-64, 64, (R * W,), generator=g, device=dev).float()
+    full = y.view(R, W).clone()
+    full[perm] += x.view(R, W)
+    for call in range(2):  # y + x, then y + 2x
+        rowops.add_rows_from_double_index_gpu(y, x, idx, R, (0, 0), W, R * W, validate=False)
+        torch.cuda.synchronize()
+        assert torch.equal(y.view(R, W).view(torch.int32), full.view(torch.int32)), call
+        full[perm] += x.view(R, W)
+    del full
+    out = torch.zeros(R * W, device=dev)
+    gidx = torch.stack([perm, torch.arange(R, device=dev)], 1).contiguous()  # out[perm[r]] = y[r]
+    rowops.assign_rows_to_double_index_gpu(out, y, gidx, R, (0, 0), W, R * W, validate=False)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(R, W)[perm], y.view(R, W))
+
+
 @pytest.mark.parametrize("W,limit_frac,shift", [(128, None, 0), (64, 0.55, 0), (130, None, 0),
                                                (128, 0.7, 1), (1024, None, 0)])
 def test_scatter_init_equals_zero_then_add(dev, W, limit_frac, shift):
