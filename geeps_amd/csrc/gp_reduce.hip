@@ -1858,12 +1858,12 @@ __global__ __launch_bounds__(kBlock) void inverse_scatter_kernel(const gp_double
 }
 
 // Whether the inverse map lists exactly `expected` rows (the residual's
-// entries): one sequential pass over it (8 loads in flight per thread), a
+// entries): one sequential pass over it (16 loads in flight per thread), a
 // block sum, one atomic add per block (a launch of about one block per CU:
 // per-wave atomics on one address measured 254 us); the last block to finish
 // compares and, on a shortfall (a repeated destination), marks the map
 // unsound as inverse_scatter_kernel does.
-constexpr int kCountPerThread = 8;
+constexpr int kCountPerThread = 16;
 __global__ __launch_bounds__(kBlock) void inverse_count_kernel(const uint64_t *__restrict__ inv, size_t rows,
                                                                uint64_t expected, unsigned long long *counters,
                                                                unsigned *__restrict__ gate_word,
