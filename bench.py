@@ -753,27 +753,42 @@ def libgeeps_multi_gpu_leg(n_gpus, rows, W, clocks=5, warmup=2, alex_clocks=10, 
     if gpus >= n_gpus:  # one process per GPU: the default hardware queues
         base_env["CLOCK_BENCH_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES", "4")
     failed = None
-    for table, nrows, slack, ck in (("1Mx1024", rd_rows, 0, clocks), ("alexnet", ALEXNET_ROWS, 1, alex_clocks)):
-        if table not in tables:
+    # the default cross-GPU path (staged) on both tables first, then in place;
+    # the whole leg within a time budget, so the scaling runs it precedes stay
+    # short (GEEPS_BENCH_MULTI_BUDGET_S, default 150 s)
+    budget_s = float(os.environ.get("GEEPS_BENCH_MULTI_BUDGET_S", "150"))
+    out["budget_s"] = budget_s
+    t_leg = time.monotonic()
+    runs = [(table, nrows, slack, ck, path, env)
+            for path, env in PEER_PATHS.items()
+            for table, nrows, slack, ck in (("1Mx1024", rd_rows, 0, clocks), ("alexnet", ALEXNET_ROWS, 1, alex_clocks))
+            if table in tables]
+    for table, nrows, slack, ck, path, env in runs:
+        key = f"{table}_{path}"
+        if failed:  # one failure (or hang) ends the leg: the headline must not wait on it
+            out[key] = {"skipped": f"after {failed} failed"}
             continue
-        for path, env in PEER_PATHS.items():
-            key = f"{table}_{path}"
-            if failed:  # one failure (or hang) ends the leg: the headline must not wait on it
-                out[key] = {"skipped": f"after {failed} failed"}
-                continue
-            try:
-                r = mod.run(n_gpus, nrows, ck, warmup, slack, "ipc", timeout=150,
-                            extra_env=dict(base_env, **env))
-            except Exception as exc:  # report it, skip the rest
-                out[key] = {"error": f"{type(exc).__name__}: {str(exc)[-800:]}"}
-                failed = key
-                continue
-            out[key] = {"rows": nrows, "slack": slack, "ms_per_clock": r["ms_per_clock_max"],
-                        "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],
-                        "read_checked": r["read_checked"], "devices": r["devices"],
-                        "nr_peer_staged": r.get("nr_peer_staged"),
-                        "nr_refresh_staged": r.get("nr_refresh_staged"),
-                        "nr_refresh_in_place": r.get("nr_refresh_in_place")}
+        left = budget_s - (time.monotonic() - t_leg)
+        if left < 20:
+            out[key] = {"skipped": f"the leg's {budget_s:.0f}-s budget is spent"}
+            continue
+        t_run = time.monotonic()
+        try:
+            r = mod.run(n_gpus, nrows, ck, warmup, slack, "ipc", timeout=max(20.0, min(150.0, left)),
+                        extra_env=dict(base_env, **env))
+        except Exception as exc:  # report it, skip the rest
+            out[key] = {"error": f"{type(exc).__name__}: {str(exc)[-800:]}",
+                        "wall_s": round(time.monotonic() - t_run, 1)}
+            failed = key
+            continue
+        out[key] = {"rows": nrows, "slack": slack, "ms_per_clock": r["ms_per_clock_max"],
+                    "wall_s": round(time.monotonic() - t_run, 1),
+                    "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],
+                    "read_checked": r["read_checked"], "devices": r["devices"],
+                    "nr_peer_staged": r.get("nr_peer_staged"),
+                    "nr_refresh_staged": r.get("nr_refresh_staged"),
+                    "nr_refresh_in_place": r.get("nr_refresh_in_place")}
+    out["wall_s"] = round(time.monotonic() - t_leg, 1)
     return out
 
 

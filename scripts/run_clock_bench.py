@@ -21,6 +21,7 @@ import json
 import os
 import socket
 import subprocess
+import time
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -91,12 +92,15 @@ def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900, extra_en
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
              for p in range(P)]
     results, errors = [], []
+    deadline = time.monotonic() + timeout  # one deadline for all P processes
     for p, pr in enumerate(procs):
         try:
-            o, e = pr.communicate(timeout=timeout)
+            o, e = pr.communicate(timeout=max(0.1, deadline - time.monotonic()))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
+            for q in procs:
+                q.wait()
             raise
         if pr.returncode != 0:
             errors.append(f"process {p} rc={pr.returncode}\n{e[-2000:]}")

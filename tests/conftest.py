@@ -27,7 +27,7 @@ FAMILIES = [
     ("configs[2] 8 shards: RCCL-shaped exchange (gloo ranks) + one process per GPU", "",
      ("test_sharded_reduction", "test_bench_multirank_flow", "test_one_process_per_gpu",
       "test_world_one_is_local", "test_hosting_requires_divisible_clients",
-      "test_rank0_runs_the_leg", "test_world_one_and_other_backends")),
+      "test_rank0_runs_the_leg", "test_world_one_and_other_backends", "test_leg_")),
     ("configs[3] Inception CIFAR-10 table, 2 workers", "test_libgeeps",
      ("test_config4_inception_cifar_two_workers",)),
     ("configs[4] AlexNet table, 8 workers x 8 shards, staleness 1", "test_libgeeps",

@@ -75,3 +75,50 @@ def test_world_one_and_other_backends_skip_the_leg():
                                        "nccl") is None
     finally:
         del os.environ["WORLD_SIZE"]
+
+
+class _FakeClockBench:
+    """Stands in for scripts/run_clock_bench.py: records the runs, sleeps `cost` s each."""
+    BIN = __file__
+
+    def __init__(self, cost=0.0, fail_on=None):
+        self.calls, self.cost, self.fail_on = [], cost, fail_on
+
+    def run(self, P, rows, clocks, warmup, slack, transport, timeout, extra_env):
+        path = "staged" if extra_env["GEEPS_STAGE_PEER_UPDATES"] == "1" else "in_place"
+        self.calls.append((rows, path, timeout))
+        time.sleep(self.cost)
+        if self.fail_on == (len(self.calls) - 1):
+            raise RuntimeError("fake failure")
+        return {"ms_per_clock_max": 1.0, "aggregate_delta_GBps": 1.0, "read_ok": True, "read_checked": 1,
+                "devices": list(range(P))}
+
+
+def _leg(monkeypatch, fake, budget=None):
+    sys.path.insert(0, REPO)
+    import bench
+    monkeypatch.setattr(bench, "_clock_bench_module", lambda: fake)
+    if budget is not None:
+        monkeypatch.setenv("GEEPS_BENCH_MULTI_BUDGET_S", str(budget))
+    return bench.libgeeps_multi_gpu_leg(8, 1024, 1024, gpus_seen=8)
+
+
+def test_leg_runs_the_staged_path_first_within_its_budget(monkeypatch):
+    fake = _FakeClockBench()
+    out = _leg(monkeypatch, fake)
+    assert [c[1] for c in fake.calls] == ["staged", "staged", "in_place", "in_place"]
+    assert all(out[k]["read_ok"] for k in ("1Mx1024_staged", "alexnet_staged", "1Mx1024_in_place",
+                                           "alexnet_in_place"))
+    assert all(c[2] <= 150 for c in fake.calls)
+    # a spent budget skips the rest (the scaling runs after it stay short)
+    fake = _FakeClockBench(cost=0.3)
+    out = _leg(monkeypatch, fake, budget=20.5)
+    assert len(fake.calls) == 2 and "budget" in out["alexnet_in_place"]["skipped"]
+
+
+def test_leg_stops_at_its_first_failure(monkeypatch):
+    fake = _FakeClockBench(fail_on=0)
+    out = _leg(monkeypatch, fake)
+    assert len(fake.calls) == 1 and "fake failure" in out["1Mx1024_staged"]["error"]
+    assert all("after 1Mx1024_staged failed" in out[k]["skipped"]
+               for k in ("alexnet_staged", "1Mx1024_in_place", "alexnet_in_place"))
