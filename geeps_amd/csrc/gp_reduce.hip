@@ -144,12 +144,22 @@ struct Gate {
   const uint64_t *inv;
 };
 
+// The gate word was written by an earlier launch on the stream and no kernel
+// writes it while a gated one runs, so it is read as constant memory: a
+// scalar load through the scalar cache (invalidated at every kernel start),
+// not a system-coherent vector load that goes out to memory -- the first
+// thing every block of a gated launch waits for (the steady state of a
+// dense-run index is ~43 gated sweep launches).
 __device__ __forceinline__ bool gate_changed(const Gate &g) {
-  return __hip_atomic_load(g.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g.gen;  // block-uniform
+  typedef const __attribute__((address_space(4))) unsigned CU;
+  return *(CU *)(g.word) == g.gen;  // block-uniform (C-style: an address-space cast)
 }
 
 __device__ __forceinline__ bool gate_closed(const Gate &g) {
-  return g.mode != kGateSelect && (g.mode == kGateIfSame) == gate_changed(g);
+  // bitwise, so the mode, word pointer and generation load together (one
+  // round trip, then the word's)
+  const bool changed = gate_changed(g);
+  return (g.mode != kGateSelect) & ((g.mode == kGateIfSame) == changed);
 }
 
 // A row kernel's GATED prologue: exit, or (select) switch to the alternative
@@ -418,9 +428,6 @@ template <int NB, int RT = kSweepRT, int TG = kSweepTG, bool ZIN = false, int U 
 __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
     f4 *__restrict__ out, const f4 *__restrict__ in, BucketPtrs b, size_t n4_tiles,
     size_t chunk, Gate gate = Gate{}) {
-  if constexpr (GATED) {
-    if (gate_closed(gate)) return;
-  }
   constexpr int kTile = kBlock * U;            // f4 per tile
   constexpr int kLds = kPhaseLdsF4 / kTile;    // tiles parked in LDS
   static_assert(kLds * kTile == kPhaseLdsF4, "whole LDS tiles");
@@ -441,7 +448,13 @@ __global__ __launch_bounds__(kBlock) void bucket_sum_sweep_kernel(
   // into load -> vmcnt(0) -> add chains (117-224 full drains per chunk, 8.3
   // instead of 6.5 ms at 8 buckets; profiles/r01b/sweep_ab.txt).
   // tests/test_kernel_schedule.py checks the schedule on the assembly.
-  if (lo >= n4_tiles) return;
+  // GATED: the gate test joins this exit, so its word's load waits on the
+  // same first batch of argument loads as the rest of the prologue (a
+  // separate test first cost each launch a round trip more, ~1.5 % of a
+  // 64-MiB chunk's 21 us).
+  bool closed = false;
+  if constexpr (GATED) closed = gate_closed(gate);
+  if (lo >= n4_tiles || closed) return;
 #pragma unroll
   for (int k = 0; k < S; ++k) {
 #pragma unroll
