@@ -17,8 +17,9 @@
  *     after every launch: src/common/row-op-util.cu:141); the caller syncs.
  *     The one exception: a large unplanned row call (gp_scatter_add_rows and
  *     kin, >= gp_set_unplanned_min_bytes) waits for its stream once on the
- *     first two calls with an index (the device scan's summary); from the
- *     third call with the same index on it is asynchronous too (ABI 11);
+ *     first call with an index (the device scan's summary; also on the second
+ *     for a scatter of rows over 128 floats, which sorts then); later calls
+ *     with the same index are asynchronous too (ABI 11, 12);
  *   - errors are returned as a status code (0 = GP_OK) with a thread-local
  *     message from gp_last_error(), instead of a glog FATAL abort
  *     (src/common/gpu-util/device_alternate.hpp:16-28).  The C++ layer above
