@@ -874,6 +874,21 @@ def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
                                             "ms_per_clock": r["ms_per_clock_max"],
                                             "delta_GBps": r["aggregate_delta_GBps"], "direct_read": True,
                                             "read_ops": "one per server shard"}
+    # SURVEY §8(f)'s next rows, measured: read-my-writes (f#4: every refresh
+    # re-applies the worker's own unpushed oplog, clientlib-data.cpp:132-150)
+    # at configs[1]'s 2 processes, and the socket path other nodes take (f#2:
+    # D2H of the oplog slice, ZMTP frames over loopback TCP, the server's H2D
+    # and sum, the refresh back the same way) on the AlexNet-sized table
+    r = mod.run(2, rd_rows, clocks, warmup, 0, "ipc", timeout=120, extra_env={"CLOCK_BENCH_RMW": "1"})
+    out["p2_read_my_writes"] = {"workers": 2, "ms_per_clock": r["ms_per_clock_max"],
+                                "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],
+                                "read_my_writes": True}
+    r = mod.run(2, ALEXNET_ROWS, clocks, warmup, 0, "tcp", timeout=120)
+    moved = 2 * 2 * (ALEXNET_ROWS // 2) * 512  # each worker: its slice out, the peer shard back
+    out["p2_alexnet_tcp"] = {"workers": 2, "rows": ALEXNET_ROWS, "ms_per_clock": r["ms_per_clock_max"],
+                             "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],
+                             "socket_GBps": round(moved / (r["ms_per_clock_max"] * 1e-3) / 1e9, 2),
+                             "transport": "ZMTP/3.0 over loopback TCP (the other-node path)"}
     return out
 
 

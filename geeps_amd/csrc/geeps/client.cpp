@@ -729,12 +729,13 @@ void ClientLib::decide_fused_init() {
     for (uint32_t t = 0; t < config_.num_tables; ++t) {
       const ParamCache &pc = ch.tables[t];
       std::vector<uint8_t> seen(pc.num_rows, 0);
-      size_t covered = 0;
+      size_t covered = 0, writers = 0;
       bool ok = pc.num_rows > 0;
       for (size_t i = 0; i < end && ok; ++i) {
         const OpInfo &w = opseq_[i];
         if (w.type != OpInfo::WRITE || w.local || w.table_id != t) continue;
         const OpInfo &pre = opseq_[w.prestep_handle];
+        bool here = false;
         if (pre.num_vals_limit < pre.rows.size() * ROW_DATA_SIZE) ok = false;
         // the op's id1 set in this channel is the contiguous range checked in
         // create_double_index; recover it from the row ids
@@ -743,13 +744,19 @@ void ClientLib::decide_fused_init() {
           const size_t id1 = pc.index.at(r);
           if (seen[id1]++) ok = false;
           ++covered;
+          here = true;
         }
+        writers += here;
       }
       // Read-my-writes re-applies a refresh's pending oplogs, the current
-      // clock's included (recv_row_batch): its rows must be zero until an
-      // op writes them, as after the reference's zerofy (clientlib-data.cpp:
-      // 356-371), so that mode keeps the zeroed oplog.
-      ch.init_ok[t] = ok && covered == pc.num_rows && !config_.read_my_writes;
+      // clock's included (recv_row_batch): its rows must be zero until an op
+      // writes them, as after the reference's zerofy (clientlib-data.cpp:
+      // 356-371).  With ONE update op per clock in this (channel, table) the
+      // oplog is created and fully written inside that Update, under the
+      // channel lock a refresh takes too (and synced before it is released),
+      // so no refresh sees it unwritten: the fused init stays.  With several,
+      // a refresh between two of them would: zeroed oplog.
+      ch.init_ok[t] = ok && covered == pc.num_rows && (!config_.read_my_writes || writers == 1);
     }
   }
   // Direct oplog: an update op whose rows are one channel's cache rows in
@@ -763,8 +770,11 @@ void ClientLib::decide_fused_init() {
     OpInfo &w = opseq_[i];
     if (w.type != OpInfo::WRITE || w.local) continue;
     OpInfo &pre = opseq_[w.prestep_handle];
+    // (not with read-my-writes: the app would write the oplog between
+    // PreUpdate and Update, outside the channel lock a refresh's re-apply of
+    // that oplog takes)
     pre.direct = direct_oplog_ && pre.direct_channel >= 0 && !pre.rows.empty() &&
-                 channels_[pre.direct_channel]->init_ok[pre.table_id];
+                 channels_[pre.direct_channel]->init_ok[pre.table_id] && !config_.read_my_writes;
   }
 }
 
@@ -1324,14 +1334,20 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
                      "copied refresh from server " << server_id << " into an unallocated cache");
         float *dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
         const size_t floats = num_rows * ROW_DATA_SIZE;
-        GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.svc_stream->get()));
-        if (config_.read_my_writes) {
+        std::vector<const float *> own;  // read-my-writes: the unreflected clocks' oplog slices, in order
+        if (config_.read_my_writes)
           for (iter_t c = self_clock + 1, fc = fast_clock_.load(); c <= fc; ++c) {
             auto it = pc.oplog.find(c);
-            if (it == pc.oplog.end()) continue;
-            const float *op = it->second->data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
-            GP_CALL(gp_add(floats, dst, op, dst, ch.svc_stream->get()));
+            if (it != pc.oplog.end()) own.push_back(it->second->data() + pc.server_row_start[server_id] * ROW_DATA_SIZE);
           }
+        if (version >= 0 && !staged) {
+          // a same-GPU master version (read-my-writes): copy and re-apply in
+          // one pass, dst = ((shard + own[0]) + own[1]) + ..., the bits of the
+          // copy-then-add sequence below, through the N-way sum kernels
+          GP_CALL(gp_bucket_sum_into(dst, rows, own.data(), (int)own.size(), floats, ch.svc_stream->get()));
+        } else {
+          GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.svc_stream->get()));
+          for (const float *op : own) GP_CALL(gp_add(floats, dst, op, dst, ch.svc_stream->get()));
         }
         ch.svc_stream->sync();
         if (version >= 0) released.push_back(version);  // copied: give it back now

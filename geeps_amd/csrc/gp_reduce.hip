@@ -2878,9 +2878,14 @@ int gp_bucket_sum_into(float *out, const float *in, const float *const *buckets,
   for (int k = 0; k < num_buckets; ++k)
     if (!buckets[k]) return set_error(GP_ERR_INVALID, "null bucket pointer");
   if (num_buckets == 0) {
-    if (out != in)
-      GP_HIP_TRY(hipMemcpyAsync(out, in, num_vals * sizeof(float), hipMemcpyDeviceToDevice,
-                                (hipStream_t)s));
+    // the copy through the sweep kernels' copy form: an IPC-mapped `in` (a
+    // peer process's master version) sends hipMemcpyAsync to a copy engine,
+    // measured at 1.3 TB/s for 2 GiB where this runs at the HBM copy rate
+    if (out != in) {
+      const int rc = launch_bucket_sum_nb<0>(out, in, BucketPtrs{}, num_vals, (hipStream_t)s);
+      if (rc != GP_OK) return rc;
+      GP_HIP_TRY(hipGetLastError());
+    }
     return GP_OK;
   }
   // The first launch reads `in` and writes `out`; any further launches (more

@@ -65,6 +65,9 @@ int main(int argc, char **argv) {
   }
   HCK(hipSetDevice(device));
   GeePsConfig cfg;
+  // CLOCK_BENCH_RMW: read-my-writes (each Read adds this worker's own
+  // unpushed updates to the refreshed rows, clientlib-data.cpp:132-150)
+  if (std::getenv("CLOCK_BENCH_RMW")) cfg.read_my_writes = 1;
   for (int i = 0; i < P; ++i) {
     cfg.host_list.push_back("127.0.0.1");
     cfg.port_list.push_back(base + 16 * i);

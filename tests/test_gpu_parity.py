@@ -144,6 +144,25 @@ def test_bucket_sum_into_leaves_master(dev, N):
     assert np.array_equal(bits(m.cpu().numpy()), bits(m0))
 
 
+@pytest.mark.parametrize("n,shift", [(3 * 96 * (1 << 18) + 5, 0), (5 * 64 * (1 << 18) + 3, 1), (1 << 20, 2)])
+def test_bucket_sum_into_zero_buckets_copies(dev, n, shift):
+    """gp_bucket_sum_into with no buckets is a copy (libgeeps' read-my-writes
+    refresh of a shard with no pending own updates): through the sweep
+    kernels' copy form, whole chunks, the tile-major rest and the scalar tail,
+    on 16-B-aligned and unaligned (shifted) buffers; every bit equal, `in`
+    untouched."""
+    from geeps_amd import rowops
+    g = torch.Generator(device=dev)
+    g.manual_seed(n)
+    src = torch.rand(n + shift, generator=g, device=dev) - 0.5
+    dst = torch.full((n + shift,), float("nan"), dtype=torch.float32, device=dev)
+    s0 = src.clone()
+    rowops.bucket_sum_into(dst[shift:], src[shift:], [])
+    torch.cuda.synchronize()
+    assert torch.equal(dst[shift:].view(torch.int32), src[shift:].view(torch.int32))
+    assert torch.equal(src.view(torch.int32), s0.view(torch.int32))
+
+
 @pytest.mark.parametrize("N,out_of_place", [(1, False), (3, False), (8, False), (8, True), (11, True)])
 def test_bucket_sum_phase_separated_path(dev, N, out_of_place):
     """128-MiB shards take the phase-separated kernel in balanced chunks (reads
