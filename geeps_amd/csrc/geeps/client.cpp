@@ -449,6 +449,34 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
   return true;
 }
 
+namespace {
+// Rows bound for a socket leave the GPU in pieces of this size, each sent as
+// soon as its copy lands (send_frame_chunked), so the D2H of a large slice
+// overlaps the send instead of preceding it.
+constexpr size_t kWireChunk = 16u << 20;
+
+// The device-to-host copy of `bytes` from `src` into pinned `dst` on `st`, an
+// event recorded after each kWireChunk piece.
+void copy_out_in_pieces(void *dst, const void *src, size_t bytes, const Stream &st,
+                        std::vector<std::unique_ptr<Event>> &events) {
+  const size_t pieces = (bytes + kWireChunk - 1) / kWireChunk;
+  while (events.size() < pieces) events.push_back(std::make_unique<Event>());
+  for (size_t k = 0; k < pieces; ++k) {
+    const size_t off = k * kWireChunk, len = std::min(kWireChunk, bytes - off);
+    GP_CALL(gp_memcpy_async(static_cast<char *>(dst) + off, static_cast<const char *>(src) + off, len, st.get()));
+    events[k]->record(st);
+  }
+}
+}  // namespace
+
+void ClientLib::send_to_server_chunked(Channel &ch, uint32_t s, const std::vector<Part> &parts,
+                                       std::vector<std::unique_ptr<Event>> &events) {
+  std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
+  GP_CHECK_MSG(!ch.server_shut[s], "send to server " << s << " after SHUTDOWN");
+  GP_CHECK_MSG(send_frame_chunked(ch.server_fd[s], parts, kWireChunk, [&](size_t k) { events[k]->sync(); }),
+               "send to server " << s << " failed");
+}
+
 void ClientLib::send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts) {
   std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
   GP_CHECK_MSG(!ch.server_shut[s], "send to server " << s << " after SHUTDOWN");
@@ -519,18 +547,16 @@ bool ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatc
   GP_CHECK_MSG(fd >= 0, "no connection to client " << client_id);
   const size_t floats = r.num_rows * ROW_DATA_SIZE;
   if (ch.reply_buf.size() < floats) ch.reply_buf.resize(floats);
-  if (floats) {
-    GP_CALL(gp_memcpy_async(ch.reply_buf.data(), r.device_rows, floats * 4, ch.svc_stream->get()));
-    ch.svc_stream->sync();
-  }
+  if (floats) copy_out_in_pieces(ch.reply_buf.data(), r.device_rows, floats * 4, *ch.svc_stream, ch.reply_events);
   sc_read_row_batch_msg_t h{};
   h.cmd = READ_ROW_BATCH;
   h.server_id = r.server_id;
   h.data_age = r.data_age;
   h.self_clock = r.self_clock;
   h.table_id = r.table_id;
-  GP_CHECK_MSG(send_frame(fd, {Part{&h, sizeof h}, Part{r.keys, r.num_rows * sizeof(RowKey)},
-                               Part{ch.reply_buf.data(), floats * 4}}),
+  GP_CHECK_MSG(send_frame_chunked(fd, {Part{&h, sizeof h}, Part{r.keys, r.num_rows * sizeof(RowKey)},
+                                       Part{ch.reply_buf.data(), floats * 4}},
+                                  kWireChunk, [&](size_t k) { ch.reply_events[k]->sync(); }),
                "send to client " << client_id << " failed");
   return false;
 }
@@ -1229,18 +1255,17 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
     } else {
       const size_t floats = n * ROW_DATA_SIZE;
       if (ch.send_buf.size() < floats) ch.send_buf.resize(floats);
-      if (floats) {
-        GP_CALL(gp_memcpy_async(ch.send_buf.data(), oplog->data() + a * ROW_DATA_SIZE, floats * 4,
-                                ch.stream->get()));
-        ch.stream->sync();
-      }
+      if (floats)
+        copy_out_in_pieces(ch.send_buf.data(), oplog->data() + a * ROW_DATA_SIZE, floats * 4, *ch.stream,
+                           ch.send_events);
       cs_clock_with_updates_batch_msg_t h{};
       h.cmd = CLOCK_WITH_UPDATES_BATCH;
       h.client_id = process_id_;
       h.clock = clock;
       h.table_id = table_id;
-      send_to_server(ch, s, {Part{&h, sizeof h}, Part{keys->data() + a, n * sizeof(RowKey)},
-                             Part{ch.send_buf.data(), floats * 4}});
+      send_to_server_chunked(ch, s, {Part{&h, sizeof h}, Part{keys->data() + a, n * sizeof(RowKey)},
+                                     Part{ch.send_buf.data(), floats * 4}},
+                             ch.send_events);
       remote_bytes += floats * 4;
     }
   }

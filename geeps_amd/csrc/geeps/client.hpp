@@ -190,6 +190,9 @@ struct Channel {
   std::vector<char> server_shut;
   std::vector<std::thread> client_readers;
   PinnedArray<float> send_buf;
+  // one event per kWireChunk piece of send_buf / reply_buf's device-to-host
+  // copy (send_frame_chunked sends each piece as it lands)
+  std::vector<std::unique_ptr<Event>> send_events, reply_events;
   // server side: one socket per remote client
   int listen_fd = -1;
   std::vector<int> client_fd;
@@ -274,6 +277,9 @@ class ClientLib {
   }
   bool ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &r, bool *held);
   void send_to_server(Channel &ch, uint32_t s, const std::vector<Part> &parts);
+  // send_to_server with the last part sent in pieces as `events` say they landed
+  void send_to_server_chunked(Channel &ch, uint32_t s, const std::vector<Part> &parts,
+                              std::vector<std::unique_ptr<Event>> &events);
   void ack_to_server(Channel &ch, uint32_t s, const RefreshAckMsg &a);
   // the reader of server s's frames has handled its SHUTDOWN (kCmdReaderDone)
   void reader_done_to_server(Channel &ch, uint32_t s);

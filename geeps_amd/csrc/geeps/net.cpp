@@ -258,6 +258,27 @@ bool send_frame(int fd, const std::vector<Part> &parts) {
   return writev_all(fd, iov, n);
 }
 
+bool send_frame_chunked(int fd, const std::vector<Part> &parts, size_t chunk,
+                        const std::function<void(size_t)> &ready) {
+  if (parts.empty() || parts.size() > kMaxParts || chunk == 0) return false;
+  uint8_t heads[kMaxParts][9];
+  iovec iov[2 * kMaxParts];
+  int n = 0;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const bool last = i + 1 == parts.size();
+    iov[n++] = {heads[i], frame_header(heads[i], last ? 0 : kFlagMore, parts[i].size)};
+    if (!last && parts[i].size) iov[n++] = {const_cast<void *>(parts[i].data), parts[i].size};
+  }
+  if (!writev_all(fd, iov, n)) return false;  // every header, the parts before the last, its header
+  const char *data = static_cast<const char *>(parts.back().data);
+  const size_t size = parts.back().size;
+  for (size_t k = 0, off = 0; off < size; ++k, off += chunk) {
+    ready(k);
+    if (!write_all(fd, data + off, size - off < chunk ? size - off : chunk)) return false;
+  }
+  return true;
+}
+
 bool recv_frame(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<char>> &scratch,
                 void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx) {
   parts.clear();

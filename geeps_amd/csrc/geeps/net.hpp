@@ -23,6 +23,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <utility>
 #include <vector>
@@ -54,6 +55,12 @@ bool zmtp_handshake(int fd, const std::string &identity,
 
 // One multipart message (every part but the last flagged MORE).  Blocking.
 bool send_frame(int fd, const std::vector<Part> &parts);
+// The same message, its last part written in `chunk`-byte pieces, piece k
+// once `ready(k)` returns (its device-to-host copy has landed): the socket
+// carries the first pieces while later ones still come off the GPU.  The
+// bytes on the wire are send_frame's.
+bool send_frame_chunked(int fd, const std::vector<Part> &parts, size_t chunk,
+                        const std::function<void(size_t)> &ready);
 // Reads one multipart message; `alloc(i, size)` returns where part i goes
 // (nullptr = a temporary vector owned by `scratch`).  Command frames between
 // messages (PING, PONG, ...) are skipped, and a PING is not answered (the
