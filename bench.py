@@ -821,7 +821,7 @@ def pre_gpu_multi_leg(args, backend):
     return res
 
 
-def libgeeps_leg(rows, W, clocks=10, warmup=2, procs=(1, 2)):
+def libgeeps_leg(rows, W, clocks=10, warmup=5, procs=(1, 2)):
     """The drop-in path end to end: scripts/apps/geeps_clock_bench (built by
     __graft_entry__.build() against libgeeps.so and include/geeps.hpp, as an
     app links) run as P processes on this GPU, one GeePS worker + tablet server
