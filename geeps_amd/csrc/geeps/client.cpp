@@ -329,21 +329,66 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
   }
 }
 
+namespace {
+// Rows bound for a socket leave the GPU in pieces of this size, each sent as
+// soon as its copy lands (send_frame_chunked), so the D2H of a large slice
+// overlaps the send instead of preceding it.
+constexpr size_t kWireChunk = 16u << 20;
+
+// The device-to-host copy of `bytes` from `src` into pinned `dst` on `st`, an
+// event recorded after each kWireChunk piece.
+void copy_out_in_pieces(void *dst, const void *src, size_t bytes, const Stream &st,
+                        std::vector<std::unique_ptr<Event>> &events) {
+  const size_t pieces = (bytes + kWireChunk - 1) / kWireChunk;
+  while (events.size() < pieces) events.push_back(std::make_unique<Event>());
+  for (size_t k = 0; k < pieces; ++k) {
+    const size_t off = k * kWireChunk, len = std::min(kWireChunk, bytes - off);
+    GP_CALL(gp_memcpy_async(static_cast<char *>(dst) + off, static_cast<const char *>(src) + off, len, st.get()));
+    events[k]->record(st);
+  }
+}
+}  // namespace
+
 // Client side of a server connection: READ_ROW_BATCH replies
 // (ServerClientDecode::read_row_batch, client/encoder-decoder.cpp:228-251).
 void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
   GP_CALL(gp_set_device(device_));
   PinnedArray<float> buf;
-  auto alloc = [](void *c, size_t i, size_t size) -> void * {
-    auto *b = static_cast<PinnedArray<float> *>(c);
+  std::vector<RecvPart> parts;
+  std::vector<std::vector<char>> scratch;
+  // A socket refresh's rows go on to HBM piece by piece as they come off the
+  // socket (into `landing`, this reader's own buffer: one refresh at a time),
+  // so the host-to-device copy overlaps the receive; recv_row_batch then
+  // copies device to device under the channel lock.
+  DeviceArray<float> landing;
+  Stream h2d;
+  auto landed = [&](size_t i, size_t off, size_t len) {
+    if (i != 2) return;
+    GP_CALL(gp_memcpy_async(reinterpret_cast<char *>(landing.data()) + off,
+                            reinterpret_cast<const char *>(buf.data()) + off, len, h2d.get()));
+  };
+  auto alloc_landing = [](void *c, size_t i, size_t size) -> void * {
+    auto *ctx = static_cast<std::pair<PinnedArray<float> *, DeviceArray<float> *> *>(c);
+    if (i != 2) return nullptr;
+    if (ctx->first->size() * 4 < size) ctx->first->resize((size + 3) / 4);
+    if (ctx->second->size() * 4 < size) ctx->second->resize((size + 3) / 4);
+    return ctx->first->data();
+  };
+  std::pair<PinnedArray<float> *, DeviceArray<float> *> ctx{&buf, &landing};
+  static const bool stream_recv = [] {
+    const char *e = std::getenv("GEEPS_STREAM_RECV");
+    return !e || std::atoi(e) != 0;
+  }();
+  auto alloc_pinned = [](void *c, size_t i, size_t size) -> void * {
+    auto *b = static_cast<std::pair<PinnedArray<float> *, DeviceArray<float> *> *>(c)->first;
     if (i != 2) return nullptr;
     if (b->size() * 4 < size) b->resize((size + 3) / 4);
     return b->data();
   };
-  std::vector<RecvPart> parts;
-  std::vector<std::vector<char>> scratch;
   for (;;) {
-    if (!recv_frame(fd, parts, scratch, alloc, &buf)) break;
+    if (stream_recv ? !recv_frame_chunked(fd, parts, scratch, alloc_landing, &ctx, kWireChunk, landed)
+                    : !recv_frame(fd, parts, scratch, alloc_pinned, &ctx))
+      break;
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == SHUTDOWN) {
@@ -402,9 +447,10 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
     }
     const size_t n = parts[1].size / sizeof(RowKey);
     GP_CHECK_EQ(parts[2].size, n * kRowBytes);
+    h2d.sync();  // every piece's copy into `landing` has landed
     const std::vector<int> released =
         recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
-                       static_cast<const float *>(parts[2].data), n, -1);
+                       n && stream_recv ? landing.data() : static_cast<const float *>(parts[2].data), n, -1);
     GP_CHECK_MSG(released.empty(), "socket refresh replaced an in-place shard of server " << server_id);
   }
 }
@@ -449,25 +495,6 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
   return true;
 }
 
-namespace {
-// Rows bound for a socket leave the GPU in pieces of this size, each sent as
-// soon as its copy lands (send_frame_chunked), so the D2H of a large slice
-// overlaps the send instead of preceding it.
-constexpr size_t kWireChunk = 16u << 20;
-
-// The device-to-host copy of `bytes` from `src` into pinned `dst` on `st`, an
-// event recorded after each kWireChunk piece.
-void copy_out_in_pieces(void *dst, const void *src, size_t bytes, const Stream &st,
-                        std::vector<std::unique_ptr<Event>> &events) {
-  const size_t pieces = (bytes + kWireChunk - 1) / kWireChunk;
-  while (events.size() < pieces) events.push_back(std::make_unique<Event>());
-  for (size_t k = 0; k < pieces; ++k) {
-    const size_t off = k * kWireChunk, len = std::min(kWireChunk, bytes - off);
-    GP_CALL(gp_memcpy_async(static_cast<char *>(dst) + off, static_cast<const char *>(src) + off, len, st.get()));
-    events[k]->record(st);
-  }
-}
-}  // namespace
 
 void ClientLib::send_to_server_chunked(Channel &ch, uint32_t s, const std::vector<Part> &parts,
                                        std::vector<std::unique_ptr<Event>> &events) {
@@ -681,6 +708,10 @@ void ClientLib::finish_virtual_iteration() {
       // place); a lagging reader can make it up to clients + 2 (server.hpp)
       planned += pc.server_num_rows[process_id_] * kRowBytes *
                  (std::min<size_t>(staged_peers, TabletServer::kMaxPendingBuckets) + 2);
+      // + a landing buffer per socket server (its reader streams a refresh's
+      // rows into HBM as they arrive, client_reader): that server's shard
+      for (uint32_t s = 0; s < num_processes_; ++s)
+        if (s != process_id_ && !ipc_to(s)) planned += pc.server_num_rows[s] * kRowBytes;
       pc.per_server_data_age.assign(num_processes_, INITIAL_DATA_AGE);
       pc.live_ver.assign(num_processes_, -1);
       pc.live_ptr.assign(num_processes_, nullptr);

@@ -279,8 +279,10 @@ bool send_frame_chunked(int fd, const std::vector<Part> &parts, size_t chunk,
   return true;
 }
 
-bool recv_frame(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<char>> &scratch,
-                void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx) {
+namespace {
+bool recv_frame_impl(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<char>> &scratch,
+                     void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx, size_t chunk,
+                     const std::function<void(size_t, size_t, size_t)> *landed) {
   parts.clear();
   scratch.resize(kMaxParts);
   for (;;) {
@@ -306,10 +308,31 @@ bool recv_frame(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<ch
       scratch[i].resize(size);
       dst = scratch[i].data();
     }
-    if (size && !read_all(fd, dst, size)) return false;
+    if (landed) {
+      for (size_t off = 0; off < size; off += chunk) {
+        const size_t len = size - off < chunk ? size - off : chunk;
+        if (!read_all(fd, static_cast<char *>(dst) + off, len)) return false;
+        (*landed)(i, off, len);
+      }
+    } else if (size && !read_all(fd, dst, size)) {
+      return false;
+    }
     parts.push_back(RecvPart{dst, size});
     if (!(flags & kFlagMore)) return true;
   }
+}
+}  // namespace
+
+bool recv_frame(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<char>> &scratch,
+                void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx) {
+  return recv_frame_impl(fd, parts, scratch, alloc, ctx, 0, nullptr);
+}
+
+bool recv_frame_chunked(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<char>> &scratch,
+                        void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx, size_t chunk,
+                        const std::function<void(size_t, size_t, size_t)> &landed) {
+  if (chunk == 0) return false;
+  return recv_frame_impl(fd, parts, scratch, alloc, ctx, chunk, &landed);
 }
 
 int listen_tcp(uint16_t port, std::string *err) {

@@ -74,6 +74,12 @@ constexpr size_t kMaxParts = 64;
 bool recv_frame(int fd, std::vector<RecvPart> &parts,
                 std::vector<std::vector<char>> &scratch,
                 void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx);
+// The same, reading each part in `chunk`-byte pieces and calling
+// `landed(index, offset, length)` as each piece is in place (the refresh's
+// host-to-device copy follows the socket piece by piece).
+bool recv_frame_chunked(int fd, std::vector<RecvPart> &parts, std::vector<std::vector<char>> &scratch,
+                        void *(*alloc)(void *ctx, size_t index, size_t size), void *ctx, size_t chunk,
+                        const std::function<void(size_t, size_t, size_t)> &landed);
 
 int listen_tcp(uint16_t port, std::string *err);
 int accept_tcp(int listen_fd);
