@@ -1765,8 +1765,9 @@ __global__ __launch_bounds__(kBlock) void index_verify_kernel(const gp_double_in
     index_verify<false>(idx, full, n, base0_word, gate_word, host_word, gen);
 }
 
-// The compact copy of an index (built with its sorted residual, on the second
-// call): id1 as 4 B per entry and base0 = id0 of entry 0; `host_broken` and
+// The compact copy of an index (built with the plan: on the first call for an
+// inverse or ranges plan, on the second with a sorted residual): id1 as 4 B
+// per entry and base0 = id0 of entry 0; `host_broken` and
 // `dev_broken` (a device word the next kernels read) set
 // when the index is not of that shape (then the full copy stays in use).
 __global__ __launch_bounds__(kBlock) void compact_copy_kernel(const gp_double_index *__restrict__ idx, size_t n,
@@ -2037,9 +2038,11 @@ struct PinnedWord {
 };
 
 // An entry is immutable once in the cache.  The first call with an index
-// leaves a copy-only entry (`sorted` null); the next call with the same
-// content builds the destination-sorted residual into a new entry that
-// shares the copy.
+// leaves a steady-state entry (an inverse map or a ranges plan, with the
+// index's compact copy) or, for a scatter of rows over 128 floats, a
+// copy-only entry (`sorted` null); the next call with the same content then
+// builds the destination-sorted residual into a new entry that shares the
+// copy.
 struct CachedPlan {
   PlanKey key{};
   std::shared_ptr<DevBuf> copy;    // the index as first seen
