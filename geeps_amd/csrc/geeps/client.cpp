@@ -432,9 +432,21 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
           ptr = it->second;
         }
       }
+      const float *src = static_cast<const float *>(ptr);
+      if (ch.stage_refresh_from[server_id] && rv.num_rows) {
+        // A staged refresh (a server on another GPU): the peer copy over xGMI
+        // goes to this reader's landing buffer first, on its own stream and
+        // outside the channel lock, so the refreshes of several peers come
+        // over their links at once; recv_row_batch's copy into the cache under
+        // the lock is then local HBM.  (The version stays held until then.)
+        const size_t bytes = rv.num_rows * kRowBytes;
+        if (landing.size() * sizeof(float) < bytes) landing.resize(bytes / sizeof(float));
+        GP_CALL(gp_memcpy_async(landing.data(), src, bytes, h2d.get()));
+        h2d.sync();
+        src = landing.data();
+      }
       const std::vector<int> released =
-          recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
-                         static_cast<const float *>(ptr), rv.num_rows, rv.version);
+          recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock, src, rv.num_rows, rv.version);
       for (int v : released) {
         RefreshAckMsg a{};
         a.cmd = kCmdRefreshAck;
@@ -709,9 +721,11 @@ void ClientLib::finish_virtual_iteration() {
       planned += pc.server_num_rows[process_id_] * kRowBytes *
                  (std::min<size_t>(staged_peers, TabletServer::kMaxPendingBuckets) + 2);
       // + a landing buffer per socket server (its reader streams a refresh's
-      // rows into HBM as they arrive, client_reader): that server's shard
+      // rows into HBM as they arrive) and per staged same-node server (its
+      // reader peer-copies a refresh there outside the channel lock,
+      // client_reader): that server's shard
       for (uint32_t s = 0; s < num_processes_; ++s)
-        if (s != process_id_ && !ipc_to(s)) planned += pc.server_num_rows[s] * kRowBytes;
+        if (s != process_id_ && (!ipc_to(s) || ch.stage_refresh_from[s])) planned += pc.server_num_rows[s] * kRowBytes;
       pc.per_server_data_age.assign(num_processes_, INITIAL_DATA_AGE);
       pc.live_ver.assign(num_processes_, -1);
       pc.live_ptr.assign(num_processes_, nullptr);

@@ -62,7 +62,7 @@ TabletServer::TabletServer(uint32_t server_id, uint32_t channel_id, uint32_t num
   GP_CHECK(num_clients_ > 0);
   tables_.resize(num_tables);
   for (auto &t : tables_) t.vec_clock.assign(num_clients_, INITIAL_DATA_AGE);
-  if (num_clients_ > 1) copy_stream_ = std::make_unique<Stream>();
+  copy_streams_.resize(num_clients_);
   thread_ = std::thread([this] { run(); });
 }
 
@@ -251,10 +251,12 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
     // peer copy over xGMI on the copy stream, overlapped with whatever else
     // arrives), so the sum streams local HBM only.  apply_pending waits for it.
     auto stage = stage_buffer(t);
-    GP_CALL(gp_memcpy_async(stage->data(), b.device_rows, batch_size * ROW_DATA_SIZE * sizeof(float),
-                            copy_stream_->get()));
+    GP_CHECK_LT(b.client_id, num_clients_);
+    auto &cs = copy_streams_[b.client_id];
+    if (!cs) cs = std::make_unique<Stream>();
+    GP_CALL(gp_memcpy_async(stage->data(), b.device_rows, batch_size * ROW_DATA_SIZE * sizeof(float), cs->get()));
     p.staged = std::make_shared<Event>();
-    p.staged->record(*copy_stream_);
+    p.staged->record(*cs);
     p.rows = stage->data();
     p.keepalive = stage;
     stats_.nr_peer_staged++;

@@ -169,7 +169,7 @@ class TabletServer {
   struct Pending {
     const float *rows;
     std::shared_ptr<void> keepalive;
-    std::shared_ptr<Event> staged;  // a peer copy into `rows` on copy_stream_
+    std::shared_ptr<Event> staged;  // a peer copy into `rows` on copy_streams_[client]
   };
   struct DataTable {
     std::vector<iter_t> vec_clock;
@@ -216,7 +216,10 @@ class TabletServer {
   std::mutex hold_mu_;  // DataTable::holders (and the versions vector's size)
   std::condition_variable release_cv_;  // a hold ended (release / release_all)
   uint64_t releases_ = 0;               // holds ended so far (hold_mu_): reader progress
-  std::unique_ptr<Stream> copy_stream_;  // peer copies of other GPUs' buckets
+  // peer copies of other GPUs' buckets: one stream per client (made on first
+  // use, server thread only), so slices from different peers come over their
+  // own xGMI links at once instead of one after another on a single stream
+  std::vector<std::unique_ptr<Stream>> copy_streams_;
   uint32_t shutdown_count_ = 0;  // server thread only
   bool shutdown_done_ = false;    // guarded by mu_
   std::condition_variable shutdown_cv_;
