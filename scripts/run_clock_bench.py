@@ -125,6 +125,7 @@ def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900, extra_en
            "read_bad": sum(r.get("read_bad", 0) for r in results)}
     out["read_ok"] = out["read_bad"] == 0 and out["read_checked"] > 0
     st = [r["stats"] for r in results if "stats" in r]
+    out["stats"] = st  # each process's libgeeps counters and timers (GetStats)
     if st:
         out["nr_peer_staged"] = sum(srv["nr_peer_staged"] for s in st for srv in s["servers"])
         out["nr_refresh_staged"] = sum(s["client"]["nr_refresh_staged"] for s in st)
