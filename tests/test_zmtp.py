@@ -354,3 +354,14 @@ def test_incompatible_socket_type_is_refused():
         if p.poll() is None:
             p.kill()
             p.wait()
+
+
+def test_chunked_send_and_receive_match_the_plain_forms():
+    """send_frame_chunked / recv_frame_chunked (libgeeps' socket pushes and
+    refreshes, sent and landed piece by piece) against send_frame /
+    recv_frame over a socketpair: the same bytes on the wire, one ready() per
+    piece in order, landed() pieces tiling every part (tests/apps/wire_chunks.cpp)."""
+    exe = os.path.join(REPO, "build", "tests", "wire_chunks")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "wire_chunks ok" in r.stdout, r.stdout + r.stderr
