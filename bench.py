@@ -273,6 +273,75 @@ def model_ms(read_bytes, write_bytes, probe):
     return read_bytes / (probe["read_GBps"] * 1e9) * 1e3 + write_bytes / (probe["write_GBps"] * 1e9) * 1e3
 
 
+def regen_delta(c, n, dev):
+    """Client c's delta buffer regenerated: the same values make_deltas wrote."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + c)
+    d = torch.rand(n, generator=g, device=dev)
+    d.sub_(0.5)
+    return d
+
+
+# Per element of a reduce-scatter exchange's refreshed table against the
+# client-order sum: |err| <= clients ulps of the largest partial sum
+# (tests/test_shard_gloo.py writes the same bound, steps = 1 here).
+def rs_tolerance(clients):
+    import numpy as np
+    return clients * float(np.finfo(np.float32).eps) * (0.5 * clients + 1)
+
+
+def exchange_check(red, deltas, R, W, C, dev, world, kind):
+    """configs[2]'s parity check on the ranks themselves: one
+    clean clock -- push (the RCCL exchange) -> apply (the HIP N-way sum) ->
+    refresh (all-gather) -- on a zeroed master, then on EVERY rank the
+    refreshed full table against
+      * the client-order sum ((0 + d0) + d1) + ... + d{C-1} of all C seeded
+        deltas regenerated on this rank's device, every element (the reference
+        server applies the clients' messages in arrival order,
+        tablet-server.cpp:119-134; a2a: bit-exact, rs: rs_tolerance);
+      * a numpy restatement of that sum on sampled rows: row 0, the last row,
+        the first and last row of every shard (the a2a split offsets and the
+        all-gather's padded-shard unpacking of an uneven partition) and 8
+        seeded random rows.
+    Returns {"ok", "max_abs_err", "rows_sampled", ...}, reduced over ranks
+    (ok: all ranks; max_abs_err: the largest)."""
+    import numpy as np
+    L = red.layout
+    red.master.zero_()
+    table = red.step(deltas)[:R * W]
+    _sync(dev)
+    rows = {0, R - 1}
+    for s, c in zip(L.starts, L.counts):
+        if c:
+            rows.update((s, s + c - 1))
+    rows.update(int(r) for r in np.random.default_rng(7).integers(0, R, 8))
+    rows = sorted(rows)
+    idx = torch.tensor(rows, dtype=torch.long, device=dev)
+    exp = torch.zeros(R * W, dtype=torch.float32, device=dev)
+    sampled = np.zeros((C, len(rows), W), np.float32)
+    for c in range(C):
+        d = regen_delta(c, R * W, dev)
+        exp.add_(d)
+        sampled[c] = d.view(R, W).index_select(0, idx).cpu().numpy()
+        del d
+    m = np.zeros((len(rows), W), np.float32)
+    for c in range(C):  # fp32 adds in client order
+        m = m + sampled[c]
+    got = table.view(R, W).index_select(0, idx).cpu().numpy()
+    err = float((table - exp).abs().max().item()) if R * W else 0.0
+    err_rows = float(np.abs(got - m).max()) if m.size else 0.0
+    if kind == "a2a":
+        ok = (torch.equal(table.view(torch.int32), exp.view(torch.int32)) and
+              np.array_equal(got.view(np.uint32), m.view(np.uint32)))
+    else:
+        ok = err <= rs_tolerance(C) and err_rows <= rs_tolerance(C)
+    del exp
+    flag = -max_over_ranks(-(1.0 if ok else 0.0), world, dev)  # min over ranks
+    return {"ok": flag == 1.0, "max_abs_err": max_over_ranks(max(err, err_rows), world, dev),
+            "bar": "bit-exact vs client order" if kind == "a2a" else f"|err| <= {rs_tolerance(C):.3g}",
+            "rows_sampled": len(rows), "elements_checked": R * W, "ranks": world}
+
+
 def timed_exchange(red, deltas, steps, warmup, world, dev):
     for _ in range(warmup):
         red.step(deltas)
@@ -1049,11 +1118,13 @@ def main(argv=None, backend="nccl", apply_fn=None):
             r = red if kind == args.exchange else ShardedReducer(R, W, C, dev, exchange=kind,
                                                                  apply_fn=apply_fn,
                                                                  layout=args.layout)
+            log(f"[rank {rank}] {kind} exchange: parity check, then {args.exchange_steps} timed steps")
+            chk = exchange_check(r, deltas, R, W, C, dev, world, kind)
             ex = timed_exchange(r, deltas, args.exchange_steps, 1, world, dev)
             ex = max_over_ranks(ex, world, dev) / args.exchange_steps
             result_exchange.append({"ms_per_step": round(ex * 1e3, 3),
                                     "value": round(delta_bytes / ex / 1e9, 2), "unit": "GB/s",
-                                    "exchange": kind,
+                                    "exchange": kind, "check": chk,
                                     "note": "RCCL bucket exchange + N-way sum + all-gather refresh"})
             if r is not red:
                 del r
@@ -1167,6 +1238,10 @@ def main(argv=None, backend="nccl", apply_fn=None):
         if result_exchange:
             line["exchange_inclusive"] = result_exchange[0]
             line["exchange_inclusive_alt"] = result_exchange[1]
+            # configs[2]'s parity on the real ranks, as top-level scalars
+            for ex in result_exchange:
+                line[f"exchange_ok_{ex['exchange']}"] = ex["check"]["ok"]
+                line[f"exchange_max_abs_err_{ex['exchange']}"] = ex["check"]["max_abs_err"]
         if probe:
             line["roofline"]["same_box_copy_GBps"] = probe["copy_GBps"]
             mm = model_ms((C + 1) * shard_bytes, shard_bytes, probe)

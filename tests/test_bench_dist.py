@@ -17,9 +17,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,exchange", [(2, "a2a"), (4, "a2a"), (2, "rs"), (8, "a2a")])
-def test_bench_multirank_flow(tmp_path, world, exchange):
-    argv = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--rows", "1000", "--width", "64",
+@pytest.mark.parametrize("world,exchange,rows", [(2, "a2a", 1000), (4, "a2a", 1000), (2, "rs", 1000),
+                                                (8, "a2a", 1000), (8, "rs", 1003), (4, "a2a", 1001)])
+def test_bench_multirank_flow(tmp_path, world, exchange, rows):
+    argv = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--rows", str(rows), "--width", "64",
             "--clients", "8", "--exchange", exchange, "--exchange-steps", "2"]
     mp.spawn(_dist_worker.run_bench, args=(world, _free_port(), argv, str(tmp_path)), nprocs=world,
              join=True)
@@ -34,3 +35,21 @@ def test_bench_multirank_flow(tmp_path, world, exchange):
     assert line["exchange_inclusive"]["exchange"] == exchange
     assert line["exchange_inclusive_alt"]["exchange"] != exchange
     assert line["cpu_baseline"] is None  # rank-0 CPU baseline runs only at N = 1
+    # configs[2]'s parity check ran on every rank for both exchanges
+    # (uneven partitions: 1003 rows over 8, 1001 over 4)
+    for kind in ("a2a", "rs"):
+        assert line[f"exchange_ok_{kind}"] is True, line
+        chk = line["exchange_inclusive" if kind == exchange else "exchange_inclusive_alt"]["check"]
+        assert chk["ok"] and chk["elements_checked"] == rows * 64 and chk["ranks"] == world
+        assert chk["rows_sampled"] >= 2 * world
+    assert line["exchange_max_abs_err_a2a"] == 0.0
+    assert 0.0 <= line["exchange_max_abs_err_rs"] <= 8 * 1.2e-7 * 5
+
+
+def test_exchange_check_catches_a_wrong_split(tmp_path):
+    """The check is not vacuous: a reducer whose all-to-all split is off by one
+    row (a wrong shard offset on the real ranks) fails it on gloo."""
+    mp.spawn(_dist_worker.run_bad_split_check, args=(2, _free_port(), str(tmp_path)), nprocs=2,
+             join=True)
+    res = json.load(open(tmp_path / "check.json"))
+    assert res["ok"] is False and res["max_abs_err"] > 0

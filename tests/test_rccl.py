@@ -1,0 +1,92 @@
+"""configs[2] on real ranks: 8 server shards, RCCL reduce-scatter / all-to-all
++ the HIP N-way sum + all-gather, one process per GPU (BASELINE.json configs[2];
+the reference's exchange: every client sends each server its slice,
+src/client/clientlib-data.cpp:487-509, each server replies its shard to every
+client, src/server/tablet-server.cpp:136-163).
+
+* test_rccl_sharded_reduction: with >= 2 GPUs, torch.distributed.run starts
+  min(GPUs, 8) (a power of two) nccl ranks as a fresh child process; each runs
+  geeps_amd.shard.ShardedReducer with both exchanges on a reduced uneven table
+  (4099 x 1024, every element against the oracle on rank 0) and at full size
+  (1M x 1024, every element against the client-order sum on every rank), via
+  bench.exchange_check -- the same check bench.py --gpus N runs.  Skips on a
+  one-GPU box.
+* test_gloo_exchange_hip_sum_one_gpu: the same flow with the exchange on
+  gloo CPU ranks and the apply on the GPU's HIP kernel (2 ranks sharing cuda:0),
+  so the multi-rank partition / order / refresh logic runs around the real
+  kernel on a one-GPU box; bit-exact against the oracle (a2a; rs at 2 ranks is a
+  two-term sum per shard, pinned against its own association).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gpu_count():
+    import torch
+    return torch.cuda.device_count()  # does not initialise the GPU in this process
+
+
+@pytest.mark.gpu
+def test_rccl_sharded_reduction(tmp_path):
+    n = _gpu_count()
+    if n < 2:
+        pytest.skip(f"needs >= 2 GPUs for nccl ranks (this box has {n})")
+    ranks = 8 if n >= 8 else 4 if n >= 4 else 2
+    out = tmp_path / "rccl.json"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "tests", "_rccl_worker.py"), str(out), "4099x1024,1048576x1024"]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert len(res) == 4
+    for r in res:
+        assert r["world"] == ranks
+        assert r["check"]["ok"], r
+        assert r["check"]["elements_checked"] == r["rows"] * r["width"]
+        if r["exchange"] == "a2a":
+            assert r["check"]["max_abs_err"] == 0.0, r
+        if r["rows"] == 4099:
+            assert r["oracle_ok"] is True, r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("num_rows,W,clients,exchange,steps", [
+    (4099, 128, 4, "a2a", 2),   # uneven: 2050 + 2049 rows
+    (4099, 128, 4, "rs", 1),
+    (1000, 1024, 2, "a2a", 3),
+])
+def test_gloo_exchange_hip_sum_one_gpu(dev, tmp_path, num_rows, W, clients, exchange, steps):
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _dist_worker
+    from oracle import oracle
+    world = 2
+    mp.spawn(_dist_worker.run_shard,
+             args=(world, _free_port(), num_rows, W, clients, exchange, steps, str(tmp_path), "hip"),
+             nprocs=world, join=True)
+    tables = [np.load(tmp_path / f"table_{r}.npy") for r in range(world)]
+    assert np.array_equal(tables[0].view(np.uint32), tables[1].view(np.uint32))
+    m = np.zeros(num_rows * W, np.float32)
+    for step in range(steps):
+        d = [oracle.synthetic_delta(c + 100 * step, num_rows * W) for c in range(clients)]
+        if exchange == "a2a":
+            oracle.apply_updates(m, d)
+        else:  # each shard's reduce-scatter adds the two ranks' slot-j deltas first
+            oracle.apply_updates(m, [d[2 * j] + d[2 * j + 1] for j in range(clients // 2)])
+    assert np.array_equal(tables[0].view(np.uint32), m.view(np.uint32))
