@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <iostream>
 #include <set>
@@ -62,6 +63,8 @@ std::string ClientStats::to_json() const {
     << ", \"nr_refresh_staged\": " << nr_refresh_staged << ", \"nr_update_direct\": " << nr_update_direct
     << ", \"nr_read_direct\": " << nr_read_direct << ", \"nr_read_pin_deferred\": " << nr_read_pin_deferred
     << ", \"nr_read_direct_capped\": " << nr_read_direct_capped
+    << ", \"nr_ipc_export_refused\": " << nr_ipc_export_refused << ", \"nr_ipc_nack_sent\": " << nr_ipc_nack_sent
+    << ", \"nr_ipc_resent\": " << nr_ipc_resent
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -110,6 +113,8 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
   direct_read_ = direct_read && std::string(direct_read) == "1";
   const char *delay = std::getenv("GEEPS_TEST_READER_DELAY_US");
   reader_delay_us_ = delay ? std::atoi(delay) : 0;
+  if (const char *f = std::getenv("GEEPS_TEST_IPC_FAULT"))
+    ipc_fault_ = std::string(f) == "tag" ? 1 : std::string(f) == "refuse" ? 2 : 0;
   // Same-node peers exchange rows device to device through IPC-mapped HBM
   // (xGMI between GPUs); GEEPS_TRANSPORT=tcp forces the socket data path.
   const char *transport = std::getenv("GEEPS_TRANSPORT");
@@ -137,6 +142,8 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
       ch->server_send_mu.push_back(std::make_unique<std::mutex>());
     ch->server_shut.assign(num_processes_, 0);
     ch->client_fd.assign(num_processes_, -1);
+    for (uint32_t s = 0; s < num_processes_; ++s)
+      ch->client_send_mu.push_back(std::make_unique<std::mutex>());
     ch->ipc_oplogs.resize(num_processes_);
     ch->ipc_client.assign(num_processes_, 0);
     ch->other_gpu.assign(num_processes_, 0);
@@ -229,6 +236,42 @@ void ClientLib::server_accept_loop(Channel &ch, int expected) {
   }
 }
 
+namespace {
+// A frame a reader holds back while it awaits a resend (IPC recovery,
+// wire.hpp): its parts copied, part 2's rows in a pinned buffer of its own.
+struct HeldFrame {
+  std::vector<std::vector<char>> parts;
+  std::shared_ptr<PinnedArray<float>> rows;  // part 2, when it had bytes
+  size_t rows_bytes = 0;
+  std::vector<RecvPart> view() {
+    std::vector<RecvPart> v;
+    for (size_t i = 0; i < parts.size(); ++i)
+      v.push_back(i == 2 && rows ? RecvPart{rows->data(), rows_bytes} : RecvPart{parts[i].data(), parts[i].size()});
+    return v;
+  }
+};
+
+// Receives one whole frame into a HeldFrame of its own (part 2 into fresh
+// pinned memory).  False at EOF.
+bool recv_held(int fd, HeldFrame *f) {
+  std::vector<RecvPart> parts;
+  std::vector<std::vector<char>> scratch;
+  auto alloc = [](void *c, size_t i, size_t size) -> void * {
+    auto *h = static_cast<HeldFrame *>(c);
+    if (i != 2 || size == 0) return nullptr;
+    h->rows = std::make_shared<PinnedArray<float>>((size + 3) / 4);
+    h->rows_bytes = size;
+    return h->rows->data();
+  };
+  if (!recv_frame(fd, parts, scratch, alloc, f)) return false;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const char *d = static_cast<const char *>(parts[i].data);
+    f->parts.emplace_back(i == 2 && f->rows ? std::vector<char>() : std::vector<char>(d, d + parts[i].size));
+  }
+  return true;
+}
+}  // namespace
+
 // Server side of a client connection: CLOCK_WITH_UPDATES_BATCH / CLOCK frames
 // (ClientServerDecode::decode_msg, server-encoder-decoder.cpp:153-183).
 void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
@@ -246,9 +289,11 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
   };
   std::vector<RecvPart> parts;
   std::vector<std::vector<char>> scratch;
-  for (;;) {
-    ctx.rows.reset();
-    if (!recv_frame(fd, parts, scratch, alloc, &ctx)) break;
+  std::deque<HeldFrame> held;  // frames after a NACKed one, until its resend
+  PinnedArray<float> resend_buf;
+  std::unique_ptr<Stream> resend_stream;
+  // false: the connection's last frame
+  auto handle = [&](const std::vector<RecvPart> &parts, const std::shared_ptr<PinnedArray<float>> &host_rows) {
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == CLOCK_WITH_UPDATES_BATCH) {
@@ -262,12 +307,14 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       b.client_id = h.client_id;
       b.clock = h.clock;
       b.table_id = h.table_id;
-      if (n) {
-        auto keys = std::make_shared<std::vector<RowKey>>(n);
-        std::memcpy(keys->data(), parts[1].data, parts[1].size);
+      auto take_keys = [&](const RecvPart &k) {
+        auto keys = std::make_shared<std::vector<RowKey>>(k.size / sizeof(RowKey));
+        std::memcpy(keys->data(), k.data, k.size);
         b.keys = keys->data();
         b.keys_owner = keys;
-      }
+      };
+      if (n) take_keys(parts[1]);
+      std::shared_ptr<PinnedArray<float>> rows = host_rows;
       if (parts.size() == 4) {
         // Same-node client: the rows stay in its oplog, mapped here over IPC.
         GP_CHECK(parts[2].size == 0 && parts[3].size == sizeof(IpcRowsRef));
@@ -277,25 +324,69 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
         if (n) GP_CHECK_EQ(ref.bytes, n * kRowBytes);
         n = ref.bytes / kRowBytes;  // key part omitted after the first message
         auto &mapped = ch.ipc_oplogs[client_id];
+        bool ok = true;
         if (ref.has_handle) {
           auto old = mapped.find(ref.buffer_id);
-          if (old != mapped.end()) GP_CALL(gp_ipc_close_handle(old->second));
+          if (old != mapped.end()) {
+            GP_CALL(gp_ipc_close_handle(old->second));
+            mapped.erase(old);
+          }
           void *p = nullptr;
-          GP_CALL(gp_ipc_open_handle(&p, ref.handle));
-          mapped[ref.buffer_id] = p;
-          if (ipc_log())
-            std::cerr << "libgeeps ipc map oplog: server " << process_id_ << " ch " << ch.id << " client "
-                      << client_id << " buffer " << ref.buffer_id << " -> " << p << "\n";
+          ok = gp_ipc_open_handle(&p, ref.handle) == GP_OK;
+          if (ok) {
+            mapped[ref.buffer_id] = p;
+            if (ipc_log())
+              std::cerr << "libgeeps ipc map oplog: server " << process_id_ << " ch " << ch.id << " client "
+                        << client_id << " buffer " << ref.buffer_id << " -> " << p << "\n";
+          } else {
+            std::cerr << "libgeeps: server " << process_id_ << " ch " << ch.id << " could not map oplog buffer "
+                      << ref.buffer_id << " of client " << client_id << " (" << gp_last_error()
+                      << "); asking for the rows by socket\n";
+          }
         }
-        auto it = mapped.find(ref.buffer_id);
-        GP_CHECK_MSG(it != mapped.end(), "unmapped oplog buffer " << ref.buffer_id);
-        b.device_rows = reinterpret_cast<const float *>(static_cast<const char *>(it->second) +
-                                                        ref.offset);
-        b.stage = ch.stage_from[client_id];
+        if (ok) {
+          auto it = mapped.find(ref.buffer_id);
+          GP_CHECK_MSG(it != mapped.end(), "unmapped oplog buffer " << ref.buffer_id);
+          b.device_rows = reinterpret_cast<const float *>(static_cast<const char *>(it->second) + ref.offset);
+          b.stage = ch.stage_from[client_id];
+        } else {
+          // NACK, then hold the client's later frames back until the slice
+          // comes again as a socket frame (the client sends it as soon as its
+          // reader sees the NACK)
+          OplogNackMsg m{};
+          m.cmd = kCmdOplogNack;
+          m.server_id = process_id_;
+          m.table_id = h.table_id;
+          m.clock = h.clock;
+          m.buffer_id = ref.buffer_id;
+          GP_CHECK_MSG(send_to_client(ch, client_id, {Part{&m, sizeof m}}),
+                       "oplog NACK to client " << client_id << " failed");
+          {
+            std::lock_guard<std::mutex> lk(stats_mu_);
+            stats_.nr_ipc_nack_sent++;
+          }
+          for (;;) {
+            HeldFrame f;
+            GP_CHECK_MSG(recv_held(fd, &f), "client " << client_id << " closed before resending clock "
+                                                        << h.clock << " of table " << h.table_id);
+            cs_clock_with_updates_batch_msg_t r{};
+            if (f.parts.size() == 3 && f.parts[0].size() == sizeof r) std::memcpy(&r, f.parts[0].data(), sizeof r);
+            if (f.parts.size() == 3 && r.cmd == CLOCK_WITH_UPDATES_BATCH && r.clock == h.clock &&
+                r.table_id == h.table_id) {
+              const std::vector<RecvPart> v = f.view();
+              GP_CHECK_EQ(v[1].size / sizeof(RowKey), n);
+              GP_CHECK_EQ(v[2].size, n * kRowBytes);
+              take_keys(v[1]);  // (the resend always carries the keys)
+              rows = f.rows;
+              break;
+            }
+            held.push_back(std::move(f));
+          }
+        }
       } else {
         GP_CHECK_EQ(parts[2].size, n * kRowBytes);
-        b.host_rows = ctx.rows;
       }
+      if (!b.device_rows) b.host_rows = rows;
       b.num_rows = n;
       ch.server->post_updates(std::move(b));
     } else if (cmd == kCmdRefreshAck) {
@@ -304,6 +395,13 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       std::memcpy(&a, parts[0].data, sizeof a);
       GP_CHECK_EQ(a.client_id, client_id);
       ch.server->release(client_id, a.table_id, a.version);
+    } else if (cmd == kCmdVersionNack) {
+      GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(VersionNackMsg));
+      VersionNackMsg m;
+      std::memcpy(&m, parts[0].data, sizeof m);
+      GP_CHECK_EQ(m.client_id, client_id);
+      if (!resend_stream) resend_stream = std::make_unique<Stream>();
+      resend_version(ch, client_id, m, resend_buf, *resend_stream);
     } else if (cmd == CLOCK) {
       GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(cs_clock_msg_t));
       cs_clock_msg_t h;
@@ -320,13 +418,127 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       ch.server->post_shutdown(client_id);
       // its last frame, kCmdReaderDone, comes once it has handled this
       // server's SHUTDOWN (shutdown()): this process waits for it
-      continue;
     } else if (cmd == kCmdReaderDone) {
-      break;
+      return false;
     } else {
       GP_CHECK_MSG(false, "server received unknown command " << (int)cmd);
     }
+    return true;
+  };
+  for (;;) {
+    if (!held.empty()) {
+      HeldFrame f = std::move(held.front());
+      held.pop_front();
+      if (!handle(f.view(), f.rows)) break;
+      continue;
+    }
+    ctx.rows.reset();
+    if (!recv_frame(fd, parts, scratch, alloc, &ctx)) break;
+    if (!handle(parts, ctx.rows)) break;
   }
+}
+
+// A client NACKed master version m.version (it could not map it): the same
+// refresh again as a socket frame from the version's rows (the client still
+// holds the version, so nothing wrote it), then the hold goes back and the
+// handle counts as not sent.
+void ClientLib::resend_version(Channel &ch, uint32_t c, const VersionNackMsg &m, PinnedArray<float> &buf,
+                               const Stream &st) {
+  const float *rows = nullptr;
+  size_t n = 0;
+  const RowKey *keys = nullptr;
+  ch.server->held_version(c, m.table_id, m.version, &rows, &n, &keys);
+  const size_t floats = n * ROW_DATA_SIZE;
+  if (buf.size() < floats) buf.resize(floats);
+  if (floats) GP_CALL(gp_memcpy_async(buf.data(), rows, floats * sizeof(float), st.get()));
+  st.sync();
+  sc_read_row_batch_msg_t h{};
+  h.cmd = READ_ROW_BATCH;
+  h.server_id = process_id_;
+  h.data_age = m.data_age;
+  h.self_clock = m.self_clock;
+  h.table_id = m.table_id;
+  GP_CHECK_MSG(send_to_client(ch, c, {Part{&h, sizeof h}, Part{keys, n * sizeof(RowKey)},
+                                      Part{buf.data(), floats * sizeof(float)}}),
+               "resend to client " << c << " failed");
+  {
+    std::lock_guard<std::mutex> lk(ch.ipc_mu);
+    ch.version_sent[c][m.table_id].erase(m.version);
+  }
+  ch.server->release(c, m.table_id, m.version);
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nr_ipc_resent++;
+}
+
+// A server NACKed this client's oplog slice of (table, clock): the oplog is
+// still here (reclaimed only once every server's refresh covers the clock,
+// and this server's cannot before it has these rows), so the slice goes again
+// as an ordinary socket frame; push_updates exports a fresh buffer in place of
+// the NACKed one on its next use.
+void ClientLib::resend_oplog(Channel &ch, uint32_t s, const OplogNackMsg &m, PinnedArray<float> &buf,
+                             const Stream &st) {
+  std::shared_ptr<DeviceArray<float>> oplog;
+  std::shared_ptr<const std::vector<RowKey>> keys;
+  size_t a = 0, n = 0;
+  {
+    std::lock_guard<std::mutex> lk(ch.mu);
+    GP_CHECK_LT(m.table_id, ch.tables.size());
+    ParamCache &pc = ch.tables[m.table_id];
+    auto it = pc.oplog.find(m.clock);
+    GP_CHECK_MSG(it != pc.oplog.end(), "server " << s << " NACKed clock " << m.clock << " of table " << m.table_id
+                                                 << ", whose oplog is gone");
+    oplog = it->second;
+    keys = pc.row_keys;
+    a = pc.server_row_start[s];
+    n = pc.server_num_rows[s];
+    pc.ipc_nacked.emplace_back((size_t)(m.buffer_id & 0xffffffffu), s);
+  }
+  const size_t floats = n * ROW_DATA_SIZE;
+  if (buf.size() < floats) buf.resize(floats);
+  if (floats) GP_CALL(gp_memcpy_async(buf.data(), oplog->data() + a * ROW_DATA_SIZE, floats * sizeof(float), st.get()));
+  st.sync();
+  cs_clock_with_updates_batch_msg_t h{};
+  h.cmd = CLOCK_WITH_UPDATES_BATCH;
+  h.client_id = process_id_;
+  h.clock = m.clock;
+  h.table_id = m.table_id;
+  {
+    // (also after this client's SHUTDOWN: the server's reader awaits this
+    // frame and holds the SHUTDOWN back behind it)
+    std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
+    GP_CHECK_MSG(send_frame(ch.server_fd[s], {Part{&h, sizeof h}, Part{keys->data() + a, n * sizeof(RowKey)},
+                                              Part{buf.data(), floats * sizeof(float)}}),
+                 "resend to server " << s << " failed");
+  }
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nr_ipc_resent++;
+}
+
+bool ClientLib::send_to_client(Channel &ch, uint32_t c, const std::vector<Part> &parts) {
+  std::lock_guard<std::mutex> lk(*ch.client_send_mu[c]);
+  return send_frame(ch.client_fd[c], parts);
+}
+
+bool ClientLib::ipc_export(void *handle, void *base, int kind) {
+  const bool fault = ipc_fault_ && !ipc_fault_used_[kind].exchange(true);
+  if (fault && ipc_fault_ == 2) {
+    std::cerr << "libgeeps: GEEPS_TEST_IPC_FAULT=refuse: export " << (kind ? "of a master version" : "of an oplog")
+              << " refused\n";
+    return false;
+  }
+  if (gp_ipc_get_handle(handle, base) != GP_OK) {
+    std::cerr << "libgeeps: IPC export of " << base << " refused (" << gp_last_error()
+              << "); the rows go by socket\n";
+    return false;
+  }
+  if (fault) {
+    // the tag's last byte (gp_reduce.hip IpcHandleOut: the runtime's 64-B
+    // handle, the tag's offset, then the 16-B tag): the importer's check fails
+    static_cast<uint8_t *>(handle)[64 + 8 + 15] ^= 0x5a;
+    std::cerr << "libgeeps: GEEPS_TEST_IPC_FAULT=tag: corrupted the tag of an exported "
+              << (kind ? "master version" : "oplog") << "\n";
+  }
+  return true;
 }
 
 namespace {
@@ -385,10 +597,23 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
     if (b->size() * 4 < size) b->resize((size + 3) / 4);
     return b->data();
   };
-  for (;;) {
-    if (stream_recv ? !recv_frame_chunked(fd, parts, scratch, alloc_landing, &ctx, kWireChunk, landed)
-                    : !recv_frame(fd, parts, scratch, alloc_pinned, &ctx))
-      break;
+  std::deque<HeldFrame> held;  // frames after a NACKed refresh, until its resend
+  PinnedArray<float> resend_buf;
+  auto ack_all = [&](uint32_t table, const std::vector<int> &released) {
+    for (int v : released) {
+      RefreshAckMsg a{};
+      a.cmd = kCmdRefreshAck;
+      a.client_id = process_id_;
+      a.table_id = table;
+      a.version = v;
+      ack_to_server(ch, server_id, a);
+    }
+  };
+  // false: the server's SHUTDOWN (its last frame).  `in_landing`: part 2's
+  // rows were streamed into `landing` (else they are in host memory at
+  // parts[2].data).
+  std::function<bool(const std::vector<RecvPart> &, bool)> handle = [&](const std::vector<RecvPart> &parts,
+                                                                         bool in_landing) {
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == SHUTDOWN) {
@@ -397,7 +622,15 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
       // before its process exits and frees what its handles named.
       GP_CALL(gp_device_synchronize());
       reader_done_to_server(ch, server_id);
-      break;
+      return false;
+    }
+    if (cmd == kCmdOplogNack) {
+      GP_CHECK(parts.size() == 1 && parts[0].size == sizeof(OplogNackMsg));
+      OplogNackMsg m;
+      std::memcpy(&m, parts[0].data, sizeof m);
+      GP_CHECK_EQ(m.server_id, server_id);
+      resend_oplog(ch, server_id, m, resend_buf, h2d);
+      return true;
     }
     if (reader_delay_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(reader_delay_us_));
     GP_CHECK((parts.size() == 3 || parts.size() == 4) &&
@@ -415,14 +648,15 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
       std::memcpy(&rv, parts[3].data, sizeof rv);
       GP_CHECK(rv.version >= 0);
       void *ptr = nullptr;
+      bool ok = true;
       {
         std::lock_guard<std::mutex> lk(ch.mu);
         auto &mapped = ch.tables[h.table_id].server_versions[server_id];
         if (rv.has_handle) {
           GP_CHECK_MSG(!mapped.count(rv.version), "version " << rv.version << " mapped twice");
-          GP_CALL(gp_ipc_open_handle(&ptr, rv.handle));
-          mapped[rv.version] = ptr;
-          if (ipc_log())
+          ok = gp_ipc_open_handle(&ptr, rv.handle) == GP_OK;
+          if (ok) mapped[rv.version] = ptr;
+          if (ok && ipc_log())
             std::cerr << "libgeeps ipc map version: client " << process_id_ << " ch " << ch.id << " server "
                       << server_id << " table " << h.table_id << " version " << rv.version << " rows "
                       << rv.num_rows << " -> " << ptr << "\n";
@@ -432,38 +666,89 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
           ptr = it->second;
         }
       }
+      if (!ok) {
+        // NACK: the server sends this refresh again as a socket frame; hold
+        // later frames back until it arrives, then take it as a copy
+        std::cerr << "libgeeps: client " << process_id_ << " ch " << ch.id << " could not map master version "
+                  << rv.version << " of server " << server_id << " (" << gp_last_error()
+                  << "); asking for the refresh by socket\n";
+        VersionNackMsg m{};
+        m.cmd = kCmdVersionNack;
+        m.client_id = process_id_;
+        m.table_id = h.table_id;
+        m.version = rv.version;
+        m.data_age = h.data_age;
+        m.self_clock = h.self_clock;
+        {
+          std::lock_guard<std::mutex> lk(*ch.server_send_mu[server_id]);
+          // after this client's SHUTDOWN it reads nothing more, and the server
+          // has let go of its holds: the refresh is dropped
+          if (ch.server_shut[server_id]) return true;
+          GP_CHECK_MSG(send_frame(ch.server_fd[server_id], {Part{&m, sizeof m}}),
+                       "version NACK to server " << server_id << " failed");
+        }
+        {
+          std::lock_guard<std::mutex> lk(stats_mu_);
+          stats_.nr_ipc_nack_sent++;
+        }
+        for (;;) {
+          HeldFrame f;
+          GP_CHECK_MSG(recv_held(fd, &f), "server " << server_id << " closed before resending table "
+                                                    << h.table_id << " at data age " << h.data_age);
+          sc_read_row_batch_msg_t r{};
+          if (f.parts.size() == 3 && f.parts[0].size() == sizeof r) std::memcpy(&r, f.parts[0].data(), sizeof r);
+          if (f.parts.size() == 3 && r.cmd == READ_ROW_BATCH && r.table_id == h.table_id &&
+              r.data_age == h.data_age) {
+            const std::vector<RecvPart> v = f.view();
+            GP_CHECK_EQ(v[2].size, rv.num_rows * kRowBytes);
+            ack_all(h.table_id, recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
+                                               static_cast<const float *>(v[2].data), rv.num_rows, -1));
+            break;
+          }
+          held.push_back(std::move(f));
+        }
+        return true;
+      }
       const float *src = static_cast<const float *>(ptr);
       if (ch.stage_refresh_from[server_id] && rv.num_rows) {
         // A staged refresh (a server on another GPU): the peer copy over xGMI
         // goes to this reader's landing buffer first, on its own stream and
         // outside the channel lock, so the refreshes of several peers come
-        // over their links at once; recv_row_batch's copy into the cache under
-        // the lock is then local HBM.  (The version stays held until then.)
+        // over their links at once; recv_row_batch then swaps it into the
+        // cache under the lock (ParamCache::shard_buf).  (The version stays
+        // held until then.)
         const size_t bytes = rv.num_rows * kRowBytes;
         if (landing.size() * sizeof(float) < bytes) landing.resize(bytes / sizeof(float));
         GP_CALL(gp_memcpy_async(landing.data(), src, bytes, h2d.get()));
         h2d.sync();
         src = landing.data();
       }
-      const std::vector<int> released =
-          recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock, src, rv.num_rows, rv.version);
-      for (int v : released) {
-        RefreshAckMsg a{};
-        a.cmd = kCmdRefreshAck;
-        a.client_id = process_id_;
-        a.table_id = h.table_id;
-        a.version = v;
-        ack_to_server(ch, server_id, a);
-      }
-      continue;
+      ack_all(h.table_id, recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock, src,
+                                         rv.num_rows, rv.version, src == landing.data() ? &landing : nullptr));
+      return true;
     }
     const size_t n = parts[1].size / sizeof(RowKey);
     GP_CHECK_EQ(parts[2].size, n * kRowBytes);
-    h2d.sync();  // every piece's copy into `landing` has landed
-    const std::vector<int> released =
-        recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
-                       n && stream_recv ? landing.data() : static_cast<const float *>(parts[2].data), n, -1);
-    GP_CHECK_MSG(released.empty(), "socket refresh replaced an in-place shard of server " << server_id);
+    if (in_landing) h2d.sync();  // every piece's copy into `landing` has landed
+    // (a socket refresh may replace a shard this client read in place, when the
+    // server's export of its version was refused: those versions go back)
+    ack_all(h.table_id,
+            recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
+                           n && in_landing ? landing.data() : static_cast<const float *>(parts[2].data), n, -1,
+                           n && in_landing ? &landing : nullptr));
+    return true;
+  };
+  for (;;) {
+    if (!held.empty()) {
+      HeldFrame f = std::move(held.front());
+      held.pop_front();
+      if (!handle(f.view(), false)) break;
+      continue;
+    }
+    if (stream_recv ? !recv_frame_chunked(fd, parts, scratch, alloc_landing, &ctx, kWireChunk, landed)
+                    : !recv_frame(fd, parts, scratch, alloc_pinned, &ctx))
+      break;
+    if (!handle(parts, stream_recv)) break;
   }
 }
 
@@ -484,11 +769,23 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
   IpcRefreshVersion rv{};
   rv.version = r.version;
   rv.num_rows = r.num_rows;
-  auto &sent = ch.version_sent[client_id][r.table_id];
-  if (!sent.count(r.version)) {
-    GP_CALL(gp_ipc_get_handle(rv.handle, const_cast<float *>(r.device_rows)));
+  bool first;
+  {
+    std::lock_guard<std::mutex> lk(ch.ipc_mu);  // (a NACK's resend erases from it on a reader thread)
+    first = !ch.version_sent[client_id][r.table_id].count(r.version);
+  }
+  if (first) {
+    if (!ipc_export(rv.handle, const_cast<float *>(r.device_rows), 1)) {
+      // the runtime refused the export: this refresh goes as a copy
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      stats_.nr_ipc_export_refused++;
+      return false;
+    }
     rv.has_handle = 1;
-    sent.insert(r.version);
+    {
+      std::lock_guard<std::mutex> lk(ch.ipc_mu);
+      ch.version_sent[client_id][r.table_id].insert(r.version);
+    }
     if (ipc_log())
       std::cerr << "libgeeps ipc export version: server " << process_id_ << " ch " << ch.id << " client "
                 << client_id << " table " << r.table_id << " version " << r.version << " rows " << r.num_rows
@@ -500,8 +797,8 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
   h.data_age = r.data_age;
   h.self_clock = r.self_clock;
   h.table_id = r.table_id;
-  GP_CHECK_MSG(send_frame(ch.client_fd[client_id], {Part{&h, sizeof h}, Part{nullptr, 0},
-                                                    Part{nullptr, 0}, Part{&rv, sizeof rv}}),
+  GP_CHECK_MSG(send_to_client(ch, client_id, {Part{&h, sizeof h}, Part{nullptr, 0},
+                                               Part{nullptr, 0}, Part{&rv, sizeof rv}}),
                "send to client " << client_id << " failed");
   *held = true;
   return true;
@@ -564,7 +861,7 @@ void ClientLib::remote_shutdown_ack(uint32_t channel, uint32_t client_id) {
   cs_clock_msg_t h{};
   h.cmd = SHUTDOWN;
   h.client_id = process_id_;
-  GP_CHECK_MSG(send_frame(ch.client_fd[client_id], {Part{&h, sizeof h}}),
+  GP_CHECK_MSG(send_to_client(ch, client_id, {Part{&h, sizeof h}}),
                "shutdown ack to client " << client_id << " failed");
 }
 
@@ -593,6 +890,7 @@ bool ClientLib::remote_reply(uint32_t channel, uint32_t client_id, const RowBatc
   h.data_age = r.data_age;
   h.self_clock = r.self_clock;
   h.table_id = r.table_id;
+  std::lock_guard<std::mutex> lk(*ch.client_send_mu[client_id]);
   GP_CHECK_MSG(send_frame_chunked(fd, {Part{&h, sizeof h}, Part{r.keys, r.num_rows * sizeof(RowKey)},
                                        Part{ch.reply_buf.data(), floats * 4}},
                                   kWireChunk, [&](size_t k) { ch.reply_events[k]->sync(); }),
@@ -689,18 +987,39 @@ void ClientLib::finish_virtual_iteration() {
         pc.index[r] = pc.num_rows++;
         pc.row_keys->emplace_back(t, r);
       }
+      pc.server_row_start.resize(num_processes_);
+      pc.server_num_rows.resize(num_processes_);
+      {
+        const size_t div = pc.num_rows / num_processes_, res = pc.num_rows % num_processes_;
+        for (size_t i = 0; i < num_processes_; ++i) {
+          pc.server_row_start[i] = div * i + std::min(i, res);
+          pc.server_num_rows[i] = div + (i < res ? 1 : 0);
+        }
+      }
       // The cache's own rows are needed only for refreshes that arrive as
-      // copies (socket peers, read-my-writes, which also scatters into it).
-      // When every server's shard will be read in place, it is never touched
-      // (a Read waits for every server's first refresh) and is not allocated.
-      bool copies = config_.read_my_writes;
-      for (uint32_t s = 0; s < num_processes_; ++s)
-        copies = copies || (s != process_id_ && (!ipc_to(s) || ch.stage_refresh_from[s]));
-      if (copies) {
+      // copies (socket peers, staged peers on another GPU, read-my-writes,
+      // which also scatters into it).  When every server's shard will be read
+      // in place, it is never touched (a Read waits for every server's first
+      // refresh) and is not allocated.  Without read-my-writes each copied
+      // shard gets a buffer of its own, which refreshes replace by a swap
+      // (shard_buf); with it, the one flat `data` the Updates scatter into.
+      auto copied = [&](uint32_t s) { return s != process_id_ && (!ipc_to(s) || ch.stage_refresh_from[s]); };
+      bool copies = false;
+      for (uint32_t s = 0; s < num_processes_; ++s) copies = copies || copied(s);
+      if (config_.read_my_writes) {
         pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
         if (pc.num_rows) GP_CALL(gp_zero(pc.data.data(), pc.data.size(), ch.stream->get()));
+        planned += pc.data.bytes();
+      } else if (copies) {
+        pc.shard_buf.resize(num_processes_);
+        for (uint32_t s = 0; s < num_processes_; ++s) {
+          if (!copied(s) || pc.server_num_rows[s] == 0) continue;
+          pc.shard_buf[s].resize(pc.server_num_rows[s] * ROW_DATA_SIZE);
+          GP_CALL(gp_zero(pc.shard_buf[s].data(), pc.shard_buf[s].size(), ch.stream->get()));
+          planned += pc.shard_buf[s].bytes();
+        }
       }
-      planned += pc.num_rows * kRowBytes * ((copies ? 1 : 0) + entries);
+      planned += pc.num_rows * kRowBytes * entries;
       // the server's staging buckets: one per pending bucket of a peer on
       // another GPU (its slice peer-copied in) or of a remote client (its
       // socket rows copied in), at most kMaxPendingBuckets (the queue is
@@ -708,13 +1027,6 @@ void ClientLib::finish_virtual_iteration() {
       size_t staged_peers = 0;
       for (uint32_t s = 0; s < num_processes_; ++s)
         staged_peers += (ch.stage_from[s] || (s != process_id_ && !ipc_to(s))) ? 1 : 0;
-      pc.server_row_start.resize(num_processes_);
-      pc.server_num_rows.resize(num_processes_);
-      const size_t div = pc.num_rows / num_processes_, res = pc.num_rows % num_processes_;
-      for (size_t i = 0; i < num_processes_; ++i) {
-        pc.server_row_start[i] = div * i + std::min(i, res);
-        pc.server_num_rows[i] = div + (i < res ? 1 : 0);
-      }
       // + this process's server's master versions of the shard: two (the
       // current one and the next, built beside it while clients read it in
       // place); a lagging reader can make it up to clients + 2 (server.hpp)
@@ -734,6 +1046,7 @@ void ClientLib::finish_virtual_iteration() {
       pc.deferred.assign(num_processes_, {});
       pc.read_events.assign(num_processes_, {});
       pc.server_clock.assign(num_processes_, INITIAL_DATA_AGE);
+      rebuild_segments(pc);
     }
     ch.stream->sync();
   }
@@ -1094,11 +1407,22 @@ std::shared_ptr<DeviceArray<float>> ClientLib::get_oplog(ParamCache &pc, iter_t 
   // clientlib-data.cpp:356-371).  A pooled buffer is reused once nothing (the
   // in-process server's pending bucket included) references it.
   std::shared_ptr<DeviceArray<float>> buf;
-  for (auto &b : pc.oplog_pool)
-    if (b.use_count() == 1) {
-      buf = b;
-      break;
+  for (size_t k = 0; k < pc.oplog_pool.size(); ++k) {
+    auto &b = pc.oplog_pool[k];
+    if (b.use_count() != 1) continue;
+    if (k < pc.oplog_bad.size() && pc.oplog_bad[k]) {
+      // its export was refused or a server could not map it: a fresh buffer
+      // takes its place (the old one is kept until Shutdown, since another
+      // server may still have it mapped), exported anew to every server
+      pc.retired.push_back(b);
+      b = std::make_shared<DeviceArray<float>>(pc.num_rows * ROW_DATA_SIZE, kShared);
+      pc.oplog_bad[k] = 0;
+      if (k < pc.exported.size()) std::fill(pc.exported[k].begin(), pc.exported[k].end(), 0);
+      zero = true;
     }
+    buf = b;
+    break;
+  }
   if (!buf) {
     // (a same-node server maps it over IPC: a whole allocation)
     pc.oplog_pool.push_back(std::make_shared<DeviceArray<float>>(pc.num_rows * ROW_DATA_SIZE, kShared));
@@ -1219,9 +1543,22 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
   size_t pool_id = 0;
   std::vector<uint8_t> *exported = nullptr;  // app thread only
   std::vector<uint8_t> *keys_sent = nullptr;  // app thread only
+  std::vector<uint8_t> *bad = nullptr;        // app thread only
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[table_id];
+    if (pc.oplog_bad.size() < pc.oplog_pool.size()) pc.oplog_bad.resize(pc.oplog_pool.size(), 0);
+    if (pc.exported.size() < pc.oplog_pool.size())
+      pc.exported.resize(pc.oplog_pool.size(), std::vector<uint8_t>(num_processes_, 0));
+    // servers that could not map a buffer (their NACK's resend went already):
+    // it is replaced before its next use, and exported anew
+    for (auto &nk : pc.ipc_nacked)
+      if (nk.first < pc.oplog_pool.size()) {
+        pc.exported[nk.first][nk.second] = 0;
+        pc.oplog_bad[nk.first] = 1;
+      }
+    pc.ipc_nacked.clear();
+    bad = &pc.oplog_bad;
     auto it = pc.oplog.find(clock);
     if (it != pc.oplog.end()) oplog = it->second;
     starts = pc.server_row_start;
@@ -1244,6 +1581,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
     }
   }
   size_t remote_bytes = 0;
+  uint8_t ch_export_handle[kIpcHandleBytes];  // the export made for server s, when first
   for (uint32_t s = 0; s < num_processes_; ++s) {
     if (!oplog) {
       // clock_broadcast: a CLOCK with no updates (encoder-decoder.cpp:85-100).
@@ -1271,7 +1609,20 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       b.device_rows = oplog->data() + a * ROW_DATA_SIZE;
       b.keepalive = oplog;  // zero-copy: the server reads the oplog slice in place
       ch.server->post_updates(std::move(b));
-    } else if (ipc_to(s)) {
+    } else if (ipc_to(s) && [&] {
+                 if ((*exported)[s]) return true;
+                 IpcRowsRef probe{};
+                 if (ipc_export(probe.handle, oplog->data(), 0)) {
+                   std::memcpy(ch_export_handle, probe.handle, sizeof probe.handle);
+                   return true;
+                 }
+                 // the runtime refused the export: this slice goes by socket,
+                 // and a fresh buffer replaces this one on its next use
+                 (*bad)[pool_id] = 1;
+                 std::lock_guard<std::mutex> lk(stats_mu_);
+                 stats_.nr_ipc_export_refused++;
+                 return false;
+               }()) {
       // Same-node server: it copies its slice straight out of this oplog.
       cs_clock_with_updates_batch_msg_t h{};
       h.cmd = CLOCK_WITH_UPDATES_BATCH;
@@ -1284,7 +1635,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       ref.offset = a * kRowBytes;
       ref.bytes = n * kRowBytes;
       if (!(*exported)[s]) {
-        GP_CALL(gp_ipc_get_handle(ref.handle, oplog->data()));
+        std::memcpy(ref.handle, ch_export_handle, sizeof ref.handle);
         ref.has_handle = 1;
         (*exported)[s] = 1;
         if (ipc_log())
@@ -1329,7 +1680,8 @@ void ClientLib::reclaim_oplogs(ParamCache &pc, iter_t upto) {
 // (clientlib-data.cpp:51-151, clientlib-cbk.cpp:81-104).
 std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
                                            uint32_t table_id, iter_t data_age, iter_t self_clock,
-                                           const float *rows, size_t num_rows, int version) {
+                                           const float *rows, size_t num_rows, int version,
+                                           DeviceArray<float> *landing) {
   const double t0 = now_s();
   Channel &ch = *channels_[channel];
   std::vector<int> released;
@@ -1356,7 +1708,18 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
       reclaim_oplogs(pc, min_clock);
       pc.server_clock_min = min_clock;
     }
-    if (num_rows == 0 && pc.num_rows && pc.data.size() == 0) {
+    bool own_buf = !pc.shard_buf.empty() && pc.shard_buf[server_id].data();
+    if (num_rows && !own_buf && pc.data.size() == 0 && !(version >= 0 && !config_.read_my_writes &&
+                                                          !ch.stage_refresh_from[server_id])) {
+      // a copied refresh from a server whose shard this cache reads in place
+      // (its export of the version was refused, IPC recovery): the shard
+      // gets a buffer of its own
+      if (pc.shard_buf.empty()) pc.shard_buf.resize(num_processes_);
+      pc.shard_buf[server_id].resize(num_rows * ROW_DATA_SIZE);
+      own_buf = true;
+      rebuild_segments(pc);
+    }
+    if (num_rows == 0 && pc.num_rows && pc.data.size() == 0 && !own_buf) {
       // An empty shard reads as zeros from the cache's own rows, which a
       // cache that takes every refresh in place has not allocated yet.
       pc.data.resize(pc.num_rows * ROW_DATA_SIZE);
@@ -1400,26 +1763,37 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
         // gathers from local HBM); or read-my-writes, which re-applies this
         // client's own not-yet-reflected updates on top of the shard and so
         // needs a private copy (clientlib-data.cpp:132-150: cublasSaxpy -> gp_add).
-        GP_CHECK_MSG(pc.data.size() == pc.num_rows * ROW_DATA_SIZE,
-                     "copied refresh from server " << server_id << " into an unallocated cache");
-        float *dst = pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
         const size_t floats = num_rows * ROW_DATA_SIZE;
+        GP_CHECK_MSG(own_buf || pc.data.size() == pc.num_rows * ROW_DATA_SIZE,
+                     "copied refresh from server " << server_id << " into an unallocated cache");
+        float *dst = own_buf ? pc.shard_buf[server_id].data()
+                             : pc.data.data() + pc.server_row_start[server_id] * ROW_DATA_SIZE;
+        bool swapped = false;
+        if (own_buf && landing && landing->data() == rows && landing->size() >= floats) {
+          // the reader's landing buffer holds the refreshed shard: it becomes
+          // the shard's buffer and the old one the reader's next landing
+          // buffer (every Read of the old one finished under this lock)
+          pc.shard_buf[server_id].swap(*landing);
+          swapped = true;
+          rebuild_segments(pc);
+        }
         std::vector<const float *> own;  // read-my-writes: the unreflected clocks' oplog slices, in order
         if (config_.read_my_writes)
           for (iter_t c = self_clock + 1, fc = fast_clock_.load(); c <= fc; ++c) {
             auto it = pc.oplog.find(c);
             if (it != pc.oplog.end()) own.push_back(it->second->data() + pc.server_row_start[server_id] * ROW_DATA_SIZE);
           }
-        if (version >= 0 && !staged) {
-          // a same-GPU master version (read-my-writes): copy and re-apply in
-          // one pass, dst = ((shard + own[0]) + own[1]) + ..., the bits of the
-          // copy-then-add sequence below, through the N-way sum kernels
+        if (swapped) {
+          // (no read-my-writes here: nothing to re-apply)
+        } else if (!own.empty()) {
+          // read-my-writes: copy and re-apply in one pass, dst = ((shard +
+          // own[0]) + own[1]) + ..., the bits of a copy followed by one add per
+          // oplog (clientlib-data.cpp:123-150), through the N-way sum kernels
           GP_CALL(gp_bucket_sum_into(dst, rows, own.data(), (int)own.size(), floats, ch.svc_stream->get()));
         } else {
           GP_CALL(gp_memcpy_async(dst, rows, num_rows * kRowBytes, ch.svc_stream->get()));
-          for (const float *op : own) GP_CALL(gp_add(floats, dst, op, dst, ch.svc_stream->get()));
         }
-        ch.svc_stream->sync();
+        if (!swapped) ch.svc_stream->sync();
         if (version >= 0) released.push_back(version);  // copied: give it back now
         if (prev >= 0) {
           retire(prev);
@@ -1452,12 +1826,15 @@ void ClientLib::rebuild_segments(ParamCache &pc) {
     const size_t n = pc.server_num_rows[s];
     if (n == 0) continue;
     const size_t first = pc.server_row_start[s];
-    const bool in_place = pc.live_ver[s] >= 0;
+    const bool in_place = !pc.live_ver.empty() && pc.live_ver[s] >= 0;
+    // a shard of its own buffer (shard_buf) is a segment of its own too
+    const bool own = !pc.shard_buf.empty() && pc.shard_buf[s].data();
     // (a shard neither in place nor copied yet is never read: see Read's wait)
     const float *base = in_place ? pc.live_ptr[s]
-                                 : pc.data.data() ? pc.data.data() + first * ROW_DATA_SIZE : nullptr;
-    any_in_place = any_in_place || in_place;
-    if (t.count && base == next_flat && !in_place) {
+                        : own    ? pc.shard_buf[s].data()
+                        : pc.data.data() ? pc.data.data() + first * ROW_DATA_SIZE : nullptr;
+    any_in_place = any_in_place || in_place || own;
+    if (t.count && base == next_flat && !in_place && !own) {
       next_flat = base + n * ROW_DATA_SIZE;
       continue;
     }
@@ -1466,7 +1843,7 @@ void ClientLib::rebuild_segments(ParamCache &pc) {
     t.first_row[t.count] = t.count ? first : 0;
     t.base[t.count] = const_cast<float *>(base);
     ++t.count;
-    next_flat = in_place ? nullptr : base + n * ROW_DATA_SIZE;
+    next_flat = in_place || own || !base ? nullptr : base + n * ROW_DATA_SIZE;
   }
   pc.segs = t;
   pc.segmented = any_in_place;

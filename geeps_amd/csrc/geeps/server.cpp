@@ -121,6 +121,20 @@ void TabletServer::release_all(uint32_t client_id) {
   release_cv_.notify_all();
 }
 
+void TabletServer::held_version(uint32_t client_id, uint32_t table_id, int version, const float **rows,
+                                size_t *num_rows, const RowKey **keys) {
+  std::lock_guard<std::mutex> lk(hold_mu_);
+  GP_CHECK_LT(table_id, tables_.size());
+  GP_CHECK_LT(client_id, num_clients_);
+  DataTable &t = tables_[table_id];
+  GP_CHECK_MSG(version >= 0 && (size_t)version < t.holders.size() && t.holders[version][client_id],
+               "client " << client_id << " asks for a resend of master version " << version << " of table "
+                         << table_id << " it does not hold");
+  *rows = t.versions[version]->data();
+  *num_rows = t.row_count;
+  *keys = t.row_keys.data();  // (immutable once the first update defined the shard)
+}
+
 void TabletServer::wait_shutdown() {
   std::unique_lock<std::mutex> lk(mu_);
   shutdown_cv_.wait(lk, [this] { return shutdown_done_; });

@@ -156,6 +156,11 @@ class TabletServer {
   void release(uint32_t client_id, uint32_t table_id, int version);
   // ... nor any version of any table (its SHUTDOWN arrived).
   void release_all(uint32_t client_id);
+  // Master version `version` of `table_id`, which `client_id` holds (so the
+  // server does not write it): its rows, row count and keys, for a resend of
+  // a refresh the client could not map (kCmdVersionNack).  Thread-safe.
+  void held_version(uint32_t client_id, uint32_t table_id, int version, const float **rows,
+                    size_t *num_rows, const RowKey **keys);
   // Blocks until every client has sent SHUTDOWN and all were acknowledged.
   void wait_shutdown();
   // Blocks until every message posted before it has been processed.

@@ -153,4 +153,39 @@ struct RefreshAckMsg {
   int32_t version;
 };
 
+// IPC recovery.  A handle the runtime refuses to map, or a
+// mapping without the exporter's tag, costs one resend of the rows over the
+// socket instead of the job:
+//
+// server -> client: the server could not map the oplog buffer that the
+// client's CLOCK_WITH_UPDATES_BATCH for (table, clock) named.  The client
+// sends that slice again as an ordinary socket frame (keys + rows), and
+// exports a fresh buffer in place of this one on its next use.  The server's
+// reader holds the client's later frames back until the resend arrives, so
+// the server sees the client's messages in their order.
+constexpr command_t kCmdOplogNack = 103;
+struct OplogNackMsg {
+  command_t cmd;
+  uint32_t server_id;
+  uint32_t table_id;
+  uint32_t pad;
+  iter_t clock;
+  uint64_t buffer_id;
+};
+// client -> server: the client could not map master version `version` of
+// `table_id` that the refresh of data age `data_age` named.  The server sends
+// that refresh again as a socket frame (keys + rows of the version, which the
+// client still holds, so it is unchanged), takes the hold back and forgets the
+// handle went out (the next refresh naming the version sends it again).  The
+// client's reader holds later frames back until the resend arrives.
+constexpr command_t kCmdVersionNack = 104;
+struct VersionNackMsg {
+  command_t cmd;
+  uint32_t client_id;
+  uint32_t table_id;
+  int32_t version;
+  iter_t data_age;
+  iter_t self_clock;
+};
+
 #endif  // GEEPS_AMD_WIRE_HPP_

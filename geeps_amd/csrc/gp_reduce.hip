@@ -1715,10 +1715,10 @@ template <bool COMPACT>
 __device__ __forceinline__ void index_verify(const gp_double_index *__restrict__ idx, const void *__restrict__ kept,
                                              size_t n, const uint64_t *__restrict__ base0_word,
                                              unsigned *__restrict__ gate_word, unsigned *__restrict__ host_word,
-                                             unsigned gen) {
+                                             unsigned gen, bool sticky) {
   const size_t step = (size_t)gridDim.x * kBlock * kCmpPerThread;
   const uint64_t base0 = COMPACT ? *base0_word : 0;
-  bool differs = false;
+  bool differs = sticky;
   for (size_t base = (size_t)blockIdx.x * kBlock * kCmpPerThread + threadIdx.x; base < n; base += step) {
     gp_double_index a[kCmpPerThread], b[kCmpPerThread];
     uint32_t c[kCmpPerThread];
@@ -1756,13 +1756,19 @@ __global__ __launch_bounds__(kBlock) void index_verify_kernel(const gp_double_in
                                                               const uint64_t *__restrict__ base0_word,
                                                               unsigned *__restrict__ gate_word,
                                                               unsigned *__restrict__ host_word, unsigned gen,
-                                                              const unsigned *__restrict__ broken) {
+                                                              const unsigned *__restrict__ broken,
+                                                              const unsigned *__restrict__ unsound) {
   bool use_compact = FORM == 1;
   if constexpr (FORM == 2) use_compact = __hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  // an entry whose inverse map was found unsound when it was built
+  // (inverse_scatter_kernel / inverse_count_kernel set the sticky word): every
+  // later call treats its index as changed, so no gated launch walks the map,
+  // however soon after the build it was queued
+  const bool sticky = __hip_atomic_load(unsound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   if (use_compact)
-    index_verify<true>(idx, compact, n, base0_word, gate_word, host_word, gen);
+    index_verify<true>(idx, compact, n, base0_word, gate_word, host_word, gen, sticky);
   else
-    index_verify<false>(idx, full, n, base0_word, gate_word, host_word, gen);
+    index_verify<false>(idx, full, n, base0_word, gate_word, host_word, gen, sticky);
 }
 
 // The compact copy of an index (built with the plan: on the first call for an
@@ -1857,7 +1863,8 @@ __global__ __launch_bounds__(kBlock) void inverse_scatter_kernel(const gp_double
                                                                  uint64_t off0, uint64_t off1,
                                                                  uint64_t *__restrict__ inv,
                                                                  unsigned *__restrict__ gate_word,
-                                                                 unsigned *__restrict__ host_word, unsigned gen) {
+                                                                 unsigned *__restrict__ host_word, unsigned gen,
+                                                                 unsigned *__restrict__ unsound) {
   const size_t total = rr.pre[rr.count];
   const size_t stride = (size_t)gridDim.x * kBlock;
   bool bad = false;
@@ -1868,6 +1875,7 @@ __global__ __launch_bounds__(kBlock) void inverse_scatter_kernel(const gp_double
     bad |= (f >> 32) != 0;
     inv[t] = ((uint64_t)e << 32) | (f & 0xffffffffu);
   }
+  if (bad) __hip_atomic_store(unsound, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (rare)
   flag_once(bad, gate_word, host_word, gen);
 }
 
@@ -1881,7 +1889,8 @@ constexpr int kCountPerThread = 16;
 __global__ __launch_bounds__(kBlock) void inverse_count_kernel(const uint64_t *__restrict__ inv, size_t rows,
                                                                uint64_t expected, unsigned long long *counters,
                                                                unsigned *__restrict__ gate_word,
-                                                               unsigned *__restrict__ host_word, unsigned gen) {
+                                                               unsigned *__restrict__ host_word, unsigned gen,
+                                                               unsigned *__restrict__ unsound) {
   const size_t step = (size_t)gridDim.x * kBlock * kCountPerThread;
   unsigned listed = 0;
   for (size_t base = (size_t)blockIdx.x * kBlock * kCountPerThread + threadIdx.x; base < rows; base += step) {
@@ -1905,6 +1914,7 @@ __global__ __launch_bounds__(kBlock) void inverse_count_kernel(const uint64_t *_
   if (__hip_atomic_fetch_add(&counters[1], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x - 1ull)
     return;
   if (__hip_atomic_load(&counters[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != expected) {
+    __hip_atomic_store(unsound, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(gate_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(host_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -2090,24 +2100,99 @@ struct CachedPlan {
   unsigned *dev_broken_word() const { return reinterpret_cast<unsigned *>(base0_word() + 1); }
   // inverse_count_kernel's listed-row count and finished-wave count
   unsigned long long *count_words() const { return reinterpret_cast<unsigned long long *>(base0_word() + 2); }
-  // Kernels of a call may still run on the device when an entry goes (it is
-  // dropped or evicted on the host): wait for them before any member frees
-  // what they read or write.
-  bool frees_memory() const {
-    auto last = [](const auto &b) { return b && b.use_count() == 1; };
-    return last(copy) || last(sorted) || last(spare) || last(gate) || last(compact) || last(inv) || changed ||
-           compact_broken;
+  // the inverse map was found unsound at its build (sticky: index_verify_kernel
+  // reads it on every later call)
+  unsigned *unsound_word() const { return reinterpret_cast<unsigned *>(base0_word() + 4); }
+  // The streams this entry's calls ran on, each with an event recorded after
+  // the call's last launch (mark_used): what the device may still be doing
+  // with the entry's buffers when the host drops it.
+  std::mutex use_mu;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+  void mark_used(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(use_mu);
+    hipEvent_t ev = nullptr;
+    for (auto &u : uses)
+      if (u.first == s) ev = u.second;
+    if (!ev) {
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+      }
+      uses.emplace_back(s, ev);
+    }
+    (void)hipEventRecord(ev, s);
   }
-  ~CachedPlan() {
-    if (!ready) return;
+  ~CachedPlan();
+};
+
+// A dropped or evicted entry's buffers and host-visible words, kept until the
+// device has passed every event of its calls (kernels of a call may still read
+// or write them): then freed in stream order.  An entry's drop never waits for
+// the device -- round 4 synchronised the whole device here, stalling every
+// stream of the process, libgeeps' server and reader streams included (ADVICE
+// r04).  Reaped at later unplanned calls and cache operations.
+struct Grave {
+  int device = 0;
+  std::vector<hipEvent_t> events;
+  hipEvent_t ready = nullptr;
+  std::vector<std::shared_ptr<DevBuf>> bufs;
+  std::vector<std::shared_ptr<PinnedWord>> words;
+};
+std::mutex g_graves_mu;
+// never destroyed: at process exit the runtime may be gone before static destructors
+std::vector<Grave> &g_graves = *new std::vector<Grave>();
+
+void reap_graves() {
+  std::vector<Grave> done;
+  {
+    std::lock_guard<std::mutex> lk(g_graves_mu);
+    for (auto it = g_graves.begin(); it != g_graves.end();) {
+      bool passed = true;
+      for (hipEvent_t e : it->events)
+        if (hipEventQuery(e) != hipSuccess) {
+          (void)hipGetLastError();  // "not ready" is not a caller's error
+          passed = false;
+          break;
+        }
+      if (passed) {
+        done.push_back(std::move(*it));
+        it = g_graves.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (Grave &g : done) {  // outside the lock: frees (hipFreeAsync) and slot returns
+    for (hipEvent_t e : g.events) (void)hipEventDestroy(e);
+    if (g.ready) (void)hipEventDestroy(g.ready);
+  }
+}
+
+CachedPlan::~CachedPlan() {
+  if (!ready) return;
+  Grave g;
+  g.device = key.device;
+  for (auto &u : uses) g.events.push_back(u.second);
+  g.ready = ready;
+  for (auto *b : {&copy, &sorted, &spare, &gate, &compact, &inv})
+    if (*b) g.bufs.push_back(std::move(*b));
+  for (auto *w : {&changed, &compact_broken})
+    if (*w) g.words.push_back(std::move(*w));
+  if (g.events.empty()) {  // no call recorded its launches (a failed build): wait for the device
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != key.device) (void)hipSetDevice(key.device);
-    if (frees_memory()) (void)hipDeviceSynchronize();
-    (void)hipEventDestroy(ready);
+    (void)hipDeviceSynchronize();
     if (cur >= 0 && cur != key.device) (void)hipSetDevice(cur);
   }
-};
+  std::lock_guard<std::mutex> lk(g_graves_mu);
+  g_graves.push_back(std::move(g));
+}
+
+// The entries the current unplanned call found or built (cache_find /
+// cache_insert on this thread): each gets mark_used on the call's stream once
+// the call has issued its last launch.
+thread_local std::vector<std::shared_ptr<CachedPlan>> t_touched;
 
 // gp_unplanned_stats_get's counters, in its field order
 enum UnplannedStat { kScans, kSteadyCalls, kStaleDrops, kInversePlans, kSortedPlans, kRangesPlans, kNumStats };
@@ -2123,6 +2208,7 @@ std::shared_ptr<CachedPlan> cache_find(const PlanKey &k) {
   for (auto &p : g_plan_cache)
     if (p->key == k) {
       p->last_use = ++g_plan_cache_tick;
+      t_touched.push_back(p);
       return p;
     }
   return nullptr;
@@ -2145,6 +2231,7 @@ void cache_insert(std::shared_ptr<CachedPlan> p) {
         ++it;
       }
     p->last_use = ++g_plan_cache_tick;
+    t_touched.push_back(p);
     g_plan_cache.push_back(std::move(p));
     auto total = [] {
       size_t b = 0;
@@ -2188,8 +2275,8 @@ int cache_first_sighting(const PlanKey &key, const gp_double_index *idx, size_t 
 int steady_state_setup(CachedPlan *p, const gp_double_index *idx, hipStream_t s, bool copy_if_broken = false) {
   const PlanKey &key = p->key;
   int rc = GP_OK;
-  // gate words, base0, broken, the inverse map's two counters
-  constexpr size_t kGateBytes = kGateSlots * sizeof(unsigned) + 4 * sizeof(uint64_t);
+  // gate words, base0, broken, the inverse map's two counters, its unsound word
+  constexpr size_t kGateBytes = kGateSlots * sizeof(unsigned) + 5 * sizeof(uint64_t);
   p->gate = std::make_shared<DevBuf>(kGateBytes, key.device, s, &rc);
   if (rc != GP_OK) return rc;
   p->changed = std::make_shared<PinnedWord>(key.device, &rc);
@@ -2243,11 +2330,11 @@ int cache_inverse_plan(const PlanKey &key, const gp_double_index *idx, const Ent
   const size_t grid = std::max<size_t>(1, std::min((p->resid + kBlock - 1) / kBlock, (size_t)num_cus() * 8));
   uint64_t *inv = static_cast<uint64_t *>(p->inv->p);
   hipLaunchKernelGGL(inverse_scatter_kernel<OP>, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, rr, key.off0,
-                     key.off1, inv, word, p->changed->p, *gen);
+                     key.off1, inv, word, p->changed->p, *gen, p->unsound_word());
   const size_t cper = (size_t)kBlock * kCountPerThread;
   const size_t cgrid = std::max<size_t>(1, std::min((inv_rows + cper - 1) / cper, (size_t)num_cus()));
   hipLaunchKernelGGL(inverse_count_kernel, dim3((unsigned)cgrid), dim3(kBlock), 0, s, inv, inv_rows,
-                     (uint64_t)p->resid, p->count_words(), word, p->changed->p, *gen);
+                     (uint64_t)p->resid, p->count_words(), word, p->changed->p, *gen, p->unsound_word());
   GP_HIP_TRY(hipGetLastError());
   GP_HIP_TRY(hipEventRecord(p->ready, s));
   *built = p;
@@ -2342,8 +2429,21 @@ int cache_second_sighting(const std::shared_ptr<CachedPlan> &seen, const gp_doub
 
 // The analysed form of launch_row_op (see the section comment).
 template <int OP>
+int launch_row_op_analyzed_body(float *y, const float *x, const gp_double_index *idx, size_t n, gp_double_index off,
+                                size_t row_size, size_t limit, hipStream_t s);
+template <int OP>
 int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx, size_t n, gp_double_index off,
                            size_t row_size, size_t limit, hipStream_t s) {
+  reap_graves();
+  t_touched.clear();
+  const int rc = launch_row_op_analyzed_body<OP>(y, x, idx, n, off, row_size, limit, s);
+  for (auto &p : t_touched) p->mark_used(s);  // after the call's last launch
+  t_touched.clear();
+  return rc;
+}
+template <int OP>
+int launch_row_op_analyzed_body(float *y, const float *x, const gp_double_index *idx, size_t n, gp_double_index off,
+                                size_t row_size, size_t limit, hipStream_t s) {
   const size_t W = row_size;
   const size_t tiles = (n + 63) / 64, groups = (tiles + kScanGroupTiles - 1) / kScanGroupTiles;
   keep_pool_memory();
@@ -2405,7 +2505,7 @@ int launch_row_op_analyzed(float *y, const float *x, const gp_double_index *idx,
                                  : &index_verify_kernel<2>;
     hipLaunchKernelGGL(verify, dim3((unsigned)grid), dim3(kBlock), 0, s, idx, cached->copy_ptr(),
                        static_cast<const uint32_t *>(cached->compact->p), n, cached->base0_word(), word,
-                       cached->changed->p, gen, cached->dev_broken_word());
+                       cached->changed->p, gen, cached->dev_broken_word(), cached->unsound_word());
     GP_HIP_TRY(hipGetLastError());
     // dense runs only if unchanged; one row launch for both outcomes: the
     // sorted residual if unchanged, else every row of the call in op order
@@ -2641,6 +2741,7 @@ int gp_unplanned_cache_entries(size_t *entries, size_t *bytes) {
 }
 
 int gp_set_unplanned_cache_bytes(size_t max_bytes) {
+  reap_graves();
   g_plan_cache_bytes.store(max_bytes, std::memory_order_relaxed);
   std::vector<std::shared_ptr<CachedPlan>> evicted;  // freed outside the lock
   {
@@ -2992,16 +3093,21 @@ constexpr size_t kIpcBlock = 2u << 20;
 constexpr size_t kIpcTagBytes = 256;  // the tag's slot at the end of the allocation
 
 static std::mutex g_ipc_prime_mu;
-static bool g_ipc_primed[kMaxDevices];  // g_ipc_prime_mu
+static bool g_ipc_primed[kMaxDevices];   // g_ipc_prime_mu
+static void *g_ipc_primer[kMaxDevices];  // g_ipc_prime_mu: kept for the process's lifetime
 
 int gp_malloc_device_shared(void **ptr, size_t bytes) {
   if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
   *ptr = nullptr;
   if (bytes == 0) return GP_OK;
   // Before a device's first shareable buffer: one throwaway export, so no
-  // real buffer is the process's first export (or older than it) -- the
-  // buffers the probe saw fail (not yet validated on its own: that run's box
-  // was lost)
+  // real buffer is the process's first export -- the buffer the probe saw
+  // fail.  The throwaway stays allocated for the process's lifetime, as in the
+  // probe's "primed" scenario (scripts/probes/ipc_probe.py): freed, its range
+  // could go to the next real buffer, the freed-and-reused case that fails
+  // too.  A precaution; what guarantees no wrong rows is the
+  // tag check, and a refused export or a failed mapping now costs a resend
+  // over the socket, not the job (libgeeps' NACKs, wire.hpp).
   int dev = 0;
   GP_HIP_TRY(hipGetDevice(&dev));
   if (dev >= 0 && dev < kMaxDevices) {
@@ -3012,7 +3118,7 @@ int gp_malloc_device_shared(void **ptr, size_t bytes) {
       if (hipMalloc(&d, kIpcBlock) == hipSuccess) {
         hipIpcMemHandle_t h;
         (void)hipIpcGetMemHandle(&h, d);
-        (void)hipFree(d);
+        g_ipc_primer[dev] = d;
       }
       (void)hipGetLastError();  // a refused throwaway export is expected, not this call's error
     }

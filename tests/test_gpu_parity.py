@@ -951,6 +951,91 @@ def test_unplanned_steady_state_does_not_wait_for_the_device(analyzed, dev):
         assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), changed
 
 
+def test_unplanned_unsound_map_stays_unsound_for_queued_calls(analyzed, dev):
+    """an inverse map found unsound at its build (here a
+    source row at or above 2^32, which the map's 4-B field would cut) must not
+    be walked by a call queued right behind the build, before the host can
+    see the finding.  The build's kernels set a sticky device word that every
+    later call's index check reads.  Two calls back to back with no sync, then
+    a third after one: all bit-exact against the oracle (the far source rows
+    mapped to a compact host copy for it).  x spans 2^32 + 64 rows of 4 floats
+    (64 GiB of HBM, mostly never touched)."""
+    from geeps_amd import native, rowops
+    rng = np.random.default_rng(23)
+    W, n, far = 4, 4 << 20, 64
+    src = np.arange(n, dtype=np.int64)
+    picks = rng.choice(n, far, replace=False)
+    src[picks] = (1 << 32) + np.arange(far)
+    idx = np.stack([src, rng.permutation(n)], 1).astype(np.int64)
+    x_near = rng.standard_normal(n * W).astype(np.float32)
+    x_far = rng.standard_normal(far * W).astype(np.float32)
+    y = rng.standard_normal(n * W).astype(np.float32)
+    # the oracle on a compact x: far row 2^32 + j -> row n + j
+    compact = idx.copy()
+    compact[picks, 0] = n + np.arange(far)
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, np.concatenate([x_near, x_far]), compact, (0, 0), W)
+    tx = torch.empty(((1 << 32) + far) * W, dtype=torch.float32, device=dev)
+    tx[:n * W].copy_(torch.from_numpy(x_near))
+    tx[(1 << 32) * W:].copy_(torch.from_numpy(x_far))
+    ti = torch.from_numpy(idx).to(dev)
+    ys = [T(y, dev) for _ in range(3)]
+    torch.cuda.synchronize()
+    s0 = native.unplanned_stats()
+    rowops.add_rows_from_double_index_gpu(ys[0], tx, ti, n, (0, 0), W, validate=False)  # builds the map
+    rowops.add_rows_from_double_index_gpu(ys[1], tx, ti, n, (0, 0), W, validate=False)  # queued behind it
+    torch.cuda.synchronize()
+    rowops.add_rows_from_double_index_gpu(ys[2], tx, ti, n, (0, 0), W, validate=False)
+    torch.cuda.synchronize()
+    d = {k: v - s0[k] for k, v in native.unplanned_stats().items()}
+    for call, ty in enumerate(ys):
+        assert np.array_equal(bits(ty.cpu().numpy()), bits(e)), call
+    assert d["inverse_plans"] >= 1, d
+    del tx, ys
+    torch.cuda.empty_cache()
+
+
+def test_unplanned_plan_drop_does_not_wait_for_other_streams(analyzed, dev):
+    """dropping a cached plan (an index refilled in place at
+    the same pointer, or an eviction) retires its buffers in stream order
+    behind the calls that used them; round 4 synchronised the whole device,
+    stalling every other stream of the process (libgeeps' server and reader
+    streams).  A call that drops a stale plan must return while another
+    stream is still busy with ~0.1 s of work; results stay exact."""
+    from geeps_amd import native, rowops
+    if not hasattr(torch.cuda, "_sleep"):
+        pytest.skip("torch.cuda._sleep unavailable")
+    rng = np.random.default_rng(31)
+    W, n = 128, 40000
+    x = rng.standard_normal(n * W).astype(np.float32)
+    y = rng.standard_normal(n * W).astype(np.float32)
+    idx = np.stack([np.arange(n), rng.permutation(n)], 1).astype(np.int64)
+    idx2 = idx.copy()
+    idx2[[5, 17], 1] = idx2[[17, 5], 1]
+    tx, ti = T(x, dev), torch.from_numpy(idx).to(dev)
+    for _ in range(3):  # planned, steady
+        rowops.add_rows_from_double_index_gpu(T(y, dev), tx, ti, n, (0, 0), W, validate=False)
+    ti.copy_(torch.from_numpy(idx2).to(dev))  # refilled in place
+    rowops.add_rows_from_double_index_gpu(T(y, dev), tx, ti, n, (0, 0), W, validate=False)  # finds the change
+    torch.cuda.synchronize()
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx2, (0, 0), W)
+    ty = T(y, dev)
+    side, mine = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    s0 = native.unplanned_stats()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(200_000_000)  # ~0.1 s on another stream
+    with torch.cuda.stream(mine):
+        rowops.add_rows_from_double_index_gpu(ty, tx, ti, n, (0, 0), W, validate=False)  # drops the stale plan
+    busy = not side.query()
+    torch.cuda.synchronize()
+    d = {k: v - s0[k] for k, v in native.unplanned_stats().items()}
+    assert d["stale_drops"] == 1, d
+    assert busy, "dropping the stale plan waited for another stream"
+    assert np.array_equal(bits(ty.cpu().numpy()), bits(e))
+
+
 @pytest.mark.parametrize("kind", ["identity", "permuted", "mixed"])
 @pytest.mark.parametrize("W,limit_frac,off", [(128, None, (0, 0)), (64, None, (5, 3)),
                                                (128, 0.83, (0, 0)), (1024, None, (0, 2)),

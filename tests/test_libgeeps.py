@@ -395,6 +395,39 @@ def test_peer_refresh_staged_into_local_cache(dev, P, slack, channels, updates):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fault,P,slack,extra", [
+    ("tag", 2, 0, {}), ("tag", 3, 1, {}), ("refuse", 2, 0, {}), ("refuse", 3, 1, {}),
+    ("tag", 2, 1, {"GEEPS_STAGE_PEER_REFRESH": "1", "GEEPS_STAGE_PEER_UPDATES": "1"}),
+    ("refuse", 2, 0, {"GEEPS_STAGE_PEER_REFRESH": "1"}),
+])
+def test_ipc_failure_costs_a_resend_not_the_job(dev, fault, P, slack, extra):
+    """an IPC export the runtime refuses, or a mapping that
+    fails (the runtime's error, or a mapping without the exporter's tag: a
+    mis-mapped buffer), no longer aborts the job.  GEEPS_TEST_IPC_FAULT makes
+    every process's first oplog export and first master-version export fail:
+      tag     the handle's tag is corrupted: the importer's check refuses the
+              mapping and NACKs (kCmdOplogNack / kCmdVersionNack), the exporter
+              resends those rows over the socket, and the oplog buffer is
+              replaced before its next use;
+      refuse  the export itself fails: those rows go by socket at once.
+    Every Read is checked exactly (SSP bounds at slack > 0); the counters show
+    each fault was hit and recovered."""
+    outs = _run_app(P, rows=900, clocks=8, slack=slack, channels=1, rmw=0, transport="ipc",
+                    extra_env=dict({"GEEPS_TEST_IPC_FAULT": fault}, **extra))
+    st = [s["client"] for s in _stats(outs)]
+    print(fault, [(c["nr_ipc_export_refused"], c["nr_ipc_nack_sent"], c["nr_ipc_resent"]) for c in st])
+    if fault == "tag":
+        # each process's first oplog export and first version export were
+        # NACKed by their importer and resent by it
+        assert sum(c["nr_ipc_nack_sent"] for c in st) == 2 * P
+        assert sum(c["nr_ipc_resent"] for c in st) == 2 * P
+        assert all(c["nr_ipc_export_refused"] == 0 for c in st)
+    else:
+        assert all(c["nr_ipc_export_refused"] == 2 for c in st)
+        assert all(c["nr_ipc_nack_sent"] == 0 for c in st)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("P,mode,direct", [(1, "float", "1"), (1, "float", "0"), (2, "int", "1"),
                                            (3, "int", "0")])
 def test_direct_oplog(dev, P, mode, direct):
