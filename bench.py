@@ -908,56 +908,70 @@ def libgeeps_leg(rows, W, clocks=10, warmup=5, procs=(1, 2)):
     out = {"app": "scripts/apps/geeps_clock_bench.cpp", "rows": rd_rows, "row_size": 128,
            "table_bytes": rd_rows * 512, "transport": "ipc (same node)", "clocks": clocks,
            "warmup": warmup}
+
+    def leg(key, fn):
+        # each run on its own: one that raises is recorded under its key and
+        # the runs before it keep their numbers
+        try:
+            out[key] = fn()
+        except Exception as exc:
+            out[key] = {"error": f"{type(exc).__name__}: {str(exc)[-500:]}"}
+
+    def run(P, env=None, rows=rd_rows, slack=0, transport="ipc", info=None, keep=()):
+        r = mod.run(P, rows, clocks, warmup, slack, transport, timeout=120, extra_env=env)
+        d = {"workers": P, "ms_per_clock": r["ms_per_clock_max"], "delta_GBps": r["aggregate_delta_GBps"]}
+        if rows != rd_rows or slack:
+            d.update(rows=rows, slack=slack)
+        d.update(info or {})
+        for k in keep:  # a result field, or (field, key to report it under)
+            src, dst = (k, k) if isinstance(k, str) else k
+            d[dst] = r.get(src)
+        return d
+
     for P in procs:
-        r = mod.run(P, rd_rows, clocks, warmup, 0, "ipc", timeout=120)
-        out[f"p{P}"] = {"workers": P, "ms_per_clock": r["ms_per_clock_max"],
-                        "delta_GBps": r["aggregate_delta_GBps"],
-                        "ms_per_clock_each": r["ms_per_clock"]}
+        leg(f"p{P}", lambda P=P: run(P, keep=(("ms_per_clock", "ms_per_clock_each"),)))
     # the same clock with the direct oplog off: Update copies the app's rows
     # into the oplog (the fused init), as before round 3
-    r = mod.run(1, rd_rows, clocks, warmup, 0, "ipc", timeout=120, extra_env={"GEEPS_DIRECT_OPLOG": "0"})
-    out["p1_copy"] = {"workers": 1, "ms_per_clock": r["ms_per_clock_max"],
-                      "delta_GBps": r["aggregate_delta_GBps"], "direct_oplog": False}
+    leg("p1_copy", lambda: run(1, {"GEEPS_DIRECT_OPLOG": "0"}, info={"direct_oplog": False}))
     # the same clock with direct reads (GEEPS_DIRECT_READ=1, opt-in: the app
     # treats Read buffers as read-only): Read hands out the in-place master
     # version's rows, so the gather's copy goes too.  A direct Read must lie in
     # one server's shard: at P = 2 the app declares one Read op per shard
     # (CLOCK_BENCH_READ_PER_SHARD=1, as per-blob ops mostly fall in one shard)
     direct = {"GEEPS_DIRECT_READ": "1", "CLOCK_BENCH_READ_PER_SHARD": "1"}
+    dinfo = {"direct_read": True, "read_ops": "one per server shard"}
     for P in procs:
-        r = mod.run(P, rd_rows, clocks, warmup, 0, "ipc", timeout=120, extra_env=direct)
-        out[f"p{P}_direct_read"] = {"workers": P, "ms_per_clock": r["ms_per_clock_max"],
-                                    "delta_GBps": r["aggregate_delta_GBps"], "direct_read": True,
-                                    "read_ops": "one per server shard"}
+        leg(f"p{P}_direct_read", lambda P=P: run(P, direct, info=dinfo))
     # configs[4]'s shape: the AlexNet-sized table (60,965,224 parameters in
     # 476,292 RowData rows, blobs padded to whole rows) clocked by 8 worker
     # processes (8 server shards) sharing this GPU, staleness bound 1
-    r = mod.run(8, ALEXNET_ROWS, clocks, warmup, 1, "ipc", timeout=120)
-    out["p8_alexnet_slack1"] = {"workers": 8, "rows": ALEXNET_ROWS, "slack": 1,
-                                "ms_per_clock": r["ms_per_clock_max"],
-                                "delta_GBps": r["aggregate_delta_GBps"],
-                                "note": "one table-wide op per clock; the per-blob op sequence is "
-                                        "tests/test_libgeeps.py's configs[4] test"}
-    r = mod.run(8, ALEXNET_ROWS, clocks, warmup, 1, "ipc", timeout=120, extra_env=direct)
-    out["p8_alexnet_slack1_direct_read"] = {"workers": 8, "rows": ALEXNET_ROWS, "slack": 1,
-                                            "ms_per_clock": r["ms_per_clock_max"],
-                                            "delta_GBps": r["aggregate_delta_GBps"], "direct_read": True,
-                                            "read_ops": "one per server shard"}
+    leg("p8_alexnet_slack1", lambda: run(8, None, ALEXNET_ROWS, 1, info={
+        "note": "one table-wide op per clock; the per-blob op sequence is tests/test_libgeeps.py's "
+                "configs[4] test"}))
+    leg("p8_alexnet_slack1_direct_read", lambda: run(8, direct, ALEXNET_ROWS, 1, info=dinfo))
     # SURVEY §8(f)'s next rows, measured: read-my-writes (f#4: every refresh
     # re-applies the worker's own unpushed oplog, clientlib-data.cpp:132-150)
     # at configs[1]'s 2 processes, and the socket path other nodes take (f#2:
     # D2H of the oplog slice, ZMTP frames over loopback TCP, the server's H2D
     # and sum, the refresh back the same way) on the AlexNet-sized table
-    r = mod.run(2, rd_rows, clocks, warmup, 0, "ipc", timeout=120, extra_env={"CLOCK_BENCH_RMW": "1"})
-    out["p2_read_my_writes"] = {"workers": 2, "ms_per_clock": r["ms_per_clock_max"],
-                                "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],
-                                "read_my_writes": True}
-    r = mod.run(2, ALEXNET_ROWS, clocks, warmup, 0, "tcp", timeout=120)
-    moved = 2 * 2 * (ALEXNET_ROWS // 2) * 512  # each worker: its slice out, the peer shard back
-    out["p2_alexnet_tcp"] = {"workers": 2, "rows": ALEXNET_ROWS, "ms_per_clock": r["ms_per_clock_max"],
-                             "delta_GBps": r["aggregate_delta_GBps"], "read_ok": r["read_ok"],
-                             "socket_GBps": round(moved / (r["ms_per_clock_max"] * 1e-3) / 1e9, 2),
-                             "transport": "ZMTP/3.0 over loopback TCP (the other-node path)"}
+    leg("p2_read_my_writes", lambda: run(2, {"CLOCK_BENCH_RMW": "1"}, info={"read_my_writes": True},
+                                         keep=("read_ok",)))
+
+    def tcp():
+        d = run(2, None, ALEXNET_ROWS, 0, "tcp", keep=("read_ok",),
+                info={"transport": "ZMTP/3.0 over loopback TCP (the other-node path)"})
+        moved = 2 * 2 * (ALEXNET_ROWS // 2) * 512  # each worker: its slice out, the peer shard back
+        d["socket_GBps"] = round(moved / (d["ms_per_clock"] * 1e-3) / 1e9, 2)
+        return d
+    leg("p2_alexnet_tcp", tcp)
+    # a4, the host tier: a gpu_memory_capacity that holds half of the
+    # AlexNet-sized table's rows, so the other half lives in host memory
+    # (vi_decide_param_cache); its Updates go device to host and are added on
+    # the CPU, its pushes and refreshes carry [host rows][HBM rows], its Reads
+    # gather on the host and copy up (clientlib-data.cpp:153-189, 280-344,
+    # 398-434); 2 processes
+    leg("p2_alexnet_host_tier", lambda: run(2, {"CLOCK_BENCH_HOST_TIER_FRAC": "0.5"}, ALEXNET_ROWS, 0,
+                                            info={"host_tier_frac": 0.5}, keep=("read_ok", "rows_host_tier")))
     return out
 
 

@@ -64,7 +64,8 @@ std::string ClientStats::to_json() const {
     << ", \"nr_read_direct\": " << nr_read_direct << ", \"nr_read_pin_deferred\": " << nr_read_pin_deferred
     << ", \"nr_read_direct_capped\": " << nr_read_direct_capped
     << ", \"nr_ipc_export_refused\": " << nr_ipc_export_refused << ", \"nr_ipc_nack_sent\": " << nr_ipc_nack_sent
-    << ", \"nr_ipc_resent\": " << nr_ipc_resent
+    << ", \"nr_ipc_resent\": " << nr_ipc_resent << ", \"rows_host_tier\": " << rows_host_tier
+    << ", \"nr_read_host\": " << nr_read_host << ", \"nr_update_host\": " << nr_update_host
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -702,7 +703,8 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
             const std::vector<RecvPart> v = f.view();
             GP_CHECK_EQ(v[2].size, rv.num_rows * kRowBytes);
             ack_all(h.table_id, recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
-                                               static_cast<const float *>(v[2].data), rv.num_rows, -1));
+                                               static_cast<const float *>(v[2].data), rv.num_rows, -1, nullptr,
+                                               static_cast<const float *>(v[2].data)));
             break;
           }
           held.push_back(std::move(f));
@@ -735,7 +737,7 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
     ack_all(h.table_id,
             recv_row_batch(ch.id, h.server_id, h.table_id, h.data_age, h.self_clock,
                            n && in_landing ? landing.data() : static_cast<const float *>(parts[2].data), n, -1,
-                           n && in_landing ? &landing : nullptr));
+                           n && in_landing ? &landing : nullptr, static_cast<const float *>(parts[2].data)));
     return true;
   };
   for (;;) {
@@ -911,6 +913,77 @@ uint32_t ClientLib::channel_of(uint32_t table_id, row_idx_t row) const {
   return (uint32_t)(row / rows_per_channel_[table_id]);  // clientlib.cpp:216-219
 }
 
+// vi_create_local_storage (clientlib-viter.cpp:160-490), reduced to what it
+// leaves used of ngr_capacity before the param cache: the local key batches
+// that are fetched or kept go to GPU memory when they fit beside a thread
+// cache of twice the peak rows in use at once (the op buffers of READ /
+// PRE_WRITE ops, counted from an op to its post-step; GPU local storage is not
+// counted in the peak), and the thread cache takes twice that peak.  libgeeps
+// keeps every local batch in HBM (no CPU local storage): when the fetched /
+// kept batches do not fit, the reference would place some in CPU memory,
+// which it allows below mm_warning_level 2 -- here that is a warning.
+size_t ClientLib::reference_ngr_used(size_t ngr_capacity) {
+  struct Batch {
+    size_t rows = 0;
+    bool fetchkeep = false;
+  };
+  std::map<std::pair<uint64_t, row_idx_t>, Batch> local;  // (table, first row)
+  auto key_of = [](const OpInfo &op) { return std::make_pair((uint64_t)op.table, op.rows[0]); };
+  for (auto &op : opseq_) {
+    if (op.local && op.type == OpInfo::READ && !op.rows.empty()) {
+      Batch &b = local[key_of(op)];
+      b.rows = op.rows.size();
+      b.fetchkeep = b.fetchkeep || op.fetch;
+    }
+    if (op.type == OpInfo::POST_READ && op.local && op.keep) {
+      const OpInfo &pre = opseq_[op.prestep_handle];
+      if (!pre.rows.empty()) local[key_of(pre)].fetchkeep = true;
+    }
+  }
+  size_t fetchkeep_rows = 0;
+  for (auto &kv : local) fetchkeep_rows += kv.second.fetchkeep ? kv.second.rows : 0;
+  // the peak of op rows in use at once, local batches in GPU memory excluded
+  auto peak_rows = [&](bool fetchkeep_in_gpu) {
+    size_t now = 0, peak = 0;
+    auto counted = [&](const OpInfo &op) {
+      return !(op.local && !op.rows.empty() && fetchkeep_in_gpu && local[key_of(op)].fetchkeep);
+    };
+    for (auto &op : opseq_) {
+      if ((op.type == OpInfo::READ || op.type == OpInfo::PRE_WRITE) && counted(op)) {
+        now += op.rows.size();
+        peak = std::max(peak, now);
+      } else if (op.type == OpInfo::POST_READ || op.type == OpInfo::WRITE) {
+        const OpInfo &pre = opseq_[op.prestep_handle];
+        if (counted(pre)) now -= std::min(now, pre.rows.size());
+      }
+    }
+    return peak;
+  };
+  const size_t peak0 = peak_rows(false);
+  GP_CHECK_MSG(ngr_capacity / 2 >= peak0, "gpu_memory_capacity holds " << ngr_capacity << " RowData rows, "
+               "less than twice the peak " << peak0 << " rows of ops in use at once (the thread cache, "
+               "clientlib-viter.cpp:338)");
+  size_t used = fetchkeep_rows, peak = peak0;
+  if (fetchkeep_rows + 2 * peak0 <= ngr_capacity) {
+    peak = peak_rows(true);
+  } else if (fetchkeep_rows) {
+    GP_CHECK_MSG(config_.mm_warning_level < 2,
+                 "local storage (" << fetchkeep_rows << " rows fetched or kept) does not fit gpu_memory_capacity "
+                 "beside the thread cache, and mm_warning_level 2 keeps all local data in GPU memory");
+    std::cerr << "libgeeps WARNING: local storage past gpu_memory_capacity stays in HBM (no CPU local "
+                 "storage tier)\n";
+  }
+  size_t thread_cache = 2 * peak;
+  const size_t left = ngr_capacity > used ? ngr_capacity - used : 0;
+  if (thread_cache > left) {
+    GP_CHECK_MSG(config_.mm_warning_level < 1, "not enough space for double buffering (thread cache of "
+                 << thread_cache << " rows, " << left << " left; clientlib-viter.cpp:482-487)");
+    std::cerr << "*** WARNING: not enough space for double buffering\n";
+    thread_cache = left;
+  }
+  return used + thread_cache;
+}
+
 void ClientLib::finish_virtual_iteration() {
   GP_CHECK(!finished_vi_);
   finished_vi_ = true;
@@ -947,45 +1020,98 @@ void ClientLib::finish_virtual_iteration() {
   }
   for (uint32_t t = 0; t < T; ++t) GP_CHECK_MSG(seen[t], "No one writes table " << t);
 
-  // Param cache rows in first-access order per table (vi_decide_param_cache).
-  std::vector<std::vector<row_idx_t>> keys(T);
-  std::vector<std::unordered_set<row_idx_t>> known(T);
-  for (auto &op : opseq_) {
-    if (op.local || (op.type != OpInfo::READ && op.type != OpInfo::PRE_WRITE) || op.rows.empty())
-      continue;
-    auto &kn = known[op.table_id];
-    const bool fresh = !kn.count(op.rows[0]);
-    for (row_idx_t r : op.rows) {
-      if (fresh) {
-        GP_CHECK_MSG(!kn.count(r), "row " << r << " of a new key batch already cached");
-        kn.insert(r);
-        keys[op.table_id].push_back(r);
-      } else {
-        GP_CHECK_MSG(kn.count(r), "row " << r << " mixes new and cached keys in one op");
-      }
-    }
-  }
-  rows_per_channel_.assign(T, 1);
-  for (uint32_t t = 0; t < T; ++t)
-    rows_per_channel_[t] = std::max<size_t>(1, (keys[t].size() + num_channels_ - 1) / num_channels_);
-
   // Oplog entries per cache row: 1, or slack + 1 with read-my-writes
-  // (vi_decide_param_cache, clientlib-viter.cpp:507-517); used for planning only,
-  // the pool grows on demand.
+  // (vi_decide_param_cache, clientlib-viter.cpp:507-517); used for planning
+  // (and the placement below), the pool grows on demand.
   iter_t max_slack = 0;
   for (auto &op : opseq_)
     if (!op.local && op.type == OpInfo::READ) max_slack = std::max(max_slack, op.slack);
   const size_t entries = config_.read_my_writes ? (size_t)max_slack + 1 : 1;
+
+  // Param cache rows in first-access order per table, each new key batch
+  // placed as vi_decide_param_cache places it (clientlib-viter.cpp:520-568):
+  // in HBM while (HBM rows + batch) x (1 + oplog entries) fits what
+  // gpu_memory_capacity leaves after local storage and the thread cache
+  // (counted in RowData rows, ngr_capacity = capacity / sizeof(RowData),
+  // :179), else in the host tier.  A later op's keys keep their batch's place.
+  const size_t ngr_capacity = config_.gpu_memory_capacity / sizeof(RowData);
+  const size_t ngr_used = reference_ngr_used(ngr_capacity);
+  const size_t ngr_param = ngr_capacity > ngr_used ? ngr_capacity - ngr_used : 0;
+  const size_t entries_per_row = 1 + entries;
+  size_t gpu_rows = 0;
+  std::vector<std::vector<row_idx_t>> keys(T);
+  std::vector<std::unordered_map<row_idx_t, bool>> on_gpu(T);
+  for (auto &op : opseq_) {
+    if (op.local || (op.type != OpInfo::READ && op.type != OpInfo::PRE_WRITE) || op.rows.empty())
+      continue;
+    auto &kn = on_gpu[op.table_id];
+    auto first = kn.find(op.rows[0]);
+    if (first == kn.end()) {
+      // a new key batch: (gpu rows + batch) x entries_per_row <= capacity left
+      const size_t n = op.rows.size();
+      const bool gpu = n <= ngr_param / entries_per_row && gpu_rows <= ngr_param / entries_per_row - n;
+      if (!gpu)
+        GP_CHECK_MSG(config_.mm_warning_level < 3,
+                     "a key batch of " << n << " rows of table " << op.table_id << " does not fit "
+                     "gpu_memory_capacity (" << config_.gpu_memory_capacity << " B: " << ngr_capacity
+                     << " RowData rows, " << ngr_used << " for local storage and the thread cache, "
+                     << gpu_rows << " x " << entries_per_row << " for the param cache so far), and "
+                     "mm_warning_level 3 keeps all parameter cache in GPU memory "
+                     "(clientlib-viter.cpp:551-552)");
+      for (row_idx_t r : op.rows) {
+        GP_CHECK_MSG(!kn.count(r), "row " << r << " of a new key batch already cached");
+        kn[r] = gpu;
+        keys[op.table_id].push_back(r);
+      }
+      if (gpu) gpu_rows += n;
+      op.cpu = !gpu;
+    } else {
+      op.cpu = !first->second;
+      for (row_idx_t r : op.rows) {
+        auto it = kn.find(r);
+        GP_CHECK_MSG(it != kn.end(), "row " << r << " mixes new and cached keys in one op");
+        GP_CHECK_MSG(it->second == first->second,
+                     "row " << r << " of an op lies in another param-cache tier than the op's first row");
+      }
+    }
+  }
+  // Post-steps take their pre-step's placement.
+  for (auto &op : opseq_)
+    if ((op.type == OpInfo::WRITE || op.type == OpInfo::POST_READ) && !op.local)
+      op.cpu = opseq_[op.prestep_handle].cpu;
+  rows_per_channel_.assign(T, 1);
+  for (uint32_t t = 0; t < T; ++t)
+    rows_per_channel_[t] = std::max<size_t>(1, (keys[t].size() + num_channels_ - 1) / num_channels_);
 
   size_t planned = 0;
   for (auto &chp : channels_) {
     Channel &ch = *chp;
     for (uint32_t t = 0; t < T; ++t) {
       ParamCache &pc = ch.tables[t];
+      HostTier &cpu = pc.cpu;
+      // each tier's rows in first-access order (vi_process_channel_table_
+      // finalize runs once per tier over its key list, clientlib-viter.cpp:624-662)
       for (row_idx_t r : keys[t]) {
         if (channel_of(t, r) != ch.id) continue;
-        pc.index[r] = pc.num_rows++;
-        pc.row_keys->emplace_back(t, r);
+        if (on_gpu[t].at(r)) {
+          pc.index[r] = pc.num_rows++;
+          pc.row_keys->emplace_back(t, r);
+        } else {
+          cpu.index[r] = cpu.num_rows++;
+          cpu.row_keys.emplace_back(t, r);
+        }
+      }
+      if (cpu.num_rows) {
+        cpu.data.assign(cpu.num_rows * ROW_DATA_SIZE, 0.0f);  // zerofy_data_cpu
+        cpu.server_row_start.resize(num_processes_);
+        cpu.server_num_rows.resize(num_processes_);
+        const size_t div = cpu.num_rows / num_processes_, res = cpu.num_rows % num_processes_;
+        for (size_t i = 0; i < num_processes_; ++i) {
+          cpu.server_row_start[i] = div * i + std::min(i, res);
+          cpu.server_num_rows[i] = div + (i < res ? 1 : 0);
+        }
+        std::lock_guard<std::mutex> lk(stats_mu_);
+        stats_.rows_host_tier += cpu.num_rows;
       }
       pc.server_row_start.resize(num_processes_);
       pc.server_num_rows.resize(num_processes_);
@@ -1046,13 +1172,30 @@ void ClientLib::finish_virtual_iteration() {
       pc.deferred.assign(num_processes_, {});
       pc.read_events.assign(num_processes_, {});
       pc.server_clock.assign(num_processes_, INITIAL_DATA_AGE);
+      if (cpu.num_rows) {
+        // every server's frame keys: its host-tier keys, then its HBM-tier keys
+        // (clientlib-data.cpp:487-509: the CPU part first)
+        pc.frame_keys.resize(num_processes_);
+        for (uint32_t s = 0; s < num_processes_; ++s) {
+          auto k = std::make_shared<std::vector<RowKey>>();
+          k->insert(k->end(), cpu.row_keys.begin() + cpu.server_row_start[s],
+                    cpu.row_keys.begin() + cpu.server_row_start[s] + cpu.server_num_rows[s]);
+          k->insert(k->end(), pc.row_keys->begin() + pc.server_row_start[s],
+                    pc.row_keys->begin() + pc.server_row_start[s] + pc.server_num_rows[s]);
+          pc.frame_keys[s] = k;
+        }
+        // the server stages every batch with a host part (one bucket each)
+        planned += (pc.server_num_rows[process_id_] + cpu.server_num_rows[process_id_]) * kRowBytes *
+                   TabletServer::kMaxPendingBuckets;
+      }
       rebuild_segments(pc);
     }
     ch.stream->sync();
   }
   for (auto &chp : channels_)
     for (uint32_t t = 0; t < T; ++t)
-      GP_CHECK_MSG(chp->tables[t].num_rows <= rows_per_channel_[t] || num_channels_ == 1,
+      GP_CHECK_MSG(chp->tables[t].num_rows + chp->tables[t].cpu.num_rows <= rows_per_channel_[t] ||
+                       num_channels_ == 1,
                    "channel " << chp->id << " of table " << t << " holds rows past its range");
 
   // Op buffers, DoubleIndex, local storage.
@@ -1071,6 +1214,8 @@ void ClientLib::finish_virtual_iteration() {
     op.buffer.resize(std::max<size_t>(1, op.rows.size()) * ROW_DATA_SIZE);
     GP_CALL(gp_zero(op.buffer.data(), op.buffer.size(), channels_[0]->stream->get()));
     planned += op.buffer.bytes();
+    if (op.cpu && cpu_buffer_.size() < op.rows.size() * ROW_DATA_SIZE)
+      cpu_buffer_.resize(op.rows.size() * ROW_DATA_SIZE);  // max_nr_each_access rows (clientlib-viter.cpp:444-447)
     // the device DoubleIndex, and an update or read op's row plans (a sorted copy)
     planned += op.rows.size() * sizeof(gp_double_index) *
                (op.type == OpInfo::PRE_WRITE || op.type == OpInfo::READ ? 2 : 1);
@@ -1078,18 +1223,15 @@ void ClientLib::finish_virtual_iteration() {
   }
   GP_CALL(gp_device_synchronize());
   decide_fused_init();
-  if (planned > config_.gpu_memory_capacity) {
-    // The reference places what does not fit in CPU memory and accumulates it
-    // there (update_batch_cpu, clientlib-viter.cpp:492-611; clientlib-data.cpp:
-    // 398-434).  libgeeps has no CPU tier: every row lives in HBM (288 GB per
-    // MI355X), so past the capacity it warns, or fails at mm_warning_level >= 2.
-    std::ostringstream o;
-    o << "planned HBM use " << planned << " B exceeds gpu_memory_capacity "
-      << config_.gpu_memory_capacity
-      << " B; libgeeps keeps every row in HBM (no CPU param-cache tier: the reference's "
-         "CPU placement, clientlib-viter.cpp:492-611, is not built)";
-    GP_CHECK_MSG(config_.mm_warning_level < 2, o.str());
-    std::cerr << "libgeeps WARNING: " << o.str() << "\n";
+  if (planned > config_.gpu_memory_capacity && config_.mm_warning_level >= 1) {
+    // The param cache's rows were placed by the reference's own model above
+    // (rows past the capacity went to the host tier).  What that model does
+    // not count is what libgeeps keeps in HBM beyond it: the tablet server's
+    // master versions and staging buckets (the reference's server is CPU
+    // memory), the op buffers and plans.
+    std::cerr << "libgeeps WARNING: planned HBM use " << planned << " B (param cache, oplogs, op buffers, "
+              << "and this process's tablet-server shards and staging buffers) exceeds gpu_memory_capacity "
+              << config_.gpu_memory_capacity << " B\n";
   }
 }
 
@@ -1117,7 +1259,7 @@ void ClientLib::decide_fused_init() {
       bool ok = pc.num_rows > 0;
       for (size_t i = 0; i < end && ok; ++i) {
         const OpInfo &w = opseq_[i];
-        if (w.type != OpInfo::WRITE || w.local || w.table_id != t) continue;
+        if (w.type != OpInfo::WRITE || w.local || w.table_id != t || w.cpu) continue;  // (host-tier ops: its own oplog)
         const OpInfo &pre = opseq_[w.prestep_handle];
         bool here = false;
         if (pre.num_vals_limit < pre.rows.size() * ROW_DATA_SIZE) ok = false;
@@ -1174,8 +1316,9 @@ void ClientLib::create_double_index(OpInfo &op) {
     const uint32_t c = channel_of(op.table_id, op.rows[j]);
     GP_CHECK_LT(c, num_channels_);
     ParamCache &pc = channels_[c]->tables[op.table_id];
-    auto it = pc.index.find(op.rows[j]);
-    GP_CHECK_MSG(it != pc.index.end(), "row " << op.rows[j] << " not in the param cache");
+    auto &index = op.cpu ? pc.cpu.index : pc.index;  // the op's tier
+    auto it = index.find(op.rows[j]);
+    GP_CHECK_MSG(it != index.end(), "row " << op.rows[j] << " not in the param cache");
     per[c].push_back(gp_double_index{j, it->second});
   }
   std::vector<gp_double_index> flat;
@@ -1206,6 +1349,13 @@ void ClientLib::create_double_index(OpInfo &op) {
   // runs (first-access order makes an op's rows one run per channel) are
   // copied by the phase-separated kernels, which hold their rate on every
   // allocation.
+  if (op.cpu) {
+    // a host-tier op: its index stays in host memory (the reference's
+    // row_index_cpu, clientlib-viter.cpp:853-876); no device index or plans
+    op.host_index = std::move(flat);
+    op.direct_channel = -1;
+    return;
+  }
   if (op.type == OpInfo::PRE_WRITE || op.type == OpInfo::READ) {
     op.direct_channel = -1;
     for (uint32_t c = 0; c < num_channels_; ++c) {
@@ -1258,6 +1408,12 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
   GP_CHECK_MSG(!op.in_use, "Read of handle " << handle << " before its PostRead");
   if (op.local) {
     *buffer = reinterpret_cast<RowData *>(op.local_ptr);
+    op.in_use = true;
+    return true;
+  }
+  if (op.cpu) {
+    read_batch_host(op);
+    *buffer = reinterpret_cast<RowData *>(op.buffer.data());
     op.in_use = true;
     return true;
   }
@@ -1326,6 +1482,94 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
   stats_.read_wait_time += waited;
   stats_.read_time += now_s() - t0;
   return true;
+}
+
+// A host-tier op's Read: per channel, wait for the data age and gather the
+// op's rows from the host cache into the pinned host buffer (read_batch_cpu,
+// assign_rows_to_double_index_cpu: clientlib-data.cpp:280-302); then one
+// host-to-device copy of num_vals_limit floats into the op buffer in HBM
+// (read_row_batch_param_cache, :233-250).
+void ClientLib::read_batch_host(OpInfo &op) {
+  const double t0 = now_s();
+  const iter_t need = iteration_ - op.slack - 1;
+  double waited = 0;
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    ParamCache &pc = ch.tables[op.table_id];
+    std::unique_lock<std::mutex> lk(ch.mu);
+    const double w0 = now_s();
+    while (pc.data_age < need) {
+      if (!ch.cv.wait_for(lk, std::chrono::milliseconds(kWaitWarnMs), [&] { return pc.data_age >= need; }) &&
+          ch.id == 0)
+        std::cerr << "machine " << process_id_ << " wait time out! Need: " << need << " Data age: " << pc.data_age
+                  << std::endl;
+    }
+    waited += now_s() - w0;
+    if (op.ch_size[ch.id])
+      GP_CALL(gp_host_gather_rows(cpu_buffer_.data(), pc.cpu.data.data(), op.host_index.data() + op.ch_start[ch.id],
+                                  op.ch_size[ch.id], gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit));
+  }
+  const size_t vals = std::min(op.num_vals_limit, op.rows.size() * ROW_DATA_SIZE);
+  Channel &ch0 = *channels_[0];
+  if (vals) GP_CALL(gp_memcpy_async(op.buffer.data(), cpu_buffer_.data(), vals * sizeof(float), ch0.stream->get()));
+  ch0.stream->sync();
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nr_read++;
+  stats_.nr_read_host++;
+  stats_.rows_read += op.rows.size();
+  stats_.read_wait_time += waited;
+  stats_.read_time += now_s() - t0;
+}
+
+// A host-tier op's Update: the app's rows (written by its device work on the
+// null stream) come to the pinned host buffer, num_vals_limit floats
+// (update_batch_param_cache, clientlib-data.cpp:309-323); then per channel,
+// under its lock, the clock's host oplog (zeroed when created) += the op's
+// rows through the host DoubleIndex, and with read-my-writes the host cache
+// too (update_batch_cpu, :398-434).
+void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
+  const size_t vals = std::min(pre.num_vals_limit, pre.rows.size() * ROW_DATA_SIZE);
+  Channel &ch0 = *channels_[0];
+  ch0.app_written.record_default();
+  GP_CALL(gp_stream_wait_event(ch0.stream->get(), ch0.app_written.get()));
+  if (vals) GP_CALL(gp_memcpy_async(cpu_buffer_.data(), pre.buffer.data(), vals * sizeof(float), ch0.stream->get()));
+  ch0.stream->sync();
+  for (auto &chp : channels_) {
+    Channel &ch = *chp;
+    std::lock_guard<std::mutex> lk(ch.mu);
+    HostTier &cpu = ch.tables[pre.table_id].cpu;
+    if (cpu.num_rows == 0) continue;
+    auto oplog = get_host_oplog(cpu, clock);
+    const size_t n = pre.ch_size[ch.id];
+    if (!n) continue;
+    const gp_double_index *idx = pre.host_index.data() + pre.ch_start[ch.id];
+    GP_CALL(gp_host_scatter_add_rows(oplog->data(), cpu_buffer_.data(), idx, n, gp_double_index{0, 0},
+                                     ROW_DATA_SIZE, pre.num_vals_limit));
+    if (config_.read_my_writes)
+      GP_CALL(gp_host_scatter_add_rows(cpu.data.data(), cpu_buffer_.data(), idx, n, gp_double_index{0, 0},
+                                       ROW_DATA_SIZE, pre.num_vals_limit));
+  }
+}
+
+// create_oplog_entry + zerofy_data_cpu (clientlib-data.cpp:412-417): a pooled
+// host buffer once nothing (a pending push, the in-process server's bucket)
+// references it.
+std::shared_ptr<std::vector<float>> ClientLib::get_host_oplog(HostTier &cpu, iter_t clock) {
+  auto it = cpu.oplog.find(clock);
+  if (it != cpu.oplog.end()) return it->second;
+  std::shared_ptr<std::vector<float>> buf;
+  for (auto &b : cpu.oplog_pool)
+    if (b.use_count() == 1) {
+      buf = b;
+      break;
+    }
+  if (!buf) {
+    cpu.oplog_pool.push_back(std::make_shared<std::vector<float>>(cpu.num_rows * ROW_DATA_SIZE));
+    buf = cpu.oplog_pool.back();
+  }
+  std::fill(buf->begin(), buf->end(), 0.0f);
+  cpu.oplog[clock] = buf;
+  return buf;
 }
 
 void ClientLib::postread_batch(int handle) {
@@ -1445,7 +1689,9 @@ void ClientLib::update_batch(int handle) {
   GP_CHECK_MSG(pre.in_use, "Update of handle " << handle << " without PreUpdate");
   const double t0 = now_s();
   const iter_t clock = iteration_;
+  if (pre.cpu) update_batch_host(pre, clock);
   for (auto &chp : channels_) {
+    if (pre.cpu) break;
     Channel &ch = *chp;
     const size_t n = pre.ch_size[ch.id];
     std::lock_guard<std::mutex> lk(ch.mu);
@@ -1495,6 +1741,7 @@ void ClientLib::update_batch(int handle) {
     std::lock_guard<std::mutex> lk(stats_mu_);
     stats_.nr_update++;
     if (was_direct) stats_.nr_update_direct++;
+    if (pre.cpu) stats_.nr_update_host++;
     stats_.rows_updated += pre.rows.size();
     stats_.update_time += now_s() - t0;
   }
@@ -1544,9 +1791,33 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
   std::vector<uint8_t> *exported = nullptr;  // app thread only
   std::vector<uint8_t> *keys_sent = nullptr;  // app thread only
   std::vector<uint8_t> *bad = nullptr;        // app thread only
+  // the host tier (empty unless gpu_memory_capacity placed rows there): its
+  // oplog, server partition and the per-server frame keys [host | HBM]
+  std::shared_ptr<std::vector<float>> hoplog;
+  std::vector<size_t> cstarts, ccounts;
+  std::vector<std::shared_ptr<std::vector<RowKey>>> frame_keys;
+  bool tiers = false, zero_filled = false;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[table_id];
+    HostTier &cpu = pc.cpu;
+    tiers = cpu.num_rows > 0;
+    if (tiers) {
+      auto hit = cpu.oplog.find(clock);
+      if (hit != cpu.oplog.end()) hoplog = hit->second;
+      const bool any = hoplog || pc.oplog.count(clock);
+      // a clock's push carries both tiers' rows (the server sums each shard
+      // positionally): a tier no op updated this clock sends zeros
+      if (any && !hoplog) hoplog = get_host_oplog(cpu, clock);
+      if (any && !pc.oplog.count(clock) && pc.num_rows) {
+        get_oplog(pc, clock, ch.stream->get(), /*zero=*/true);
+        zero_filled = true;
+      }
+      cstarts = cpu.server_row_start;
+      ccounts = cpu.server_num_rows;
+      frame_keys = pc.frame_keys;
+      if (hoplog && !config_.read_my_writes) cpu.oplog.erase(clock);  // (the frames keep it alive)
+    }
     if (pc.oplog_bad.size() < pc.oplog_pool.size()) pc.oplog_bad.resize(pc.oplog_pool.size(), 0);
     if (pc.exported.size() < pc.oplog_pool.size())
       pc.exported.resize(pc.oplog_pool.size(), std::vector<uint8_t>(num_processes_, 0));
@@ -1565,7 +1836,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
     counts = pc.server_num_rows;
     keys = pc.row_keys;
     bool ipc_readers = false;  // a same-node server reads its slice from this oplog
-    for (uint32_t s = 0; s < num_processes_; ++s) ipc_readers |= ipc_to(s) && counts[s] > 0;
+    for (uint32_t s = 0; s < num_processes_; ++s) ipc_readers |= ipc_to(s) && counts[s] > 0 && !tiers;
     if (oplog) {
       for (size_t k = 0; k < pc.oplog_pool.size(); ++k)
         if (pc.oplog_pool[k] == oplog) pool_id = k;
@@ -1580,9 +1851,52 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       if (!config_.read_my_writes && !ipc_readers) pc.oplog.erase(it);
     }
   }
+  if (zero_filled) ch.stream->sync();  // (the in-process server reads it on its own stream)
   size_t remote_bytes = 0;
   uint8_t ch_export_handle[kIpcHandleBytes];  // the export made for server s, when first
   for (uint32_t s = 0; s < num_processes_; ++s) {
+    if (tiers && hoplog) {
+      // A table with host-tier rows: every frame is [host rows of s][HBM rows
+      // of s] (push_updates_param_cache, clientlib-data.cpp:487-509).  The
+      // in-process server gets the host part and the oplog slice in place;
+      // every other server an ordinary socket frame (the reference's own
+      // path; same-node IPC carries HBM-only tables).
+      const size_t ca = cstarts[s], cn = ccounts[s], a = starts[s], n = counts[s];
+      if (s == process_id_) {
+        UpdateBatch b;
+        b.client_id = process_id_;
+        b.clock = clock;
+        b.table_id = table_id;
+        b.keys = frame_keys[s]->data();
+        b.keys_owner = frame_keys[s];
+        b.num_rows = cn + n;
+        b.split = cn;
+        b.host_head = hoplog->data() + ca * ROW_DATA_SIZE;
+        b.head_keepalive = hoplog;
+        if (n) {
+          b.device_rows = oplog->data() + a * ROW_DATA_SIZE;
+          b.keepalive = oplog;
+        }
+        ch.server->post_updates(std::move(b));
+        continue;
+      }
+      const size_t floats = (cn + n) * ROW_DATA_SIZE;
+      if (ch.send_buf.size() < floats) ch.send_buf.resize(floats);
+      if (cn) std::memcpy(ch.send_buf.data(), hoplog->data() + ca * ROW_DATA_SIZE, cn * kRowBytes);
+      if (n)
+        GP_CALL(gp_memcpy_async(ch.send_buf.data() + cn * ROW_DATA_SIZE, oplog->data() + a * ROW_DATA_SIZE,
+                                n * kRowBytes, ch.stream->get()));
+      ch.stream->sync();
+      cs_clock_with_updates_batch_msg_t h{};
+      h.cmd = CLOCK_WITH_UPDATES_BATCH;
+      h.client_id = process_id_;
+      h.clock = clock;
+      h.table_id = table_id;
+      send_to_server(ch, s, {Part{&h, sizeof h}, Part{frame_keys[s]->data(), (cn + n) * sizeof(RowKey)},
+                             Part{ch.send_buf.data(), floats * sizeof(float)}});
+      remote_bytes += floats * sizeof(float);
+      continue;
+    }
     if (!oplog) {
       // clock_broadcast: a CLOCK with no updates (encoder-decoder.cpp:85-100).
       if (s == process_id_) {
@@ -1674,6 +1988,8 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
 void ClientLib::reclaim_oplogs(ParamCache &pc, iter_t upto) {
   for (auto it = pc.oplog.begin(); it != pc.oplog.end() && it->first <= upto;)
     it = pc.oplog.erase(it);
+  for (auto it = pc.cpu.oplog.begin(); it != pc.cpu.oplog.end() && it->first <= upto;)
+    it = pc.cpu.oplog.erase(it);
 }
 
 // recv_row_batch + recv_row_batch_gpu + server_clock_cbk
@@ -1681,7 +1997,7 @@ void ClientLib::reclaim_oplogs(ParamCache &pc, iter_t upto) {
 std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
                                            uint32_t table_id, iter_t data_age, iter_t self_clock,
                                            const float *rows, size_t num_rows, int version,
-                                           DeviceArray<float> *landing) {
+                                           DeviceArray<float> *landing, const float *host_rows) {
   const double t0 = now_s();
   Channel &ch = *channels_[channel];
   std::vector<int> released;
@@ -1693,9 +2009,12 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
     ParamCache &pc = ch.tables[table_id];
     GP_CHECK_LT(server_id, num_processes_);
     // An empty reply means the server has seen no updates for the table yet:
-    // the shard is all zeros, as the freshly zeroed cache already is.
-    GP_CHECK_MSG(num_rows == pc.server_num_rows[server_id] || num_rows == 0,
-                 "refresh of " << num_rows << " rows, expected " << pc.server_num_rows[server_id]);
+    // the shard is all zeros, as the freshly zeroed cache already is.  With a
+    // host tier the shard is [its host-tier rows][its HBM-tier rows].
+    HostTier &cpu = pc.cpu;
+    const size_t split = cpu.num_rows ? cpu.server_num_rows[server_id] : 0;
+    GP_CHECK_MSG(num_rows == split + pc.server_num_rows[server_id] || num_rows == 0,
+                 "refresh of " << num_rows << " rows, expected " << split + pc.server_num_rows[server_id]);
     iter_t &age = pc.per_server_data_age[server_id];
     GP_CHECK_MSG(data_age > age, "old or duplicate data received: " << data_age << " vs " << age);
     GP_CHECK_LE(data_age, self_clock);
@@ -1707,6 +2026,31 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
     if (min_clock > pc.server_clock_min) {
       reclaim_oplogs(pc, min_clock);
       pc.server_clock_min = min_clock;
+    }
+    if (num_rows && split) {
+      // recv_row_batch_cpu (clientlib-data.cpp:153-189): the host-tier part
+      // into the host cache -- from the socket frame's host copy, or device to
+      // host from the master version -- then with read-my-writes this
+      // client's own unreflected host oplogs on top, clock by clock.
+      float *dst = cpu.data.data() + cpu.server_row_start[server_id] * ROW_DATA_SIZE;
+      if (host_rows) {
+        std::memcpy(dst, host_rows, split * kRowBytes);
+      } else {
+        GP_CALL(gp_memcpy_async(dst, rows, split * kRowBytes, ch.svc_stream->get()));
+        ch.svc_stream->sync();
+      }
+      if (config_.read_my_writes)
+        for (iter_t c = self_clock + 1, fc = fast_clock_.load(); c <= fc; ++c) {
+          auto it = cpu.oplog.find(c);
+          if (it != cpu.oplog.end())
+            GP_CALL(gp_host_add(split * ROW_DATA_SIZE, dst,
+                                it->second->data() + cpu.server_row_start[server_id] * ROW_DATA_SIZE));
+        }
+      // the rest is the HBM tier's part of the shard
+      rows += split * ROW_DATA_SIZE;
+      if (host_rows) host_rows += split * ROW_DATA_SIZE;
+      num_rows -= split;
+      if (num_rows == 0 && version >= 0) released.push_back(version);  // nothing of it read in place
     }
     bool own_buf = !pc.shard_buf.empty() && pc.shard_buf[server_id].data();
     if (num_rows && !own_buf && pc.data.size() == 0 && !(version >= 0 && !config_.read_my_writes &&

@@ -88,9 +88,35 @@ struct OpInfo {
   DeviceArray<float> buffer;           // READ / PRE_WRITE op buffer
   float *local_ptr = nullptr;          // local READ: GPU-resident storage
   bool in_use = false;
+  // The op's key batch was placed in the host tier (vi_decide_param_cache,
+  // clientlib-viter.cpp:551-566: past gpu_memory_capacity): its DoubleIndex
+  // lives in host memory (id1 = host cache row, channel-major like `index`),
+  // and its rows move through the host buffer (update_batch_cpu /
+  // read_batch_cpu, clientlib-data.cpp:280-302, 398-434).
+  bool cpu = false;
+  std::vector<gp_double_index> host_index;
+};
+
+// The CPU param cache of one (channel, table): the rows of the key batches
+// that vi_decide_param_cache placed in host memory, as the reference keeps them
+// (DataStorage::CPU: plain host memory, clientlib-viter.cpp:651-659), worked on
+// with the reference's CPU twins (gp_host_*).  Each server's shard is [its
+// host-tier rows][its HBM-tier rows], in the server's master and on the wire
+// (clientlib-data.cpp:487-509; the refresh is split back the same way, :59-67).
+struct HostTier {
+  size_t num_rows = 0;
+  std::unordered_map<row_idx_t, size_t> index;  // row id -> host cache row
+  std::vector<RowKey> row_keys;
+  std::vector<float> data;                       // num_rows x 128
+  std::vector<size_t> server_row_start, server_num_rows;
+  std::map<iter_t, std::shared_ptr<std::vector<float>>> oplog;
+  std::vector<std::shared_ptr<std::vector<float>>> oplog_pool;
 };
 
 struct ParamCache {
+  HostTier cpu;  // the host tier's rows (empty unless gpu_memory_capacity pushed some out)
+  // with a host tier: each server's frame keys, [host-tier keys][HBM-tier keys]
+  std::vector<std::shared_ptr<std::vector<RowKey>>> frame_keys;
   std::unordered_map<row_idx_t, size_t> index;  // row id -> cache row
   std::shared_ptr<std::vector<RowKey>> row_keys = std::make_shared<std::vector<RowKey>>();
   size_t num_rows = 0;
@@ -161,6 +187,8 @@ struct ClientStats {
   // socket instead), peers' handles this process could not map (NACKed), and
   // rows this process resent after a peer's NACK
   uint64_t nr_ipc_export_refused = 0, nr_ipc_nack_sent = 0, nr_ipc_resent = 0;
+  // the host tier: param-cache rows placed there, and Reads / Updates of its ops
+  uint64_t rows_host_tier = 0, nr_read_host = 0, nr_update_host = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
 };
@@ -267,9 +295,12 @@ class ClientLib {
   // Returns the master versions this client gives back to the server.
   // `landing` (a reader's own buffer holding `rows`): the cache may swap it
   // for the shard's buffer instead of copying (ParamCache::shard_buf).
+  // `host_rows`: a host copy of `rows` (a socket refresh), else null.  With
+  // a host tier the first rows of the shard are its host-tier rows.
   std::vector<int> recv_row_batch(uint32_t channel, uint32_t server_id, uint32_t table_id,
                                   iter_t data_age, iter_t self_clock, const float *rows,
-                                  size_t num_rows, int version, DeviceArray<float> *landing = nullptr);
+                                  size_t num_rows, int version, DeviceArray<float> *landing = nullptr,
+                                  const float *host_rows = nullptr);
   void rebuild_segments(ParamCache &pc);
   // Returns true if the client holds reply.version after the call.
   bool remote_reply(uint32_t channel, uint32_t client_id, const RowBatchReply &r);
@@ -287,6 +318,13 @@ class ClientLib {
   std::shared_ptr<DeviceArray<float>> get_oplog(ParamCache &pc, iter_t clock, gp_stream s,
                                                 bool zero);
   void decide_fused_init();
+  // The reference's GPU rows in use before the param cache (vi_create_local_
+  // storage, clientlib-viter.cpp:160-490: GPU local storage + a thread cache
+  // of twice the peak op rows), in RowData rows out of ngr_capacity.
+  size_t reference_ngr_used(size_t ngr_capacity);
+  std::shared_ptr<std::vector<float>> get_host_oplog(HostTier &cpu, iter_t clock);
+  void read_batch_host(OpInfo &op);
+  void update_batch_host(OpInfo &pre, iter_t clock);
   void reclaim_oplogs(ParamCache &pc, iter_t upto);
   void start_network();
   void server_accept_loop(Channel &ch, int expected);
@@ -341,6 +379,9 @@ class ClientLib {
   std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)
 
   std::vector<OpInfo> opseq_;
+  // the reference's thread cpu_buffer (mallocHost, clientlib-viter.cpp:444-447):
+  // host-tier ops' rows on their way to / from the op buffer in HBM
+  PinnedArray<float> cpu_buffer_;
   std::map<std::vector<row_idx_t>, std::unique_ptr<DeviceArray<float>>> local_storage_;
   std::vector<size_t> rows_per_channel_;
   std::vector<std::unique_ptr<Channel>> channels_;

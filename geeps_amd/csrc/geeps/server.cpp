@@ -20,14 +20,15 @@ double now_s() {
 }
 
 // How long free_version waits with no release at all before it gives up:
-// GEEPS_VERSION_WAIT_S seconds; unset or 0 = wait forever with the 12-s
-// warnings, as the reference waits for its clients (a paused worker -- a
-// checkpoint, a long evaluation -- must not kill the job).  The
-// tests set a limit, so a stuck reader fails them with the holders matrix.
+// GEEPS_VERSION_WAIT_S seconds, default 1800 (a paused worker -- a
+// checkpoint, a long evaluation -- must not kill the job, ADVICE r03, but a
+// dead or stuck reader must not hang it forever either: it fails with the
+// holders matrix); 0 = no limit, the 12-s warnings only.  Every
+// release restarts the clock.  The tests set 60 s.
 double version_wait_limit_s() {
   static const double limit = [] {
     const char *v = std::getenv("GEEPS_VERSION_WAIT_S");
-    const double d = v ? std::atof(v) : 0.0;
+    const double d = v ? std::atof(v) : 1800.0;
     return d > 0 ? d : 0.0;
   }();
   return limit;
@@ -260,7 +261,24 @@ void TabletServer::update_row_batch(UpdateBatch &b) {
   GP_CHECK_EQ(t.row_count, batch_size);
 
   Pending p;
-  if (b.device_rows && b.stage) {
+  if (b.split) {
+    // Host-tier rows first, then the HBM-tier slice (the in-process client of
+    // a table with a host tier): both into one staging bucket, so the sum
+    // reads one contiguous bucket as for any client.
+    GP_CHECK_LE(b.split, batch_size);
+    const double t0 = now_s();
+    auto stage = stage_buffer(t);
+    GP_CALL(gp_memcpy_async(stage->data(), b.host_head, b.split * ROW_DATA_SIZE * sizeof(float), stream_));
+    if (batch_size > b.split) {
+      GP_CHECK(b.device_rows);
+      GP_CALL(gp_memcpy_async(stage->data() + b.split * ROW_DATA_SIZE, b.device_rows,
+                              (batch_size - b.split) * ROW_DATA_SIZE * sizeof(float), stream_));
+    }
+    GP_CALL(gp_stream_synchronize(stream_));  // the host part is released when `b` dies
+    stats_.stage_time += now_s() - t0;
+    p.rows = stage->data();
+    p.keepalive = stage;
+  } else if (b.device_rows && b.stage) {
     // A same-node peer on another GPU: copy its slice into local HBM now (a
     // peer copy over xGMI on the copy stream, overlapped with whatever else
     // arrives), so the sum streams local HBM only.  apply_pending waits for it.

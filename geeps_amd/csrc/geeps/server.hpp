@@ -84,6 +84,13 @@ struct UpdateBatch {
   bool stage = false;
   std::shared_ptr<void> keepalive;
   std::shared_ptr<PinnedArray<float>> host_rows;
+  // The in-process client's batch of a table with a host tier: its first
+  // `split` rows are host-tier rows at `host_head` (its host oplog, kept alive
+  // by head_keepalive), the other num_rows - split at `device_rows`.  The
+  // server stages the two into one bucket in HBM.
+  size_t split = 0;
+  const float *host_head = nullptr;
+  std::shared_ptr<const void> head_keepalive;
 };
 
 // The refreshed shard, as the server hands it to a client sink.  `device_rows`

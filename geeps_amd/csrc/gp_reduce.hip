@@ -3346,3 +3346,9 @@ int gp_ipc_close_handle(void *device_ptr) {
 }
 
 }  // extern "C"
+
+// The thread's gp_last_error message, for the C-ABI's host-memory functions
+// (gp_host.cpp, another translation unit of the library).
+namespace gp_internal {
+int set_error(int code, const char *msg) { return ::set_error(code, msg); }
+}  // namespace gp_internal

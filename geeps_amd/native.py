@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 12  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 13  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -99,6 +99,9 @@ _SIGNATURES = {
     "gp_bucket_sum_sweep_plan": (_i, [_sz, _i, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
     "gp_bucket_sum_launch_plan": (_i, [_sz, _i, _c.POINTER(SumPlan)]),
     "gp_add": (_i, [_sz, _vp, _vp, _vp, _vp]),
+    "gp_host_scatter_add_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz]),
+    "gp_host_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz]),
+    "gp_host_add": (_i, [_sz, _vp, _vp]),
     "gp_zero": (_i, [_vp, _sz, _vp]),
     "gp_hbm_probe": (_i, [_i, _vp, _sz, _vp]),
     "gp_device_count": (_i, [_c.POINTER(_i)]),

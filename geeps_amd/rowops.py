@@ -446,3 +446,52 @@ def add_row_batch_gpu(rows_y: torch.Tensor, rows_x: torch.Tensor, batch_size: in
 def zerofy_data_gpu(t: torch.Tensor, stream=None) -> None:
     _dev_f32(t, "t")
     check(native.lib().gp_zero(t.data_ptr(), t.numel(), _stream_ptr(stream)), "gp_zero")
+
+
+# -- host-memory rows (the reference's CPU twins; libgeeps' host tier) ------
+def _host_f32(a, name):
+    import numpy as np
+    if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous):
+        raise ValueError(f"{name} must be a C-contiguous float32 numpy array")
+
+
+def _host_index(index):
+    import numpy as np
+    if not (isinstance(index, np.ndarray) and index.dtype in (np.int64, np.uint64) and index.ndim == 2
+            and index.shape[1] == 2 and index.flags.c_contiguous):
+        raise ValueError("index must be a contiguous (n, 2) int64 numpy array")
+
+
+def add_rows_from_double_index_cpu(rows_y, rows_x, index, index_offset=None, row_size=ROW_DATA_SIZE,
+                                   num_vals_limit=None) -> None:
+    """``y[(id1+off1)*W + v] += x[(id0+off0)*W + v]`` in host memory, entries in
+    order (reference row-op-util.hpp:121-139) -- gp_host_scatter_add_rows."""
+    _host_f32(rows_y, "rows_y")
+    _host_f32(rows_x, "rows_x")
+    _host_index(index)
+    limit = (1 << 64) - 1 if num_vals_limit is None else num_vals_limit
+    check(native.lib().gp_host_scatter_add_rows(rows_y.ctypes.data, rows_x.ctypes.data, index.ctypes.data,
+                                                index.shape[0], _as_offset(index_offset), row_size, limit),
+          "gp_host_scatter_add_rows")
+
+
+def assign_rows_to_double_index_cpu(rows_y, rows_x, index, index_offset=None, row_size=ROW_DATA_SIZE,
+                                    num_vals_limit=None) -> None:
+    """``y[(id0+off0)*W + v] = x[(id1+off1)*W + v]`` in host memory (reference
+    row-op-util.hpp:81-99) -- gp_host_gather_rows."""
+    _host_f32(rows_y, "rows_y")
+    _host_f32(rows_x, "rows_x")
+    _host_index(index)
+    limit = (1 << 64) - 1 if num_vals_limit is None else num_vals_limit
+    check(native.lib().gp_host_gather_rows(rows_y.ctypes.data, rows_x.ctypes.data, index.ctypes.data,
+                                           index.shape[0], _as_offset(index_offset), row_size, limit),
+          "gp_host_gather_rows")
+
+
+def add_row_batch_cpu(rows_y, rows_x) -> None:
+    """``y += x`` in host memory (reference add_row_batch, row-op-util.hpp:64-70) -- gp_host_add."""
+    _host_f32(rows_y, "rows_y")
+    _host_f32(rows_x, "rows_x")
+    if rows_x.size < rows_y.size:
+        raise ValueError("rows_x shorter than rows_y")
+    check(native.lib().gp_host_add(rows_y.size, rows_y.ctypes.data, rows_x.ctypes.data), "gp_host_add")

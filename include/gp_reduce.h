@@ -47,7 +47,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 12
+#define GP_ABI_VERSION 13
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -373,6 +373,30 @@ int gp_hbm_probe(int kind, float *buffer, size_t num_vals, gp_stream s);
 /* Zero `num_vals` floats — DataStorage::zerofy_data_gpu
  * (src/common/common-util.hpp:445-456). */
 int gp_zero(float *y, size_t num_vals, gp_stream s);
+
+/* ---------------------------------------------------------------------------
+ * Host-memory row ops: the reference's CPU twins, for rows a GeePS param cache
+ * keeps in host memory.  When `gpu_memory_capacity` cannot hold every row, the
+ * reference places whole key batches in a CPU param cache
+ * (vi_decide_param_cache, src/client/clientlib-viter.cpp:492-611) and runs
+ * these loops there (update_batch_cpu / read_batch_cpu / recv_row_batch_cpu,
+ * src/client/clientlib-data.cpp:153-189, 280-302, 398-434); libgeeps' host
+ * tier does the same with these (ABI 13).  Synchronous, on the calling
+ * thread; same index, offset, `num_vals_limit` and order semantics as the
+ * reference loops (entries in index order, so a repeated destination gets
+ * its adds in op order).  Pure host code: no device, stream or HIP runtime.
+ * ------------------------------------------------------------------------- */
+/* y[(id1+off1)*W + v] += x[(id0+off0)*W + v] where (id0+off0)*W + v < limit
+ * -- add_rows_from_double_index_cpu (src/common/row-op-util.hpp:121-139). */
+int gp_host_scatter_add_rows(float *y, const float *x, const gp_double_index *index, size_t num_rows,
+                             gp_double_index offset, size_t row_size, size_t num_vals_limit);
+/* y[(id0+off0)*W + v] = x[(id1+off1)*W + v] where (id0+off0)*W + v < limit
+ * -- assign_rows_to_double_index_cpu (src/common/row-op-util.hpp:81-99). */
+int gp_host_gather_rows(float *y, const float *x, const gp_double_index *index, size_t num_rows,
+                        gp_double_index offset, size_t row_size, size_t num_vals_limit);
+/* y[i] += x[i], i < n -- add_row_batch (src/common/row-op-util.hpp:64-70,
+ * cpu_axpy with alpha 1: the same bits as one fp32 add per element). */
+int gp_host_add(size_t n, float *y, const float *x);
 
 /* ---------------------------------------------------------------------------
  * Runtime helpers, so host C++ never names a HIP type.

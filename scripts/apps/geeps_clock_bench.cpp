@@ -68,6 +68,17 @@ int main(int argc, char **argv) {
   // CLOCK_BENCH_RMW: read-my-writes (each Read adds this worker's own
   // unpushed updates to the refreshed rows, clientlib-data.cpp:132-150)
   if (std::getenv("CLOCK_BENCH_RMW")) cfg.read_my_writes = 1;
+  // CLOCK_BENCH_HOST_TIER_FRAC=f: the table's rows as two key batches (rows
+  // [0, h) and [h, rows), h = (1 - f) rows), each read and updated by an op of
+  // its own, and a gpu_memory_capacity that holds the thread cache (twice the
+  // peak rows in use: both Reads and both PreUpdates, 2 x rows) and the first
+  // batch only (2 rows of capacity per cached row: the cache and one oplog),
+  // so the second batch, f of the rows, lives in libgeeps' host tier
+  // (vi_decide_param_cache, clientlib-viter.cpp:520-568)
+  const char *frac_env = std::getenv("CLOCK_BENCH_HOST_TIER_FRAC");
+  const double host_frac = frac_env ? std::atof(frac_env) : 0.0;
+  const size_t split_at = host_frac > 0 ? (size_t)((1.0 - host_frac) * (double)rows) : rows;
+  if (host_frac > 0) cfg.gpu_memory_capacity = (4 * rows + 2 * split_at) * sizeof(RowData);
   for (int i = 0; i < P; ++i) {
     cfg.host_list.push_back("127.0.0.1");
     cfg.port_list.push_back(base + 16 * i);
@@ -80,23 +91,37 @@ int main(int argc, char **argv) {
   const bool per_shard = std::getenv("CLOCK_BENCH_READ_PER_SHARD") != nullptr;
   std::vector<int> hr, hpr;
   std::vector<size_t> hr_rows;
-  for (int s = 0; s < (per_shard ? P : 1); ++s) {
-    const size_t div = rows / P, res = rows % P;
-    const size_t lo = per_shard ? div * s + std::min<size_t>(s, res) : 0;
-    const size_t hi = per_shard ? lo + div + ((size_t)s < res ? 1 : 0) : rows;
-    hr.push_back(ps->VirtualRead(0, std::vector<size_t>(ids.begin() + lo, ids.begin() + hi), slack));
-    hr_rows.push_back(hi - lo);
+  std::vector<std::pair<size_t, size_t>> batches;  // [lo, hi) of each Read op
+  if (host_frac > 0) {
+    batches = {{0, split_at}, {split_at, rows}};
+  } else {
+    for (int s = 0; s < (per_shard ? P : 1); ++s) {
+      const size_t div = rows / P, res = rows % P;
+      const size_t lo = per_shard ? div * s + std::min<size_t>(s, res) : 0;
+      batches.emplace_back(lo, per_shard ? lo + div + ((size_t)s < res ? 1 : 0) : rows);
+    }
   }
-  const int hp = ps->VirtualPreUpdate(0, ids);
+  for (auto &b : batches) {
+    hr.push_back(ps->VirtualRead(0, std::vector<size_t>(ids.begin() + b.first, ids.begin() + b.second), slack));
+    hr_rows.push_back(b.second - b.first);
+  }
+  // one update op over the table, or one per batch (a host-tier batch is
+  // updated by ops of its own)
+  std::vector<std::pair<size_t, size_t>> ubatches = host_frac > 0 ? batches : std::vector<std::pair<size_t, size_t>>{{0, rows}};
+  std::vector<int> hps, hus;
+  for (auto &b : ubatches)
+    hps.push_back(ps->VirtualPreUpdate(0, std::vector<size_t>(ids.begin() + b.first, ids.begin() + b.second)));
   for (int h : hr) hpr.push_back(ps->VirtualPostRead(h));
-  const int hu = ps->VirtualUpdate(hp);
+  for (int h : hps) hus.push_back(ps->VirtualUpdate(h));
   ps->VirtualClock();
   ps->FinishVirtualIteration();
 
   RowOpVal *ub = nullptr;
-  ps->PreUpdate(hp, &ub);
-  HCK(hipMemset(ub, 0, rows * sizeof(RowOpVal)));
-  ps->Update(hu);
+  for (size_t i = 0; i < hps.size(); ++i) {
+    ps->PreUpdate(hps[i], &ub);
+    HCK(hipMemset(ub, 0, (ubatches[i].second - ubatches[i].first) * sizeof(RowOpVal)));
+  }
+  for (int h : hus) ps->Update(h);
   ps->Clock();
   ps->StartIterations();
 
@@ -106,12 +131,15 @@ int main(int argc, char **argv) {
     if (c == warmup) t0 = clk::now();
     RowData *rb = nullptr;
     for (int h : hr) ps->Read(h, &rb);
-    ps->PreUpdate(hp, &ub);
-    // the app's "gradient": 0.5 everywhere, written on the device
-    HCK(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(ub), 0x3f000000, rows * ROW_DATA_SIZE));
+    for (size_t i = 0; i < hps.size(); ++i) {
+      ps->PreUpdate(hps[i], &ub);
+      // the app's "gradient": 0.5 everywhere, written on the device
+      HCK(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(ub), 0x3f000000,
+                       (ubatches[i].second - ubatches[i].first) * ROW_DATA_SIZE));
+    }
     HCK(hipDeviceSynchronize());
     for (int h : hpr) ps->PostRead(h);
-    ps->Update(hu);
+    for (int h : hus) ps->Update(h);
     ps->Clock();
   }
   // the last Read waits for the last clock's refresh: include it

@@ -134,12 +134,11 @@ int main(int argc, char **argv) {
   cfg.num_comm_channels = channels;
   cfg.read_my_writes = rmw;
   cfg.gpu_memory_capacity = (size_t)1 << 34;
-  // GEEPS_TEST_CAPACITY=<bytes>: a tight capacity with mm_warning_level 2, so
-  // FinishVirtualIteration must refuse (libgeeps has no CPU param-cache tier)
-  if (const char *cap = std::getenv("GEEPS_TEST_CAPACITY")) {
-    cfg.gpu_memory_capacity = std::strtoull(cap, nullptr, 10);
-    cfg.mm_warning_level = 2;
-  }
+  // GEEPS_TEST_CAPACITY=<bytes>: a tight gpu_memory_capacity, so key batches
+  // past it go to libgeeps' host tier (vi_decide_param_cache);
+  // GEEPS_TEST_MM_LEVEL=<n>: mm_warning_level (3 refuses a host tier)
+  if (const char *cap = std::getenv("GEEPS_TEST_CAPACITY")) cfg.gpu_memory_capacity = std::strtoull(cap, nullptr, 10);
+  if (const char *lvl = std::getenv("GEEPS_TEST_MM_LEVEL")) cfg.mm_warning_level = std::atoi(lvl);
   GeePs *ps = new GeePs(pid, cfg);
 
   size_t total = 0;

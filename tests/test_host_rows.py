@@ -1,0 +1,82 @@
+"""The C-ABI's host-memory row ops (ABI 13: gp_host_scatter_add_rows,
+gp_host_gather_rows, gp_host_add) against the oracle, bit for bit, on CPU.
+
+They are the reference's CPU twins (src/common/row-op-util.hpp:64-139), which
+libgeeps' host tier runs on the key batches a param cache places in host
+memory past `gpu_memory_capacity` (src/client/clientlib-viter.cpp:492-611).
+Cases: identity / permuted / repeated destinations (op order), offsets,
+`num_vals_limit` cutting a row mid-way and whole rows off, widths 1..1024,
+empty calls, and argument rejection.
+"""
+import numpy as np
+import pytest
+
+from geeps_amd import rowops
+from oracle import oracle
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def _index(rng, kind, n_op, n_cache):
+    id0 = np.arange(n_op)
+    if kind == "identity":
+        id1 = np.arange(n_op)
+    elif kind == "permuted":
+        id1 = rng.permutation(n_cache)[:n_op]
+    else:  # repeated: destinations drawn with replacement (op order matters)
+        id1 = rng.integers(0, n_cache, n_op)
+    return np.stack([id0, id1], 1).astype(np.int64)
+
+
+@pytest.mark.parametrize("kind", ["identity", "permuted", "repeated"])
+@pytest.mark.parametrize("W,limit_frac,off", [(128, None, (0, 0)), (128, 0.71, (0, 0)), (64, None, (3, 5)),
+                                               (1, 0.5, (0, 0)), (1024, 0.9, (1, 2)), (7, None, (2, 0))])
+def test_host_scatter_add_and_gather_match_oracle(kind, W, limit_frac, off):
+    rng = np.random.default_rng(W * 13 + len(kind) + int((limit_frac or 0) * 100))
+    n_op, n_cache = 300, 400
+    idx = _index(rng, kind, n_op, n_cache - off[1])
+    limit = None if limit_frac is None else int((n_op + off[0]) * W * limit_frac) + 3
+    x = rng.standard_normal((n_op + off[0]) * W).astype(np.float32)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    rowops.add_rows_from_double_index_cpu(y, x, idx, off, W, limit)
+    assert np.array_equal(bits(y), bits(e))
+    # the gather (Read of a host-tier op): cache rows -> op buffer, guard on the op buffer
+    if kind != "repeated":
+        cache = rng.standard_normal(n_cache * W).astype(np.float32)
+        gidx = np.stack([idx[:, 0], idx[:, 1]], 1).astype(np.int64)
+        gy = np.zeros((n_op + off[0]) * W, np.float32)
+        ge = gy.copy()
+        goff = (off[0], off[1])
+        oracle.assign_rows_to_double_index(ge, cache, gidx, goff, W, limit)
+        rowops.assign_rows_to_double_index_cpu(gy, cache, gidx, goff, W, limit)
+        assert np.array_equal(bits(gy), bits(ge))
+
+
+def test_host_add_matches_vsadd():
+    rng = np.random.default_rng(3)
+    for n in (1, 127, 128 * 1000 + 5):
+        y = rng.standard_normal(n).astype(np.float32)
+        x = rng.standard_normal(n).astype(np.float32)
+        e = oracle.vs_add(y, x)
+        rowops.add_row_batch_cpu(y, x)
+        assert np.array_equal(bits(y), bits(e))
+    empty = np.zeros(0, np.float32)
+    rowops.add_row_batch_cpu(empty, empty)  # a no-op (vsAdd's n > 0 precondition does not apply)
+
+
+def test_host_row_ops_reject_bad_arguments_and_skip_empty_calls():
+    from geeps_amd import native
+    L = native.lib()
+    assert L.gp_host_scatter_add_rows(None, None, None, 0, native.DoubleIndex(0, 0), 128, 10) == 0
+    assert L.gp_host_scatter_add_rows(None, None, None, 3, native.DoubleIndex(0, 0), 128, 10) == 1
+    assert b"gp_host_scatter_add_rows" in L.gp_last_error()
+    y = np.zeros(8, np.float32)
+    assert L.gp_host_gather_rows(y.ctypes.data, y.ctypes.data, y.ctypes.data, 1, native.DoubleIndex(0, 0), 0,
+                                 10) == 1
+    assert L.gp_host_add(4, None, None) == 1
+    with pytest.raises(ValueError):
+        rowops.add_rows_from_double_index_cpu(y, y.astype(np.float64), np.zeros((1, 2), np.int64))

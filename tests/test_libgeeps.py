@@ -55,13 +55,15 @@ def test_libgeeps_exports_reference_symbol_set():
     assert not missing, missing
 
 
-def test_capacity_message_names_the_reference_cpu_tier():
-    """libgeeps keeps every row in HBM; past gpu_memory_capacity its message names
-    the reference's CPU placement it does not build (test_capacity_past_hbm_names_the_missing_cpu_tier runs it)."""
+def test_capacity_messages_cite_the_reference_placement():
+    """Past gpu_memory_capacity libgeeps places key batches in its host tier as
+    vi_decide_param_cache does; the refusals it shares with the reference cite
+    it (test_capacity_mm_level_3_refuses_a_host_tier runs one)."""
     assert os.path.exists(LIB), "run __graft_entry__.build() first"
     with open(LIB, "rb") as f:
         blob = f.read()
-    assert b"no CPU param-cache tier" in blob and b"clientlib-viter.cpp:492-611" in blob
+    assert b"mm_warning_level 3 keeps all parameter cache in GPU memory" in blob
+    assert b"clientlib-viter.cpp:551-552" in blob and b"not enough space for double buffering" in blob
 
 
 def test_app_links_with_public_header_only(tmp_path):
@@ -310,12 +312,12 @@ def test_config5_alexnet_8_workers_8_shards_staleness_1(dev, transport):
 
 
 def _run_app_layers(P, rows, spec, clocks, slack, timeout=600, transport="ipc", tables=1,
-                    local=0, out_dir="", extra_env=None):
+                    local=0, out_dir="", extra_env=None, channels=1, rmw=0, mode="int"):
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
-    base = _ports(P, 1)
+    base = _ports(P, channels)
     procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), str(clocks), str(slack),
-                     "1", "0", "int", spec, str(tables), str(local), out_dir],
+                     str(channels), str(rmw), mode, spec, str(tables), str(local), out_dir],
                     _env(transport, extra=extra_env))
              for p in range(P)]
     return _collect(procs, timeout)
@@ -538,21 +540,80 @@ def test_direct_read_two_tables_lagging_readers_keep_version_cap_live(dev):
     assert all(srv["nr_versions"] <= 2 * (P + 2) for s in st for srv in s["servers"])  # 2 tables
 
 
+# The host tier (a4).  The sum app's op sequence is every
+# layer's Read, then per layer (last first) PreUpdate / PostRead / Update: the
+# reference's thread cache is twice the peak rows in use at once (from an op
+# to its post-step, vi_create_local_storage), and each key batch
+# (a layer, first read) then takes (1 + oplog entries) rows per row of the
+# param-cache capacity that is left (vi_decide_param_cache).
+def _host_tier_capacity(layers, gpu_layers, entries):
+    now = peak = sum(layers)  # every Read
+    for r in reversed(layers):  # PreUpdate (+), PostRead (-), Update (-)
+        now += r
+        peak = max(peak, now)
+        now -= 2 * r
+    return (2 * peak + (1 + entries) * sum(layers[:gpu_layers])) * 512
+
+
+HOST_TIER_LAYERS = [300, 200, 400, 100]
+
+
 @pytest.mark.gpu
-def test_capacity_past_hbm_names_the_missing_cpu_tier(dev):
-    """Optional VERDICT r03 #8: a table past gpu_memory_capacity at
-    mm_warning_level 2 fails in FinishVirtualIteration with a message naming
-    the reference's CPU placement, which libgeeps does not build."""
+@pytest.mark.parametrize("P,slack,channels,rmw,transport,mode,gpu_layers,extra", [
+    (1, 0, 1, 0, "ipc", "float", 2, {}),
+    (1, 1, 2, 1, "ipc", "float", 1, {}),
+    (2, 0, 1, 0, "ipc", "int", 2, {}),
+    (2, 1, 2, 0, "tcp", "int", 2, {}),
+    (2, 1, 1, 1, "ipc", "int", 3, {}),
+    (3, 2, 2, 1, "ipc", "int", 1, {}),
+    (2, 0, 1, 0, "ipc", "int", 2, {"GEEPS_STAGE_PEER_REFRESH": "1", "GEEPS_STAGE_PEER_UPDATES": "1"}),
+    (2, 1, 1, 0, "ipc", "int", 0, {}),  # every batch in the host tier
+])
+def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mode, gpu_layers, extra):
+    """A gpu_memory_capacity that holds only the first `gpu_layers` key
+    batches: the rest go to the host tier, placed as vi_decide_param_cache
+    places them (clientlib-viter.cpp:520-568).  Their Updates are staged
+    device to host and scatter-added into the host oplog with the reference's
+    CPU loop, every push sends each server [host rows][HBM rows], refreshes are
+    split back, Reads gather on the host and copy up (clientlib-data.cpp:
+    153-189, 280-344, 398-434, 487-509).  Every Read is checked exactly (float
+    mode: bit for bit in the server's order; SSP bounds at slack > 0), with
+    read-my-writes, several channels, sockets and staged peers."""
+    entries = slack + 1 if rmw else 1
+    spec = ",".join(str(r) for r in HOST_TIER_LAYERS)
+    rows = sum(HOST_TIER_LAYERS)
+    cap = _host_tier_capacity(HOST_TIER_LAYERS, gpu_layers, entries)
+    outs = _run_app_layers(P, rows, spec, clocks=6, slack=slack, transport=transport, channels=channels, rmw=rmw,
+                           mode=mode, extra_env=dict({"GEEPS_TEST_CAPACITY": str(cap)}, **extra), timeout=300)
+    host_rows = sum(HOST_TIER_LAYERS[gpu_layers:])
+    for s in _stats(outs):
+        c = s["client"]
+        print("host tier:", c["rows_host_tier"], c["nr_read_host"], c["nr_update_host"])
+        assert c["rows_host_tier"] == host_rows
+        n_host_layers = len(HOST_TIER_LAYERS) - gpu_layers
+        assert c["nr_update_host"] > 0 and c["nr_read_host"] > 0
+        # every clock Reads and Updates each host-tier layer once (the setup
+        # clock only Updates)
+        assert c["nr_read_host"] == 6 * n_host_layers and c["nr_update_host"] == 7 * n_host_layers
+
+
+@pytest.mark.gpu
+def test_capacity_mm_level_3_refuses_a_host_tier(dev):
+    """mm_warning_level 3 keeps all parameter cache in GPU memory: a key batch
+    past gpu_memory_capacity fails FinishVirtualIteration, as the reference's
+    CHECK_LT(mm_warning_level, 3) does (clientlib-viter.cpp:551-552)."""
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
     base = _ports(1, 1)
-    pr = _spawn([SUM_APP, "0", "1", str(base), "512", "2", "0", "1", "0"],
-                _env("ipc", extra={"GEEPS_TEST_CAPACITY": "65536"}))
+    spec = ",".join(str(r) for r in HOST_TIER_LAYERS)
+    cap = _host_tier_capacity(HOST_TIER_LAYERS, 2, 1)
+    pr = _spawn([SUM_APP, "0", "1", str(base), str(sum(HOST_TIER_LAYERS)), "2", "0", "1", "0", "int", spec],
+                _env("ipc", extra={"GEEPS_TEST_CAPACITY": str(cap), "GEEPS_TEST_MM_LEVEL": "3"}))
     pr.wait(timeout=120)
     pr.err_file.seek(0)
     err = pr.err_file.read()
     assert pr.returncode != 0
-    assert "no CPU param-cache tier" in err and "clientlib-viter.cpp:492-611" in err, err[-2000:]
+    assert "mm_warning_level 3" in err and "clientlib-viter.cpp:551-552" in err, err[-2000:]
 
 
 def _one_process_per_gpu(P, extra):
