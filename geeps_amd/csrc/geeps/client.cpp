@@ -1102,7 +1102,8 @@ void ClientLib::finish_virtual_iteration() {
         }
       }
       if (cpu.num_rows) {
-        cpu.data.assign(cpu.num_rows * ROW_DATA_SIZE, 0.0f);  // zerofy_data_cpu
+        cpu.data = std::make_unique<HostBuf>(cpu.num_rows * ROW_DATA_SIZE, config_.pinned_cpu_memory != 0);
+        cpu.data->zero();  // zerofy_data_cpu
         cpu.server_row_start.resize(num_processes_);
         cpu.server_num_rows.resize(num_processes_);
         const size_t div = cpu.num_rows / num_processes_, res = cpu.num_rows % num_processes_;
@@ -1506,7 +1507,7 @@ void ClientLib::read_batch_host(OpInfo &op) {
     }
     waited += now_s() - w0;
     if (op.ch_size[ch.id])
-      GP_CALL(gp_host_gather_rows(cpu_buffer_.data(), pc.cpu.data.data(), op.host_index.data() + op.ch_start[ch.id],
+      GP_CALL(gp_host_gather_rows(cpu_buffer_.data(), pc.cpu.data->data(), op.host_index.data() + op.ch_start[ch.id],
                                   op.ch_size[ch.id], gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit));
   }
   const size_t vals = std::min(op.num_vals_limit, op.rows.size() * ROW_DATA_SIZE);
@@ -1546,7 +1547,7 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
     GP_CALL(gp_host_scatter_add_rows(oplog->data(), cpu_buffer_.data(), idx, n, gp_double_index{0, 0},
                                      ROW_DATA_SIZE, pre.num_vals_limit));
     if (config_.read_my_writes)
-      GP_CALL(gp_host_scatter_add_rows(cpu.data.data(), cpu_buffer_.data(), idx, n, gp_double_index{0, 0},
+      GP_CALL(gp_host_scatter_add_rows(cpu.data->data(), cpu_buffer_.data(), idx, n, gp_double_index{0, 0},
                                        ROW_DATA_SIZE, pre.num_vals_limit));
   }
 }
@@ -1554,20 +1555,20 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
 // create_oplog_entry + zerofy_data_cpu (clientlib-data.cpp:412-417): a pooled
 // host buffer once nothing (a pending push, the in-process server's bucket)
 // references it.
-std::shared_ptr<std::vector<float>> ClientLib::get_host_oplog(HostTier &cpu, iter_t clock) {
+std::shared_ptr<HostBuf> ClientLib::get_host_oplog(HostTier &cpu, iter_t clock) {
   auto it = cpu.oplog.find(clock);
   if (it != cpu.oplog.end()) return it->second;
-  std::shared_ptr<std::vector<float>> buf;
+  std::shared_ptr<HostBuf> buf;
   for (auto &b : cpu.oplog_pool)
     if (b.use_count() == 1) {
       buf = b;
       break;
     }
   if (!buf) {
-    cpu.oplog_pool.push_back(std::make_shared<std::vector<float>>(cpu.num_rows * ROW_DATA_SIZE));
+    cpu.oplog_pool.push_back(std::make_shared<HostBuf>(cpu.num_rows * ROW_DATA_SIZE, config_.pinned_cpu_memory != 0));
     buf = cpu.oplog_pool.back();
   }
-  std::fill(buf->begin(), buf->end(), 0.0f);
+  buf->zero();
   cpu.oplog[clock] = buf;
   return buf;
 }
@@ -1793,7 +1794,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
   std::vector<uint8_t> *bad = nullptr;        // app thread only
   // the host tier (empty unless gpu_memory_capacity placed rows there): its
   // oplog, server partition and the per-server frame keys [host | HBM]
-  std::shared_ptr<std::vector<float>> hoplog;
+  std::shared_ptr<HostBuf> hoplog;
   std::vector<size_t> cstarts, ccounts;
   std::vector<std::shared_ptr<std::vector<RowKey>>> frame_keys;
   bool tiers = false, zero_filled = false;
@@ -2032,7 +2033,7 @@ std::vector<int> ClientLib::recv_row_batch(uint32_t channel, uint32_t server_id,
       // into the host cache -- from the socket frame's host copy, or device to
       // host from the master version -- then with read-my-writes this
       // client's own unreflected host oplogs on top, clock by clock.
-      float *dst = cpu.data.data() + cpu.server_row_start[server_id] * ROW_DATA_SIZE;
+      float *dst = cpu.data->data() + cpu.server_row_start[server_id] * ROW_DATA_SIZE;
       if (host_rows) {
         std::memcpy(dst, host_rows, split * kRowBytes);
       } else {

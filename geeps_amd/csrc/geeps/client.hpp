@@ -99,7 +99,8 @@ struct OpInfo {
 
 // The CPU param cache of one (channel, table): the rows of the key batches
 // that vi_decide_param_cache placed in host memory, as the reference keeps them
-// (DataStorage::CPU: plain host memory, clientlib-viter.cpp:651-659), worked on
+// (DataStorage::CPU, clientlib-viter.cpp:651-659; page-locked here with
+// pinned_cpu_memory, the default, for the copies to and from HBM), worked on
 // with the reference's CPU twins (gp_host_*).  Each server's shard is [its
 // host-tier rows][its HBM-tier rows], in the server's master and on the wire
 // (clientlib-data.cpp:487-509; the refresh is split back the same way, :59-67).
@@ -107,10 +108,10 @@ struct HostTier {
   size_t num_rows = 0;
   std::unordered_map<row_idx_t, size_t> index;  // row id -> host cache row
   std::vector<RowKey> row_keys;
-  std::vector<float> data;                       // num_rows x 128
+  std::unique_ptr<HostBuf> data;                 // num_rows x 128
   std::vector<size_t> server_row_start, server_num_rows;
-  std::map<iter_t, std::shared_ptr<std::vector<float>>> oplog;
-  std::vector<std::shared_ptr<std::vector<float>>> oplog_pool;
+  std::map<iter_t, std::shared_ptr<HostBuf>> oplog;
+  std::vector<std::shared_ptr<HostBuf>> oplog_pool;
 };
 
 struct ParamCache {
@@ -322,7 +323,7 @@ class ClientLib {
   // storage, clientlib-viter.cpp:160-490: GPU local storage + a thread cache
   // of twice the peak op rows), in RowData rows out of ngr_capacity.
   size_t reference_ngr_used(size_t ngr_capacity);
-  std::shared_ptr<std::vector<float>> get_host_oplog(HostTier &cpu, iter_t clock);
+  std::shared_ptr<HostBuf> get_host_oplog(HostTier &cpu, iter_t clock);
   void read_batch_host(OpInfo &op);
   void update_batch_host(OpInfo &pre, iter_t clock);
   void reclaim_oplogs(ParamCache &pc, iter_t upto);

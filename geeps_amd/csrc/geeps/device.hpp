@@ -132,6 +132,43 @@ class PinnedArray {
   size_t n_ = 0;
 };
 
+// Host memory of libgeeps' host tier (the rows a param cache keeps in CPU
+// memory past gpu_memory_capacity): page-locked when `pinned` (the config's
+// pinned_cpu_memory, default on), so its copies to and from HBM run at the
+// pinned PCIe rate; plain memory otherwise, as the reference's DataStorage::CPU.
+class HostBuf {
+ public:
+  HostBuf(size_t n, bool pinned) : n_(n), pinned_(pinned) {
+    if (!n) return;
+    if (pinned) {
+      void *p = nullptr;
+      GP_CALL(gp_malloc_host(&p, n * sizeof(float)));
+      p_ = static_cast<float *>(p);
+    } else {
+      p_ = new float[n];
+    }
+  }
+  ~HostBuf() {
+    if (!p_) return;
+    if (pinned_)
+      gp_free_host(p_);
+    else
+      delete[] p_;
+  }
+  HostBuf(const HostBuf &) = delete;
+  HostBuf &operator=(const HostBuf &) = delete;
+  float *data() const { return p_; }
+  size_t size() const { return n_; }
+  void zero() {
+    for (size_t i = 0; i < n_; ++i) p_[i] = 0.0f;
+  }
+
+ private:
+  float *p_ = nullptr;
+  size_t n_ = 0;
+  bool pinned_ = false;
+};
+
 // A row plan: a DoubleIndex compiled once, on the current device, for the ops
 // whose index is fixed after FinishVirtualIteration -- a scatter plan
 // (gp_row_plan_create) for Update, a gather plan (gp_gather_plan_create) for

@@ -4,12 +4,23 @@
 // memory past `gpu_memory_capacity` (src/client/clientlib-viter.cpp:492-611).
 //
 // Each loop visits the index entries in order, as the reference's does, so a
-// destination listed twice gets its adds in op order.  The one change is
-// shape: a whole row under the limit runs as a straight, vectorisable loop,
-// and only the row that straddles `num_vals_limit` is guarded per element
-// (the same elements are written with the same values either way).
+// destination listed twice gets its adds in op order.  Two changes of shape,
+// neither of which changes a bit of the result:
+//   * a whole row under the limit runs as a straight, vectorisable loop, and
+//     only the row that straddles `num_vals_limit` is guarded per element;
+//   * a large call runs on several threads, each owning a contiguous range of
+//     DESTINATION rows and walking the whole index in order for the entries
+//     that land there: every destination still gets its entries in index
+//     order, from one thread (the reference's loop is one thread; a host tier
+//     of a large table is memory-bound, and one core reads ~10 GB/s).
+//     Threads: GP_HOST_THREADS, else OMP_NUM_THREADS, else the hardware's,
+//     at most 32; calls under 4 MiB of rows stay on the calling thread.
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
+#include <thread>
+#include <vector>
 
 #include "gp_reduce.h"
 
@@ -33,6 +44,55 @@ inline void guarded_row(size_t base, size_t row_size, size_t limit, F &&f) {
 
 int host_error(const char *msg) { return gp_internal::set_error(GP_ERR_INVALID, msg); }
 
+unsigned host_threads() {
+  static const unsigned n = [] {
+    for (const char *name : {"GP_HOST_THREADS", "OMP_NUM_THREADS"})
+      if (const char *e = std::getenv(name)) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0) return (unsigned)std::min<long>(v, 32);
+      }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(hw, 32u));
+  }();
+  return n;
+}
+
+constexpr size_t kParallelBytes = 4u << 20;
+
+// Runs body(lo, hi) over [0, n) split into contiguous ranges, one per thread
+// (the calling thread takes the first).
+template <typename F>
+void parallel_ranges(size_t n, size_t bytes, F &&body) {
+  const unsigned t = bytes < kParallelBytes ? 1u : (unsigned)std::min<size_t>(host_threads(), n);
+  if (t <= 1) {
+    body((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(t - 1);
+  const size_t per = (n + t - 1) / t;
+  for (unsigned k = 1; k < t; ++k) {
+    const size_t lo = std::min(n, k * per), hi = std::min(n, lo + per);
+    if (lo < hi) pool.emplace_back([&body, lo, hi] { body(lo, hi); });
+  }
+  body((size_t)0, std::min(n, per));
+  for (auto &th : pool) th.join();
+}
+
+// The destination rows an index writes, [lo, hi) (offsets applied), for the
+// destination-range split.
+template <bool TO_ID1>
+void dest_span(const gp_double_index *index, size_t n, gp_double_index off, size_t *lo, size_t *hi) {
+  size_t a = SIZE_MAX, b = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const size_t d = (TO_ID1 ? index[i].id1 + off.id1 : index[i].id0 + off.id0);
+    a = std::min(a, d);
+    b = std::max(b, d);
+  }
+  *lo = a;
+  *hi = b + 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -41,13 +101,20 @@ int gp_host_scatter_add_rows(float *y, const float *x, const gp_double_index *in
                              gp_double_index offset, size_t row_size, size_t num_vals_limit) {
   if (num_rows == 0) return GP_OK;
   if (!y || !x || !index || row_size == 0) return host_error("gp_host_scatter_add_rows: bad argument");
-  for (size_t i = 0; i < num_rows; ++i) {
-    const size_t from = index[i].id0 + offset.id0, to = index[i].id1 + offset.id1;
-    const float *__restrict__ xs = x + from * row_size;
-    float *__restrict__ ys = y + to * row_size;
-    // the guard is on the source (x) index, row-op-util.hpp:133-135
-    guarded_row(from * row_size, row_size, num_vals_limit, [&](size_t v) { ys[v] += xs[v]; });
-  }
+  size_t d0 = 0, d1 = 0;
+  const size_t bytes = num_rows * row_size * sizeof(float);
+  if (bytes >= kParallelBytes) dest_span<true>(index, num_rows, offset, &d0, &d1);
+  parallel_ranges(d1 - d0, bytes, [&](size_t lo, size_t hi) {
+    const bool all = bytes < kParallelBytes;  // one thread: every entry
+    for (size_t i = 0; i < num_rows; ++i) {
+      const size_t from = index[i].id0 + offset.id0, to = index[i].id1 + offset.id1;
+      if (!all && (to < d0 + lo || to >= d0 + hi)) continue;
+      const float *__restrict__ xs = x + from * row_size;
+      float *__restrict__ ys = y + to * row_size;
+      // the guard is on the source (x) index, row-op-util.hpp:133-135
+      guarded_row(from * row_size, row_size, num_vals_limit, [&](size_t v) { ys[v] += xs[v]; });
+    }
+  });
   return GP_OK;
 }
 
@@ -55,20 +122,29 @@ int gp_host_gather_rows(float *y, const float *x, const gp_double_index *index, 
                         gp_double_index offset, size_t row_size, size_t num_vals_limit) {
   if (num_rows == 0) return GP_OK;
   if (!y || !x || !index || row_size == 0) return host_error("gp_host_gather_rows: bad argument");
-  for (size_t i = 0; i < num_rows; ++i) {
-    const size_t from = index[i].id1 + offset.id1, to = index[i].id0 + offset.id0;
-    const float *__restrict__ xs = x + from * row_size;
-    float *__restrict__ ys = y + to * row_size;
-    // the guard is on the destination (y, the op buffer) index, row-op-util.hpp:93-95
-    guarded_row(to * row_size, row_size, num_vals_limit, [&](size_t v) { ys[v] = xs[v]; });
-  }
+  size_t d0 = 0, d1 = 0;
+  const size_t bytes = num_rows * row_size * sizeof(float);
+  if (bytes >= kParallelBytes) dest_span<false>(index, num_rows, offset, &d0, &d1);
+  parallel_ranges(d1 - d0, bytes, [&](size_t lo, size_t hi) {
+    const bool all = bytes < kParallelBytes;
+    for (size_t i = 0; i < num_rows; ++i) {
+      const size_t from = index[i].id1 + offset.id1, to = index[i].id0 + offset.id0;
+      if (!all && (to < d0 + lo || to >= d0 + hi)) continue;
+      const float *__restrict__ xs = x + from * row_size;
+      float *__restrict__ ys = y + to * row_size;
+      // the guard is on the destination (y, the op buffer) index, row-op-util.hpp:93-95
+      guarded_row(to * row_size, row_size, num_vals_limit, [&](size_t v) { ys[v] = xs[v]; });
+    }
+  });
   return GP_OK;
 }
 
 int gp_host_add(size_t n, float *y, const float *x) {
   if (n == 0) return GP_OK;
   if (!y || !x) return host_error("gp_host_add: null pointer");
-  for (size_t i = 0; i < n; ++i) y[i] += x[i];
+  parallel_ranges(n, n * sizeof(float), [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) y[i] += x[i];
+  });
   return GP_OK;
 }
 

@@ -56,9 +56,33 @@ def test_host_scatter_add_and_gather_match_oracle(kind, W, limit_frac, off):
         assert np.array_equal(bits(gy), bits(ge))
 
 
+@pytest.mark.parametrize("kind", ["permuted", "repeated"])
+def test_host_row_ops_multithreaded_keep_op_order(kind):
+    """Calls of 4 MiB of rows and more run on several threads, each owning a
+    range of destination rows and walking the index in order: a destination
+    listed many times still gets its adds in op order, bit for bit."""
+    rng = np.random.default_rng(99 + len(kind))
+    W, n_op, n_cache = 128, 40000, 50000
+    idx = _index(rng, kind, n_op, n_cache)
+    if kind == "repeated":
+        idx[::7, 1] = 123  # one row listed ~5,700 times
+    x = rng.standard_normal(n_op * W).astype(np.float32)
+    y = rng.standard_normal(n_cache * W).astype(np.float32)
+    e = y.copy()
+    oracle.add_rows_from_double_index(e, x, idx, (0, 0), W, n_op * W - 77)
+    rowops.add_rows_from_double_index_cpu(y, x, idx, (0, 0), W, n_op * W - 77)
+    assert np.array_equal(bits(y), bits(e))
+    if kind == "permuted":
+        g, ge = np.zeros(n_op * W, np.float32), np.zeros(n_op * W, np.float32)
+        gidx = np.stack([np.arange(n_op), rng.integers(0, n_cache, n_op)], 1).astype(np.int64)
+        oracle.assign_rows_to_double_index(ge, y, gidx, (0, 0), W, n_op * W - 5)
+        rowops.assign_rows_to_double_index_cpu(g, y, gidx, (0, 0), W, n_op * W - 5)
+        assert np.array_equal(bits(g), bits(ge))
+
+
 def test_host_add_matches_vsadd():
     rng = np.random.default_rng(3)
-    for n in (1, 127, 128 * 1000 + 5):
+    for n in (1, 127, 128 * 1000 + 5, (8 << 20) + 3):
         y = rng.standard_normal(n).astype(np.float32)
         x = rng.standard_normal(n).astype(np.float32)
         e = oracle.vs_add(y, x)
