@@ -48,6 +48,31 @@ ok / failure counts, the allocation addresses (is a small buffer a fragment
 of a shared block?) and the runtime's stderr lines.
 
 Usage: python scripts/probes/ipc_probe.py [scenario ...]
+
+Round 5: a GPU box was lost running the `late` / `primed`
+scenarios (scripts/gpu_runs/r04/dev5.sh), 20 runs of two processes with 64 x
+2 MiB exports each.  What in this probe could leave a box unrecoverable, from
+its code (nothing came back from that run):
+  1. open_and_check read 16 B at +0 and at +nbytes-16 of every mapping with
+     hipMemcpy, whatever the runtime mapped.  The probe had seen mappings of
+     OTHER memory (0xFF instead of the exported value); a mapping of a
+     smaller or unrelated range read at +2 MiB - 16 is a device access past
+     the mapping: a GPU memory fault, the one step here that can take a device
+     (and, on this pool, its host) down.
+  2. `keep` mappings (128 in those scenarios) were left open to process exit,
+     including any mis-mapped one, so the runtime tore them down at exit.
+  3. The driver's 45-s deadline SIGKILLed a process still holding mappings
+     (and maybe a queued copy through one).
+  4. The rocprofv3 step after the probe ran only first_call_breakdown.py
+     (kernel + memory-copy traces, no counters): not implicated.
+Fixed here: a mapping is read only after hipMemGetAddressRange shows that it
+spans every byte read (else it is reported as mis-mapped, unread); every
+mapping is closed before the process exits; a stuck process gets SIGTERM and
+5 s before SIGKILL.  The `late` / `primed` / `warm` / `retry` scenarios are not
+to be run on the shared pool again: they refuse to start unless
+IPC_PROBE_ALLOW_YOUNG=1.  libgeeps itself checks a mapping's range and tag
+before it reads one byte of it (gp_ipc_open_handle), and a failed mapping
+costs a resend over the socket (wire.hpp, NACKs).
 """
 from __future__ import annotations
 
@@ -125,8 +150,20 @@ def get(d, name, timeout=30.0):
         return f.read()
 
 
+OPEN_MAPPINGS = []  # kept mappings, closed before the process exits (close_all)
+OPEN_LOCK = threading.Lock()
+
+
+def close_all(h):
+    with OPEN_LOCK:
+        while OPEN_MAPPINGS:
+            h.hipIpcCloseMemHandle(OPEN_MAPPINGS.pop())
+
+
 def open_and_check(h, raw, value, nbytes, keep=False):
-    """Open a handle; return (ok, detail).  keep: leave the mapping open."""
+    """Open a handle; return (ok, detail).  keep: leave the mapping open (until
+    close_all).  The mapping is read only where hipMemGetAddressRange shows it
+    spans the bytes read: a mis-mapped handle is reported, never read past."""
     hd = IpcHandle()
     assert len(raw) == 64
     ctypes.memmove(ctypes.addressof(hd), raw, 64)
@@ -134,13 +171,21 @@ def open_and_check(h, raw, value, nbytes, keep=False):
     rc = h.hipIpcOpenMemHandle(ctypes.byref(p), hd, 1)  # hipIpcMemLazyEnablePeerAccess
     if rc != 0:
         return False, "open: " + h.hipGetErrorString(rc).decode()
+    base, size = ctypes.c_void_p(), ctypes.c_size_t()
+    if h.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), p) != 0 or base.value is None \
+            or p.value < base.value or p.value + nbytes > base.value + size.value:
+        h.hipIpcCloseMemHandle(p)
+        return False, f"mapping {p.value:#x} does not span {nbytes} B (range {base.value} + {size.value}): unread"
     out = (ctypes.c_ubyte * 16)()
     for off in (0, nbytes - 16):
         call(h, h.hipMemcpy(out, ctypes.c_void_p(p.value + off), 16, 2), "D2H")  # DeviceToHost
         if any(b != value for b in out):
             h.hipIpcCloseMemHandle(p)
             return False, f"mapped bytes {list(out)[:4]} at +{off}, exported {value}"
-    if not keep:
+    if keep:
+        with OPEN_LOCK:
+            OPEN_MAPPINGS.append(p)
+    else:
         call(h, h.hipIpcCloseMemHandle(p), "close")
     return True, ""
 
@@ -284,6 +329,7 @@ def importer(scn, d):
             t.start()
         for t in ths:
             t.join()
+        close_all(h)
         put(d, "done", b"1")
         print(json.dumps({"role": "importer", "results": results}))
         return
@@ -299,6 +345,7 @@ def importer(scn, d):
         results.append({"k": k, "ok": ok, "why": why})
         if scn.startswith("seq"):
             put(d, f"opened{k}", b"1")
+    close_all(h)
     put(d, "done", b"1")
     print(json.dumps({"role": "importer", "results": results}))
 
@@ -335,7 +382,14 @@ def peer(scn, d, me):
     print(json.dumps({"role": f"peer{me}", "opened": n, "errors": errors}))
 
 
+YOUNG = ("retry", "late", "warm", "primed")  # the scenarios of the lost box (see the header)
+
+
 def run(scn):
+    if scn in YOUNG and os.environ.get("IPC_PROBE_ALLOW_YOUNG") != "1":
+        print(json.dumps({"scenario": scn, "refused": "retired from the shared GPU pool (VERDICT r04 #3); "
+                                                      "IPC_PROBE_ALLOW_YOUNG=1 overrides"}), flush=True)
+        return
     d = tempfile.mkdtemp(prefix="ipc_probe_")
     me = os.path.abspath(__file__)
     if scn == "bidir":
@@ -349,8 +403,12 @@ def run(scn):
         try:
             o, e = p.communicate(timeout=max(1.0, deadline - time.monotonic()))
         except subprocess.TimeoutExpired:
-            p.kill()
-            o, e = p.communicate()
+            p.terminate()  # SIGTERM first: let it unwind its mappings
+            try:
+                o, e = p.communicate(timeout=5)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                o, e = p.communicate()
         outs.append({"rc": p.returncode, "out": [json.loads(x) for x in o.splitlines() if x.startswith("{")],
                      "stderr": [x for x in e.splitlines() if x.strip()][-40:]})
     print(json.dumps({"scenario": scn, "procs": outs}), flush=True)
