@@ -317,13 +317,20 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       if (n) take_keys(parts[1]);
       std::shared_ptr<PinnedArray<float>> rows = host_rows;
       if (parts.size() == 4) {
-        // Same-node client: the rows stay in its oplog, mapped here over IPC.
-        GP_CHECK(parts[2].size == 0 && parts[3].size == sizeof(IpcRowsRef));
+        // Same-node client: the rows stay in its oplog, mapped here over IPC;
+        // a table with a host tier sends its host-tier rows in the frame, first
+        GP_CHECK(parts[3].size == sizeof(IpcRowsRef) && parts[2].size % kRowBytes == 0);
         IpcRowsRef ref;
         std::memcpy(&ref, parts[3].data, sizeof ref);
         GP_CHECK(ref.bytes % kRowBytes == 0);
-        if (n) GP_CHECK_EQ(ref.bytes, n * kRowBytes);
-        n = ref.bytes / kRowBytes;  // key part omitted after the first message
+        const size_t head = parts[2].size / kRowBytes;
+        if (n) GP_CHECK_EQ(parts[2].size + ref.bytes, n * kRowBytes);
+        n = head + ref.bytes / kRowBytes;  // key part omitted after the first message
+        if (head) {
+          b.split = head;
+          b.host_head = rows->data();
+          b.head_keepalive = rows;
+        }
         auto &mapped = ch.ipc_oplogs[client_id];
         bool ok = true;
         if (ref.has_handle) {
@@ -379,6 +386,9 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
               GP_CHECK_EQ(v[2].size, n * kRowBytes);
               take_keys(v[1]);  // (the resend always carries the keys)
               rows = f.rows;
+              b.split = 0;  // (all its rows, host-tier ones first, in the frame)
+              b.host_head = nullptr;
+              b.head_keepalive.reset();
               break;
             }
             held.push_back(std::move(f));
@@ -479,8 +489,10 @@ void ClientLib::resend_version(Channel &ch, uint32_t c, const VersionNackMsg &m,
 void ClientLib::resend_oplog(Channel &ch, uint32_t s, const OplogNackMsg &m, PinnedArray<float> &buf,
                              const Stream &st) {
   std::shared_ptr<DeviceArray<float>> oplog;
+  std::shared_ptr<HostBuf> hoplog;  // with a host tier: its rows go first
   std::shared_ptr<const std::vector<RowKey>> keys;
-  size_t a = 0, n = 0;
+  const RowKey *key0 = nullptr;
+  size_t a = 0, n = 0, ca = 0, cn = 0;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     GP_CHECK_LT(m.table_id, ch.tables.size());
@@ -489,14 +501,28 @@ void ClientLib::resend_oplog(Channel &ch, uint32_t s, const OplogNackMsg &m, Pin
     GP_CHECK_MSG(it != pc.oplog.end(), "server " << s << " NACKed clock " << m.clock << " of table " << m.table_id
                                                  << ", whose oplog is gone");
     oplog = it->second;
-    keys = pc.row_keys;
     a = pc.server_row_start[s];
     n = pc.server_num_rows[s];
+    if (pc.cpu.num_rows) {
+      auto hit = pc.cpu.oplog.find(m.clock);
+      GP_CHECK_MSG(hit != pc.cpu.oplog.end(), "NACKed clock " << m.clock << ": its host oplog is gone");
+      hoplog = hit->second;
+      ca = pc.cpu.server_row_start[s];
+      cn = pc.cpu.server_num_rows[s];
+      keys = pc.frame_keys[s];
+      key0 = keys->data();
+    } else {
+      keys = pc.row_keys;
+      key0 = keys->data() + a;
+    }
     pc.ipc_nacked.emplace_back((size_t)(m.buffer_id & 0xffffffffu), s);
   }
-  const size_t floats = n * ROW_DATA_SIZE;
+  const size_t floats = (cn + n) * ROW_DATA_SIZE;
   if (buf.size() < floats) buf.resize(floats);
-  if (floats) GP_CALL(gp_memcpy_async(buf.data(), oplog->data() + a * ROW_DATA_SIZE, floats * sizeof(float), st.get()));
+  if (cn) std::memcpy(buf.data(), hoplog->data() + ca * ROW_DATA_SIZE, cn * kRowBytes);
+  if (n)
+    GP_CALL(gp_memcpy_async(buf.data() + cn * ROW_DATA_SIZE, oplog->data() + a * ROW_DATA_SIZE, n * kRowBytes,
+                            st.get()));
   st.sync();
   cs_clock_with_updates_batch_msg_t h{};
   h.cmd = CLOCK_WITH_UPDATES_BATCH;
@@ -507,7 +533,7 @@ void ClientLib::resend_oplog(Channel &ch, uint32_t s, const OplogNackMsg &m, Pin
     // (also after this client's SHUTDOWN: the server's reader awaits this
     // frame and holds the SHUTDOWN back behind it)
     std::lock_guard<std::mutex> lk(*ch.server_send_mu[s]);
-    GP_CHECK_MSG(send_frame(ch.server_fd[s], {Part{&h, sizeof h}, Part{keys->data() + a, n * sizeof(RowKey)},
+    GP_CHECK_MSG(send_frame(ch.server_fd[s], {Part{&h, sizeof h}, Part{key0, (cn + n) * sizeof(RowKey)},
                                               Part{buf.data(), floats * sizeof(float)}}),
                  "resend to server " << s << " failed");
   }
@@ -1817,7 +1843,11 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       cstarts = cpu.server_row_start;
       ccounts = cpu.server_num_rows;
       frame_keys = pc.frame_keys;
-      if (hoplog && !config_.read_my_writes) cpu.oplog.erase(clock);  // (the frames keep it alive)
+      // (the frames keep it alive; a same-node server's NACK needs it until
+      // its refresh covers the clock, as the HBM oplog: recv_row_batch reclaims)
+      bool ipc_servers = false;
+      for (uint32_t s = 0; s < num_processes_; ++s) ipc_servers |= ipc_to(s);
+      if (hoplog && !config_.read_my_writes && !(ipc_servers && pc.num_rows)) cpu.oplog.erase(clock);
     }
     if (pc.oplog_bad.size() < pc.oplog_pool.size()) pc.oplog_bad.resize(pc.oplog_pool.size(), 0);
     if (pc.exported.size() < pc.oplog_pool.size())
@@ -1837,7 +1867,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
     counts = pc.server_num_rows;
     keys = pc.row_keys;
     bool ipc_readers = false;  // a same-node server reads its slice from this oplog
-    for (uint32_t s = 0; s < num_processes_; ++s) ipc_readers |= ipc_to(s) && counts[s] > 0 && !tiers;
+    for (uint32_t s = 0; s < num_processes_; ++s) ipc_readers |= ipc_to(s) && (counts[s] > 0 || tiers);
     if (oplog) {
       for (size_t k = 0; k < pc.oplog_pool.size(); ++k)
         if (pc.oplog_pool[k] == oplog) pool_id = k;
@@ -1859,9 +1889,9 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
     if (tiers && hoplog) {
       // A table with host-tier rows: every frame is [host rows of s][HBM rows
       // of s] (push_updates_param_cache, clientlib-data.cpp:487-509).  The
-      // in-process server gets the host part and the oplog slice in place;
-      // every other server an ordinary socket frame (the reference's own
-      // path; same-node IPC carries HBM-only tables).
+      // in-process server gets the host part and the oplog slice in place; a
+      // same-node server the host part in the frame and the HBM part over IPC;
+      // any other server an ordinary socket frame (the reference's own path).
       const size_t ca = cstarts[s], cn = ccounts[s], a = starts[s], n = counts[s];
       if (s == process_id_) {
         UpdateBatch b;
@@ -1879,6 +1909,41 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
           b.keepalive = oplog;
         }
         ch.server->post_updates(std::move(b));
+        continue;
+      }
+      if (oplog && ipc_to(s) && [&] {
+            if ((*exported)[s]) return true;
+            IpcRowsRef probe{};
+            if (ipc_export(probe.handle, oplog->data(), 0)) {
+              std::memcpy(ch_export_handle, probe.handle, sizeof probe.handle);
+              return true;
+            }
+            (*bad)[pool_id] = 1;
+            std::lock_guard<std::mutex> lk(stats_mu_);
+            stats_.nr_ipc_export_refused++;
+            return false;
+          }()) {
+        // Same-node server: the host-tier rows travel in the frame (from the
+        // pinned host oplog), the HBM rows stay in this oplog, mapped over IPC
+        cs_clock_with_updates_batch_msg_t h{};
+        h.cmd = CLOCK_WITH_UPDATES_BATCH;
+        h.client_id = process_id_;
+        h.clock = clock;
+        h.table_id = table_id;
+        IpcRowsRef ref{};
+        ref.buffer_id = ((uint64_t)table_id << 32) | (uint64_t)pool_id;
+        ref.offset = a * kRowBytes;
+        ref.bytes = n * kRowBytes;
+        if (!(*exported)[s]) {
+          std::memcpy(ref.handle, ch_export_handle, sizeof ref.handle);
+          ref.has_handle = 1;
+          (*exported)[s] = 1;
+        }
+        const bool with_keys = !(*keys_sent)[s];
+        send_to_server(ch, s, {Part{&h, sizeof h},
+                               with_keys ? Part{frame_keys[s]->data(), (cn + n) * sizeof(RowKey)} : Part{nullptr, 0},
+                               Part{hoplog->data() + ca * ROW_DATA_SIZE, cn * kRowBytes}, Part{&ref, sizeof ref}});
+        (*keys_sent)[s] = 1;
         continue;
       }
       const size_t floats = (cn + n) * ROW_DATA_SIZE;

@@ -546,13 +546,14 @@ def test_direct_read_two_tables_lagging_readers_keep_version_cap_live(dev):
 # to its post-step, vi_create_local_storage), and each key batch
 # (a layer, first read) then takes (1 + oplog entries) rows per row of the
 # param-cache capacity that is left (vi_decide_param_cache).
-def _host_tier_capacity(layers, gpu_layers, entries):
+def _host_tier_capacity(layers, gpu_layers, entries, local_rows=0):
     now = peak = sum(layers)  # every Read
     for r in reversed(layers):  # PreUpdate (+), PostRead (-), Update (-)
         now += r
         peak = max(peak, now)
         now -= 2 * r
-    return (2 * peak + (1 + entries) * sum(layers[:gpu_layers])) * 512
+    # (a fetched / kept local batch sits in GPU memory, outside the peak)
+    return (local_rows + 2 * peak + (1 + entries) * sum(layers[:gpu_layers])) * 512
 
 
 HOST_TIER_LAYERS = [300, 200, 400, 100]
@@ -568,6 +569,8 @@ HOST_TIER_LAYERS = [300, 200, 400, 100]
     (3, 2, 2, 1, "ipc", "int", 1, {}),
     (2, 0, 1, 0, "ipc", "int", 2, {"GEEPS_STAGE_PEER_REFRESH": "1", "GEEPS_STAGE_PEER_UPDATES": "1"}),
     (2, 1, 1, 0, "ipc", "int", 0, {}),  # every batch in the host tier
+    (2, 0, 1, 0, "ipc", "int", 2, {"GEEPS_TEST_IPC_FAULT": "tag"}),  # NACK: the resend carries both parts
+    (3, 1, 1, 0, "ipc", "int", 1, {"GEEPS_TEST_IPC_FAULT": "refuse"}),
 ])
 def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mode, gpu_layers, extra):
     """A gpu_memory_capacity that holds only the first `gpu_layers` key
@@ -703,8 +706,9 @@ def test_randomized_configurations(dev, case):
     """Seeded random mixes of what the other tests vary one at a time:
     processes, slack, channels, tables, read-my-writes, a local-access op,
     transport, layer shapes, shuffled update rows, jitter, the direct oplog,
-    both peer-staging switches and direct reads.  Every Read is checked by the app (exact at
-    BSP, within the SSP bounds otherwise)."""
+    both peer-staging switches and direct reads; slow readers and queued device reads (round 4);
+    a host tier and IPC faults (round 5).  Every Read is checked by the app (exact at BSP, within
+    the SSP bounds otherwise)."""
     import random
     if not os.path.exists(SUM_APP):
         pytest.skip("geeps_sum_app not built")
@@ -740,6 +744,15 @@ def test_randomized_configurations(dev, case):
         extra["GEEPS_TEST_READER_DELAY_US"] = str(rng.choice([2000, 15000]))
     if rng.random() < 0.5 and "GEEPS_DIRECT_READ" in extra:
         extra["GEEPS_TEST_ASYNC_READ"] = "200"
+    # (round 5, drawn last again) the host tier: a capacity that holds the
+    # first k key batches (layers, in first-access order) and no more; and the
+    # IPC faults, each process's first exports refused or mis-tagged
+    if rng.random() < 0.3:
+        k = rng.randrange(0, len(layers))
+        extra["GEEPS_TEST_CAPACITY"] = str(_host_tier_capacity(layers, k, slack + 1 if rmw else 1,
+                                                               3 if local else 0))
+    if rng.random() < 0.2:
+        extra["GEEPS_TEST_IPC_FAULT"] = rng.choice(["tag", "refuse"])
     desc = dict(P=P, slack=slack, channels=channels, rmw=rmw, tables=tables, local=local, mode=mode,
                 layers=layers, transport=transport, **extra)
     print("config", desc)
