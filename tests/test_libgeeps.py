@@ -552,8 +552,12 @@ def _host_tier_capacity(layers, gpu_layers, entries, local_rows=0):
         now += r
         peak = max(peak, now)
         now -= 2 * r
-    # (a fetched / kept local batch sits in GPU memory, outside the peak)
-    return (local_rows + 2 * peak + (1 + entries) * sum(layers[:gpu_layers])) * 512
+    # A fetched / kept local batch (the app's local op spans the whole
+    # sequence) goes to GPU memory only if it fits beside twice the peak
+    # counted WITH it (CHECK_GE(ngr_capacity, 2 x peak), clientlib-viter.cpp:
+    # 338-341); once there it leaves the peak, which frees 2 x its rows more
+    # for the param cache than the k batches need.
+    return (local_rows + 2 * (peak + local_rows) + (1 + entries) * sum(layers[:gpu_layers])) * 512
 
 
 HOST_TIER_LAYERS = [300, 200, 400, 100]
