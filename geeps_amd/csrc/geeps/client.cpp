@@ -294,7 +294,8 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
   PinnedArray<float> resend_buf;
   std::unique_ptr<Stream> resend_stream;
   // false: the connection's last frame
-  auto handle = [&](const std::vector<RecvPart> &parts, const std::shared_ptr<PinnedArray<float>> &host_rows) {
+  std::function<bool(const std::vector<RecvPart> &, const std::shared_ptr<PinnedArray<float>> &)> handle =
+      [&](const std::vector<RecvPart> &parts, const std::shared_ptr<PinnedArray<float>> &host_rows) -> bool {
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == CLOCK_WITH_UPDATES_BATCH) {
@@ -390,6 +391,14 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
               b.host_head = nullptr;
               b.head_keepalive.reset();
               break;
+            }
+            // the client's own NACK of a version, and its releases, do not
+            // wait behind the resend (its reader may be awaiting this server's
+            // resend at the same time: holding them back would deadlock)
+            const command_t fc = f.parts.empty() || f.parts[0].empty() ? 0 : (command_t)f.parts[0][0];
+            if (fc == kCmdVersionNack || fc == kCmdRefreshAck) {
+              handle(f.view(), f.rows);
+              continue;
             }
             held.push_back(std::move(f));
           }
@@ -732,6 +741,12 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
                                                static_cast<const float *>(v[2].data), rv.num_rows, -1, nullptr,
                                                static_cast<const float *>(v[2].data)));
             break;
+          }
+          // the server's NACK of an oplog does not wait behind the resend
+          // (its reader may be awaiting this client's resend at the same time)
+          if (!f.parts.empty() && !f.parts[0].empty() && (command_t)f.parts[0][0] == kCmdOplogNack) {
+            handle(f.view(), false);
+            continue;
           }
           held.push_back(std::move(f));
         }
