@@ -764,4 +764,7 @@ def test_randomized_configurations(dev, case):
     procs = [_spawn([SUM_APP, str(p), str(P), str(base), str(rows), "8", str(slack), str(channels),
                      str(rmw), mode, ",".join(map(str, layers)), str(tables), str(local)],
                     _env(transport, extra=extra)) for p in range(P)]
-    _collect(procs, 240)
+    st = [s["client"] for s in _stats(_collect(procs, 240))]
+    # what the run recovered from (IPC) and placed on the host, summed over processes
+    print("recovered", {k: sum(c[k] for c in st) for k in ("nr_ipc_export_refused", "nr_ipc_nack_sent",
+                                                           "nr_ipc_resent", "rows_host_tier")})
