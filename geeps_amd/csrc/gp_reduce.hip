@@ -2174,6 +2174,19 @@ void reap_graves() {
 
 CachedPlan::~CachedPlan() {
   if (!ready) return;
+  // every call that used the entry already done (the usual case when the
+  // host drops it: an idle device): free now, as the member destructors do
+  bool passed = !uses.empty();
+  for (auto &u : uses)
+    if (passed && hipEventQuery(u.second) != hipSuccess) {
+      (void)hipGetLastError();
+      passed = false;
+    }
+  if (passed) {
+    for (auto &u : uses) (void)hipEventDestroy(u.second);
+    (void)hipEventDestroy(ready);
+    return;
+  }
   Grave g;
   g.device = key.device;
   for (auto &u : uses) g.events.push_back(u.second);
@@ -2719,11 +2732,12 @@ int gp_set_unplanned_min_bytes(size_t min_bytes) {
 }
 
 int gp_unplanned_cache_clear(void) {
-  std::vector<std::shared_ptr<CachedPlan>> gone;  // freed outside the lock
   {
+    std::vector<std::shared_ptr<CachedPlan>> gone;  // freed outside the lock
     std::lock_guard<std::mutex> lk(g_plan_cache_mu);
     gone.swap(g_plan_cache);
   }
+  reap_graves();
   return GP_OK;
 }
 
