@@ -328,11 +328,11 @@ def exchange_check(red, deltas, R, W, C, dev, world, kind):
     for c in range(C):  # fp32 adds in client order
         m = m + sampled[c]
     got = table.view(R, W).index_select(0, idx).cpu().numpy()
-    err = float((table - exp).abs().max().item()) if R * W else 0.0
+    bits_equal = torch.equal(table.view(torch.int32), exp.view(torch.int32))
+    err = float(exp.sub_(table).abs_().max().item()) if R * W else 0.0  # (in place: no 4-GiB temporaries)
     err_rows = float(np.abs(got - m).max()) if m.size else 0.0
     if kind == "a2a":
-        ok = (torch.equal(table.view(torch.int32), exp.view(torch.int32)) and
-              np.array_equal(got.view(np.uint32), m.view(np.uint32)))
+        ok = bits_equal and np.array_equal(got.view(np.uint32), m.view(np.uint32))
     else:
         ok = err <= rs_tolerance(C) and err_rows <= rs_tolerance(C)
     del exp
