@@ -182,6 +182,12 @@ static void row_cases(void) {
   oracle_add_rows_from_double_index(want, hx, idx, rows, off0, off1, W, limit);
   expect_same("gp_scatter_add_rows", got, want, y_vals);
 
+  /* 2b. the host-memory twin (ABI 13, the host tier): the same rows in host
+   * memory through gp_host_scatter_add_rows, against the same oracle sum */
+  memcpy(got, hy, y_vals * sizeof(float));
+  CALL(gp_host_scatter_add_rows(got, hx, (const gp_double_index *)idx, rows, off, W, limit));
+  expect_same("gp_host_scatter_add_rows", got, want, y_vals);
+
   /* 3. the same through a row plan: add, then fused init */
   CALL(gp_row_plan_create(&plan, (const gp_double_index *)idx, rows, off, W, limit));
   to_dev(dy, hy, y_vals * sizeof(float));
@@ -222,6 +228,13 @@ static void row_cases(void) {
     oracle_assign_rows_to_double_index(gwant, hy, idx, rows, off0, off1, W, glimit);
     expect_same("gp_gather_rows_planned", ggot, gwant, gy_vals);
     CALL(gp_row_plan_destroy(plan));
+
+    /* the host-memory twin (ABI 13): gp_host_gather_rows on the same rows */
+    fill(ggot, gy_vals);
+    memcpy(gwant, ggot, gy_vals * sizeof(float));
+    CALL(gp_host_gather_rows(ggot, hy, (const gp_double_index *)idx, rows, off, W, glimit));
+    oracle_assign_rows_to_double_index(gwant, hy, idx, rows, off0, off1, W, glimit);
+    expect_same("gp_host_gather_rows", ggot, gwant, gy_vals);
     CALL(gp_free_device(gy));
     CALL(gp_free_device(gx));
     free(gwant);
