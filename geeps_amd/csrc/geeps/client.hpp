@@ -20,10 +20,12 @@
 //     (recv_row_batch_gpu, clientlib-data.cpp:110-151) and Read() gathers the
 //     op's rows (assign_rows_to_double_index) — gp_gather_rows.
 //
-// Everything lives in HBM (288 GB per MI355X): param cache, oplogs, op buffers
-// and local storage; there is no CPU param-cache tier.  API calls run on the
-// calling thread; device work is ordered on per-channel HIP streams and synced
-// before a call returns data to the app.
+// The param cache, oplogs, op buffers and local storage live in HBM (288 GB
+// per MI355X), except the key batches that gpu_memory_capacity leaves out:
+// those live in the host tier (HostTier, placed as vi_decide_param_cache
+// places them, clientlib-viter.cpp:492-568).  API calls run on the calling
+// thread; device work is ordered on per-channel HIP streams and synced before
+// a call returns data to the app.
 
 #include <array>
 #include <atomic>
