@@ -159,9 +159,7 @@ class HostBuf {
   HostBuf &operator=(const HostBuf &) = delete;
   float *data() const { return p_; }
   size_t size() const { return n_; }
-  void zero() {
-    for (size_t i = 0; i < n_; ++i) p_[i] = 0.0f;
-  }
+  void zero() { GP_CALL(gp_host_zero(n_, p_)); }  // zerofy_data_cpu, threaded when large
 
  private:
   float *p_ = nullptr;

@@ -19,6 +19,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -144,6 +145,15 @@ int gp_host_add(size_t n, float *y, const float *x) {
   if (!y || !x) return host_error("gp_host_add: null pointer");
   parallel_ranges(n, n * sizeof(float), [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) y[i] += x[i];
+  });
+  return GP_OK;
+}
+
+int gp_host_zero(size_t n, float *y) {
+  if (n == 0) return GP_OK;
+  if (!y) return host_error("gp_host_zero: null pointer");
+  parallel_ranges(n, n * sizeof(float), [&](size_t lo, size_t hi) {
+    std::memset(y + lo, 0, (hi - lo) * sizeof(float));
   });
   return GP_OK;
 }

@@ -102,6 +102,7 @@ _SIGNATURES = {
     "gp_host_scatter_add_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz]),
     "gp_host_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz]),
     "gp_host_add": (_i, [_sz, _vp, _vp]),
+    "gp_host_zero": (_i, [_sz, _vp]),
     "gp_zero": (_i, [_vp, _sz, _vp]),
     "gp_hbm_probe": (_i, [_i, _vp, _sz, _vp]),
     "gp_device_count": (_i, [_c.POINTER(_i)]),

@@ -397,6 +397,10 @@ int gp_host_gather_rows(float *y, const float *x, const gp_double_index *index, 
 /* y[i] += x[i], i < n -- add_row_batch (src/common/row-op-util.hpp:64-70,
  * cpu_axpy with alpha 1: the same bits as one fp32 add per element). */
 int gp_host_add(size_t n, float *y, const float *x);
+/* y[i] = 0, i < n -- zerofy_data_cpu (src/common/common-util.hpp:437-443),
+ * threaded like the row ops for large buffers (a host oplog of a large table
+ * is zeroed every clock). */
+int gp_host_zero(size_t n, float *y);
 
 /* ---------------------------------------------------------------------------
  * Runtime helpers, so host C++ never names a HIP type.

@@ -92,6 +92,15 @@ def test_host_add_matches_vsadd():
     rowops.add_row_batch_cpu(empty, empty)  # a no-op (vsAdd's n > 0 precondition does not apply)
 
 
+def test_host_zero():
+    from geeps_amd import native
+    for n in (1, 1000, (8 << 20) + 5):
+        y = np.full(n, np.float32(-3.5))
+        native.check(native.lib().gp_host_zero(n - 1, y.ctypes.data), "gp_host_zero")
+        assert not y[:n - 1].any() and y[n - 1] == np.float32(-3.5)
+    assert native.lib().gp_host_zero(3, None) == 1
+
+
 def test_host_row_ops_reject_bad_arguments_and_skip_empty_calls():
     from geeps_amd import native
     L = native.lib()
