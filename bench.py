@@ -969,9 +969,15 @@ def libgeeps_leg(rows, W, clocks=10, warmup=5, procs=(1, 2)):
     # (vi_decide_param_cache); its Updates go device to host and are added on
     # the CPU, its pushes and refreshes carry [host rows][HBM rows], its Reads
     # gather on the host and copy up (clientlib-data.cpp:153-189, 280-344,
-    # 398-434); 2 processes
-    leg("p2_alexnet_host_tier", lambda: run(2, {"CLOCK_BENCH_HOST_TIER_FRAC": "0.5"}, ALEXNET_ROWS, 0,
-                                            info={"host_tier_frac": 0.5}, keep=("read_ok", "rows_host_tier")))
+    # 398-434); 2 processes.  The peer server reads the host-tier rows from
+    # the client's shared host oplog (nr_host_shared); `_frames`: with
+    # GEEPS_HOST_SHARE=0 they travel in the socket frame instead
+    host = {"CLOCK_BENCH_HOST_TIER_FRAC": "0.5"}
+    leg("p2_alexnet_host_tier", lambda: run(2, host, ALEXNET_ROWS, 0, info={"host_tier_frac": 0.5},
+                                            keep=("read_ok", "rows_host_tier", "nr_host_shared")))
+    leg("p2_alexnet_host_tier_frames", lambda: run(2, dict(host, GEEPS_HOST_SHARE="0"), ALEXNET_ROWS, 0,
+                                                   info={"host_tier_frac": 0.5},
+                                                   keep=("read_ok", "rows_host_tier", "nr_host_shared")))
     return out
 
 

@@ -66,6 +66,7 @@ std::string ClientStats::to_json() const {
     << ", \"nr_ipc_export_refused\": " << nr_ipc_export_refused << ", \"nr_ipc_nack_sent\": " << nr_ipc_nack_sent
     << ", \"nr_ipc_resent\": " << nr_ipc_resent << ", \"rows_host_tier\": " << rows_host_tier
     << ", \"nr_read_host\": " << nr_read_host << ", \"nr_update_host\": " << nr_update_host
+    << ", \"nr_host_shared\": " << nr_host_shared << ", \"nr_host_share_refused\": " << nr_host_share_refused
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -127,6 +128,11 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
   for (uint32_t s = 0; s < num_processes_; ++s)
     same_node_[s] = allow_ipc && num_processes_ > 1 &&
                     norm(config_.host_list[s]) == norm(config_.host_list[process_id_]);
+  const char *share = std::getenv("GEEPS_HOST_SHARE");
+  host_share_ = config_.pinned_cpu_memory != 0 && !(share && std::string(share) == "0");
+  bool any_peer = false;
+  for (uint32_t s = 0; s < num_processes_; ++s) any_peer |= ipc_to(s);
+  host_share_ = host_share_ && any_peer;
   channels_.resize(num_channels_);
   for (uint32_t c = 0; c < num_channels_; ++c) {
     auto ch = std::make_unique<Channel>();
@@ -146,6 +152,8 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     for (uint32_t s = 0; s < num_processes_; ++s)
       ch->client_send_mu.push_back(std::make_unique<std::mutex>());
     ch->ipc_oplogs.resize(num_processes_);
+    ch->host_oplogs.resize(num_processes_);
+    ch->host_share_off.assign(num_processes_, 0);
     ch->ipc_client.assign(num_processes_, 0);
     ch->other_gpu.assign(num_processes_, 0);
     ch->stage_from.assign(num_processes_, 0);
@@ -299,8 +307,7 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
     GP_CHECK(!parts.empty() && parts[0].size >= 1);
     const command_t cmd = *static_cast<const command_t *>(parts[0].data);
     if (cmd == CLOCK_WITH_UPDATES_BATCH) {
-      GP_CHECK((parts.size() == 3 || parts.size() == 4) &&
-               parts[0].size == sizeof(cs_clock_with_updates_batch_msg_t));
+      GP_CHECK(parts.size() >= 3 && parts.size() <= 5 && parts[0].size == sizeof(cs_clock_with_updates_batch_msg_t));
       cs_clock_with_updates_batch_msg_t h;
       std::memcpy(&h, parts[0].data, sizeof h);
       GP_CHECK_EQ(h.client_id, client_id);
@@ -317,20 +324,55 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
       };
       if (n) take_keys(parts[1]);
       std::shared_ptr<PinnedArray<float>> rows = host_rows;
-      if (parts.size() == 4) {
+      if (parts.size() >= 4) {
         // Same-node client: the rows stay in its oplog, mapped here over IPC;
-        // a table with a host tier sends its host-tier rows in the frame, first
+        // a table with a host tier sends its host-tier rows first, in the
+        // frame, or (a 5th part) names them in its shared host oplog
         GP_CHECK(parts[3].size == sizeof(IpcRowsRef) && parts[2].size % kRowBytes == 0);
         IpcRowsRef ref;
         std::memcpy(&ref, parts[3].data, sizeof ref);
         GP_CHECK(ref.bytes % kRowBytes == 0);
-        const size_t head = parts[2].size / kRowBytes;
-        if (n) GP_CHECK_EQ(parts[2].size + ref.bytes, n * kRowBytes);
+        HostRowsRef href{};
+        const bool host_ref = parts.size() == 5;
+        if (host_ref) {
+          GP_CHECK(parts[4].size == sizeof(HostRowsRef) && parts[2].size == 0);
+          std::memcpy(&href, parts[4].data, sizeof href);
+          GP_CHECK(href.bytes % kRowBytes == 0 && href.bytes > 0);
+        }
+        const size_t head_bytes = host_ref ? href.bytes : parts[2].size;
+        const size_t head = head_bytes / kRowBytes;
+        if (n) GP_CHECK_EQ(head_bytes + ref.bytes, n * kRowBytes);
         n = head + ref.bytes / kRowBytes;  // key part omitted after the first message
-        if (head) {
+        if (head && !host_ref) {
           b.split = head;
           b.host_head = rows->data();
           b.head_keepalive = rows;
+        }
+        uint32_t unmapped = 0;  // kNackDevice | kNackHost
+        if (host_ref) {
+          auto &hmapped = ch.host_oplogs[client_id];
+          if (href.has_handle) {
+            hmapped.erase(href.buffer_id);
+            std::string why;
+            std::shared_ptr<SharedHostMem> m = SharedHostMem::open(href.handle, &why);
+            if (m) {
+              hmapped[href.buffer_id] = m;
+            } else {
+              unmapped |= kNackHost;
+              std::cerr << "libgeeps: server " << process_id_ << " ch " << ch.id << " could not map host oplog "
+                        << href.buffer_id << " of client " << client_id << " (" << why
+                        << "); asking for the rows by socket\n";
+            }
+          }
+          if (!unmapped) {
+            auto it = hmapped.find(href.buffer_id);
+            GP_CHECK_MSG(it != hmapped.end(), "unmapped host oplog " << href.buffer_id);
+            GP_CHECK_LE(href.offset + href.bytes, it->second->bytes());
+            b.split = head;
+            b.host_head =
+                reinterpret_cast<const float *>(static_cast<const char *>(it->second->data()) + href.offset);
+            b.head_keepalive = it->second;
+          }
         }
         auto &mapped = ch.ipc_oplogs[client_id];
         bool ok = true;
@@ -353,11 +395,14 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
                       << "); asking for the rows by socket\n";
           }
         }
-        if (ok) {
-          auto it = mapped.find(ref.buffer_id);
-          GP_CHECK_MSG(it != mapped.end(), "unmapped oplog buffer " << ref.buffer_id);
-          b.device_rows = reinterpret_cast<const float *>(static_cast<const char *>(it->second) + ref.offset);
-          b.stage = ch.stage_from[client_id];
+        if (!ok) unmapped |= kNackDevice;
+        if (!unmapped) {
+          if (ref.bytes) {  // (none: the table's rows are all in the host tier)
+            auto it = mapped.find(ref.buffer_id);
+            GP_CHECK_MSG(it != mapped.end(), "unmapped oplog buffer " << ref.buffer_id);
+            b.device_rows = reinterpret_cast<const float *>(static_cast<const char *>(it->second) + ref.offset);
+            b.stage = ch.stage_from[client_id];
+          }
         } else {
           // NACK, then hold the client's later frames back until the slice
           // comes again as a socket frame (the client sends it as soon as its
@@ -366,6 +411,7 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
           m.cmd = kCmdOplogNack;
           m.server_id = process_id_;
           m.table_id = h.table_id;
+          m.unmapped = unmapped;
           m.clock = h.clock;
           m.buffer_id = ref.buffer_id;
           GP_CHECK_MSG(send_to_client(ch, client_id, {Part{&m, sizeof m}}),
@@ -494,7 +540,8 @@ void ClientLib::resend_version(Channel &ch, uint32_t c, const VersionNackMsg &m,
 // still here (reclaimed only once every server's refresh covers the clock,
 // and this server's cannot before it has these rows), so the slice goes again
 // as an ordinary socket frame; push_updates exports a fresh buffer in place of
-// the NACKed one on its next use.
+// the NACKed one on its next use, or, when it was the shared host oplog the
+// server could not map, sends that server the host-tier rows in the frame.
 void ClientLib::resend_oplog(Channel &ch, uint32_t s, const OplogNackMsg &m, PinnedArray<float> &buf,
                              const Stream &st) {
   std::shared_ptr<DeviceArray<float>> oplog;
@@ -507,9 +554,11 @@ void ClientLib::resend_oplog(Channel &ch, uint32_t s, const OplogNackMsg &m, Pin
     GP_CHECK_LT(m.table_id, ch.tables.size());
     ParamCache &pc = ch.tables[m.table_id];
     auto it = pc.oplog.find(m.clock);
-    GP_CHECK_MSG(it != pc.oplog.end(), "server " << s << " NACKed clock " << m.clock << " of table " << m.table_id
-                                                 << ", whose oplog is gone");
-    oplog = it->second;
+    if (pc.num_rows || it != pc.oplog.end()) {  // (a table wholly in the host tier has no HBM oplog)
+      GP_CHECK_MSG(it != pc.oplog.end(), "server " << s << " NACKed clock " << m.clock << " of table "
+                                                   << m.table_id << ", whose oplog is gone");
+      oplog = it->second;
+    }
     a = pc.server_row_start[s];
     n = pc.server_num_rows[s];
     if (pc.cpu.num_rows) {
@@ -524,7 +573,12 @@ void ClientLib::resend_oplog(Channel &ch, uint32_t s, const OplogNackMsg &m, Pin
       keys = pc.row_keys;
       key0 = keys->data() + a;
     }
-    pc.ipc_nacked.emplace_back((size_t)(m.buffer_id & 0xffffffffu), s);
+    if (m.unmapped != kNackHost) pc.ipc_nacked.emplace_back((size_t)(m.buffer_id & 0xffffffffu), s);
+    if (m.unmapped & kNackHost) ch.host_share_off[s] = 1;  // its host-tier rows go in the frame from now on
+  }
+  if (m.unmapped & kNackHost) {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.nr_host_share_refused++;
   }
   const size_t floats = (cn + n) * ROW_DATA_SIZE;
   if (buf.size() < floats) buf.resize(floats);
@@ -1606,8 +1660,18 @@ std::shared_ptr<HostBuf> ClientLib::get_host_oplog(HostTier &cpu, iter_t clock) 
       break;
     }
   if (!buf) {
-    cpu.oplog_pool.push_back(std::make_shared<HostBuf>(cpu.num_rows * ROW_DATA_SIZE, config_.pinned_cpu_memory != 0));
+    bool share = host_share_;
+    if (share && ipc_fault_ == 2 && !ipc_fault_used_[2].exchange(true)) {
+      std::cerr << "libgeeps: GEEPS_TEST_IPC_FAULT=refuse: shared host oplog refused\n";
+      share = false;
+    }
+    cpu.oplog_pool.push_back(
+        std::make_shared<HostBuf>(cpu.num_rows * ROW_DATA_SIZE, config_.pinned_cpu_memory != 0, share));
     buf = cpu.oplog_pool.back();
+    if (host_share_ && !buf->shared()) {
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      stats_.nr_host_share_refused++;
+    }
   }
   buf->zero();
   cpu.oplog[clock] = buf;
@@ -1839,6 +1903,11 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
   std::vector<size_t> cstarts, ccounts;
   std::vector<std::shared_ptr<std::vector<RowKey>>> frame_keys;
   bool tiers = false, zero_filled = false;
+  // ... and, when the host oplog is shared memory, which same-node servers map
+  // it (app thread only) and which of them could not (their NACKs)
+  size_t hpool_id = 0;
+  std::vector<uint8_t> *hexported = nullptr;
+  std::vector<uint8_t> share_off;
   {
     std::lock_guard<std::mutex> lk(ch.mu);
     ParamCache &pc = ch.tables[table_id];
@@ -1858,11 +1927,19 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       cstarts = cpu.server_row_start;
       ccounts = cpu.server_num_rows;
       frame_keys = pc.frame_keys;
+      if (hoplog && hoplog->shared()) {
+        for (size_t k = 0; k < cpu.oplog_pool.size(); ++k)
+          if (cpu.oplog_pool[k] == hoplog) hpool_id = k;
+        if (cpu.exported.size() < cpu.oplog_pool.size())
+          cpu.exported.resize(cpu.oplog_pool.size(), std::vector<uint8_t>(num_processes_, 0));
+        hexported = &cpu.exported[hpool_id];
+        share_off = ch.host_share_off;
+      }
       // (the frames keep it alive; a same-node server's NACK needs it until
       // its refresh covers the clock, as the HBM oplog: recv_row_batch reclaims)
       bool ipc_servers = false;
       for (uint32_t s = 0; s < num_processes_; ++s) ipc_servers |= ipc_to(s);
-      if (hoplog && !config_.read_my_writes && !(ipc_servers && pc.num_rows)) cpu.oplog.erase(clock);
+      if (hoplog && !config_.read_my_writes && !ipc_servers) cpu.oplog.erase(clock);
     }
     if (pc.oplog_bad.size() < pc.oplog_pool.size()) pc.oplog_bad.resize(pc.oplog_pool.size(), 0);
     if (pc.exported.size() < pc.oplog_pool.size())
@@ -1881,6 +1958,8 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
     starts = pc.server_row_start;
     counts = pc.server_num_rows;
     keys = pc.row_keys;
+    if (pc.ipc_keys_sent.size() < num_processes_) pc.ipc_keys_sent.assign(num_processes_, 0);
+    keys_sent = &pc.ipc_keys_sent;
     bool ipc_readers = false;  // a same-node server reads its slice from this oplog
     for (uint32_t s = 0; s < num_processes_; ++s) ipc_readers |= ipc_to(s) && (counts[s] > 0 || tiers);
     if (oplog) {
@@ -1889,8 +1968,6 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       if (pc.exported.size() < pc.oplog_pool.size())
         pc.exported.resize(pc.oplog_pool.size(), std::vector<uint8_t>(num_processes_, 0));
       exported = &pc.exported[pool_id];
-      if (pc.ipc_keys_sent.size() < num_processes_) pc.ipc_keys_sent.assign(num_processes_, 0);
-      keys_sent = &pc.ipc_keys_sent;
       // reclaim_oplog now, unless it must outlive the refresh (read-my-writes
       // re-apply; same-node servers copying out of it): then recv_row_batch
       // reclaims it once every server's data age covers the clock.
@@ -1905,8 +1982,9 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
       // A table with host-tier rows: every frame is [host rows of s][HBM rows
       // of s] (push_updates_param_cache, clientlib-data.cpp:487-509).  The
       // in-process server gets the host part and the oplog slice in place; a
-      // same-node server the host part in the frame and the HBM part over IPC;
-      // any other server an ordinary socket frame (the reference's own path).
+      // same-node server the HBM part over IPC and the host part through the
+      // shared host oplog (or in the frame); any other server an ordinary
+      // socket frame (the reference's own path).
       const size_t ca = cstarts[s], cn = ccounts[s], a = starts[s], n = counts[s];
       if (s == process_id_) {
         UpdateBatch b;
@@ -1926,7 +2004,8 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
         ch.server->post_updates(std::move(b));
         continue;
       }
-      if (oplog && ipc_to(s) && [&] {
+      const bool host_shared = ipc_to(s) && cn && hexported && !share_off[s];
+      if (ipc_to(s) && (oplog ? [&] {
             if ((*exported)[s]) return true;
             IpcRowsRef probe{};
             if (ipc_export(probe.handle, oplog->data(), 0)) {
@@ -1937,27 +2016,54 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
             std::lock_guard<std::mutex> lk(stats_mu_);
             stats_.nr_ipc_export_refused++;
             return false;
-          }()) {
-        // Same-node server: the host-tier rows travel in the frame (from the
-        // pinned host oplog), the HBM rows stay in this oplog, mapped over IPC
+          }() : host_shared)) {
+        // Same-node server: the HBM rows stay in this oplog, mapped over IPC
+        // (none: every row of the table in the host tier); the host-tier rows
+        // stay in the shared host oplog, mapped by the server too (a 5th
+        // part), or travel in the frame
         cs_clock_with_updates_batch_msg_t h{};
         h.cmd = CLOCK_WITH_UPDATES_BATCH;
         h.client_id = process_id_;
         h.clock = clock;
         h.table_id = table_id;
+        HostRowsRef href{};
+        if (host_shared) {
+          href.buffer_id = ((uint64_t)table_id << 32) | (uint64_t)hpool_id;
+          href.offset = ca * kRowBytes;
+          href.bytes = cn * kRowBytes;
+          if (!(*hexported)[s]) {
+            href.has_handle = 1;
+            href.handle = hoplog->shared()->handle();
+            if (ipc_fault_ == 1 && !ipc_fault_used_[2].exchange(true)) {
+              href.handle.tag[15] ^= 0x5a;  // the server's tag check fails
+              std::cerr << "libgeeps: GEEPS_TEST_IPC_FAULT=tag: corrupted the tag of a shared host oplog\n";
+            }
+            (*hexported)[s] = 1;
+          }
+        }
         IpcRowsRef ref{};
-        ref.buffer_id = ((uint64_t)table_id << 32) | (uint64_t)pool_id;
-        ref.offset = a * kRowBytes;
-        ref.bytes = n * kRowBytes;
-        if (!(*exported)[s]) {
-          std::memcpy(ref.handle, ch_export_handle, sizeof ref.handle);
-          ref.has_handle = 1;
-          (*exported)[s] = 1;
+        if (oplog) {
+          ref.buffer_id = ((uint64_t)table_id << 32) | (uint64_t)pool_id;
+          ref.offset = a * kRowBytes;
+          ref.bytes = n * kRowBytes;
+          if (!(*exported)[s]) {
+            std::memcpy(ref.handle, ch_export_handle, sizeof ref.handle);
+            ref.has_handle = 1;
+            (*exported)[s] = 1;
+          }
         }
         const bool with_keys = !(*keys_sent)[s];
-        send_to_server(ch, s, {Part{&h, sizeof h},
-                               with_keys ? Part{frame_keys[s]->data(), (cn + n) * sizeof(RowKey)} : Part{nullptr, 0},
-                               Part{hoplog->data() + ca * ROW_DATA_SIZE, cn * kRowBytes}, Part{&ref, sizeof ref}});
+        const Part keys_part =
+            with_keys ? Part{frame_keys[s]->data(), (cn + n) * sizeof(RowKey)} : Part{nullptr, 0};
+        if (host_shared) {
+          send_to_server(ch, s, {Part{&h, sizeof h}, keys_part, Part{nullptr, 0}, Part{&ref, sizeof ref},
+                                 Part{&href, sizeof href}});
+          std::lock_guard<std::mutex> lk(stats_mu_);
+          stats_.nr_host_shared++;
+        } else {
+          send_to_server(ch, s, {Part{&h, sizeof h}, keys_part, Part{hoplog->data() + ca * ROW_DATA_SIZE, cn * kRowBytes},
+                                 Part{&ref, sizeof ref}});
+        }
         (*keys_sent)[s] = 1;
         continue;
       }

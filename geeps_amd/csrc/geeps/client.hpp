@@ -114,6 +114,8 @@ struct HostTier {
   std::vector<size_t> server_row_start, server_num_rows;
   std::map<iter_t, std::shared_ptr<HostBuf>> oplog;
   std::vector<std::shared_ptr<HostBuf>> oplog_pool;
+  // which shared oplog buffers each same-node server has mapped
+  std::vector<std::vector<uint8_t>> exported;  // [oplog pool index][server]
 };
 
 struct ParamCache {
@@ -190,8 +192,12 @@ struct ClientStats {
   // socket instead), peers' handles this process could not map (NACKed), and
   // rows this process resent after a peer's NACK
   uint64_t nr_ipc_export_refused = 0, nr_ipc_nack_sent = 0, nr_ipc_resent = 0;
-  // the host tier: param-cache rows placed there, and Reads / Updates of its ops
+  // the host tier: param-cache rows placed there, and Reads / Updates of its ops;
+  // frames to same-node servers whose host-tier rows the server read from the
+  // shared host oplog, and shared-memory buffers refused (by this system, or a
+  // server that could not map one: those rows then go in the frame)
   uint64_t rows_host_tier = 0, nr_read_host = 0, nr_update_host = 0;
+  uint64_t nr_host_shared = 0, nr_host_share_refused = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
 };
@@ -255,6 +261,11 @@ struct Channel {
   // takes refreshes in place (its ZMTP READY said so), and which master versions'
   // IPC handles it already has
   std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
+  // same-node clients' shared host oplogs (a table with a host tier)
+  std::vector<std::map<uint64_t, std::shared_ptr<SharedHostMem>>> host_oplogs;  // [client][buffer id]
+  // client side, [server]: it could not map a shared host oplog (its NACK),
+  // so the host-tier rows go to it in the frame (under mu)
+  std::vector<uint8_t> host_share_off;
   std::vector<uint8_t> ipc_client;                       // [client]
   // [process]: runs on another GPU of this node (its READY's PCI bus id)
   std::vector<uint8_t> other_gpu;
@@ -376,9 +387,13 @@ class ClientLib {
   bool direct_read_ = false;  // GEEPS_DIRECT_READ=1: Read buffers are read-only (§4)
   int stage_refresh_mode_ = -1;
   int reader_delay_us_ = 0;   // GEEPS_TEST_READER_DELAY_US (test hook)
-  // GEEPS_TEST_IPC_FAULT (test hook): 1 = "tag", 2 = "refuse" (ipc_export)
+  // GEEPS_TEST_IPC_FAULT (test hook): 1 = "tag", 2 = "refuse" (ipc_export;
+  // kind 2: a shared host oplog)
   int ipc_fault_ = 0;
-  std::atomic<bool> ipc_fault_used_[2] = {{false}, {false}};
+  std::atomic<bool> ipc_fault_used_[3] = {{false}, {false}, {false}};
+  // host oplogs are shared memory a same-node server maps (pinned_cpu_memory,
+  // a same-node peer; GEEPS_HOST_SHARE=0 sends their rows in the frame instead)
+  bool host_share_ = false;
   std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)
 
   std::vector<OpInfo> opseq_;

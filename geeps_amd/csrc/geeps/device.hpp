@@ -6,10 +6,14 @@
 // host library.
 
 #include <cstddef>
+#include <iostream>
+#include <memory>
+#include <string>
 #include <utility>
 
 #include "check.hpp"
 #include "gp_reduce.h"
+#include "hostshare.hpp"
 
 namespace geeps {
 
@@ -136,10 +140,22 @@ class PinnedArray {
 // memory past gpu_memory_capacity): page-locked when `pinned` (the config's
 // pinned_cpu_memory, default on), so its copies to and from HBM run at the
 // pinned PCIe rate; plain memory otherwise, as the reference's DataStorage::CPU.
+// `shareable` (pinned host oplogs with a same-node server): shared memory a
+// peer can map (hostshare.hpp), private pinned memory if the system refuses it.
 class HostBuf {
  public:
-  HostBuf(size_t n, bool pinned) : n_(n), pinned_(pinned) {
+  HostBuf(size_t n, bool pinned, bool shareable = false) : n_(n), pinned_(pinned) {
     if (!n) return;
+    if (pinned && shareable) {
+      std::string why;
+      shm_ = SharedHostMem::create(n * sizeof(float), &why);
+      if (shm_) {
+        p_ = static_cast<float *>(shm_->data());
+        return;
+      }
+      std::cerr << "libgeeps: shared host memory refused (" << why
+                << "); this host oplog's rows go to same-node servers by socket\n";
+    }
     if (pinned) {
       void *p = nullptr;
       GP_CALL(gp_malloc_host(&p, n * sizeof(float)));
@@ -149,7 +165,7 @@ class HostBuf {
     }
   }
   ~HostBuf() {
-    if (!p_) return;
+    if (!p_ || shm_) return;  // (shm_ unmaps itself)
     if (pinned_)
       gp_free_host(p_);
     else
@@ -160,8 +176,10 @@ class HostBuf {
   float *data() const { return p_; }
   size_t size() const { return n_; }
   void zero() { GP_CALL(gp_host_zero(n_, p_)); }  // zerofy_data_cpu, threaded when large
+  const SharedHostMem *shared() const { return shm_.get(); }  // null: private memory
 
  private:
+  std::unique_ptr<SharedHostMem> shm_;
   float *p_ = nullptr;
   size_t n_ = 0;
   bool pinned_ = false;

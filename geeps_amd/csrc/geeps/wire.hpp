@@ -52,6 +52,7 @@
 
 #include "geeps-user-defined-types.hpp"
 #include "gp_reduce.h"
+#include "hostshare.hpp"
 
 // Clock value of a table nobody has clocked yet, and the largest clock
 // (src/common/internal-config.hpp:34-36).
@@ -134,6 +135,19 @@ struct IpcRowsRef {
   uint8_t handle[kIpcHandleBytes];
 };
 
+// 5th part of a CLOCK_WITH_UPDATES_BATCH from a same-node client of a table
+// with a host tier (round 5): the host-tier rows stay in the client's host
+// oplog too, shared memory the server maps (hostshare.hpp), and part 2 is
+// empty.  The handle rides along on the first use of buffer_id per server.
+struct HostRowsRef {
+  uint64_t buffer_id;   // (table << 32) | host oplog pool index
+  uint64_t offset;      // bytes from the buffer base to this server's host-tier rows
+  uint64_t bytes;
+  uint32_t has_handle;  // first use of buffer_id: `handle` is valid
+  uint32_t pad;
+  geeps::HostShareHandle handle;
+};
+
 // 4th part of a READ_ROW_BATCH from a same-node server: the shard is the
 // server's master version `version`, which the client reads in place through
 // the IPC mapping of that version's buffer (the handle rides along the first
@@ -164,11 +178,15 @@ struct RefreshAckMsg {
 // reader holds the client's later frames back until the resend arrives, so
 // the server sees the client's messages in their order.
 constexpr command_t kCmdOplogNack = 103;
+// `unmapped`: kNackDevice, the HBM slice's buffer (replaced on its next use);
+// kNackHost, the host-tier rows' shared buffer (the client's frames to this
+// server then carry those rows again).
+constexpr uint32_t kNackDevice = 1, kNackHost = 2;
 struct OplogNackMsg {
   command_t cmd;
   uint32_t server_id;
   uint32_t table_id;
-  uint32_t pad;
+  uint32_t unmapped;
   iter_t clock;
   uint64_t buffer_id;
 };

@@ -3162,6 +3162,18 @@ int gp_free_host(void *ptr) {
   return GP_OK;
 }
 
+int gp_host_register(void *ptr, size_t bytes) {
+  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
+  if (bytes == 0) return GP_OK;
+  GP_HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return GP_OK;
+}
+
+int gp_host_unregister(void *ptr) {
+  if (ptr) GP_HIP_TRY(hipHostUnregister(ptr));
+  return GP_OK;
+}
+
 int gp_memcpy_async(void *dst, const void *src, size_t bytes, gp_stream s) {
   if (bytes == 0) return GP_OK;
   if (!dst || !src) return set_error(GP_ERR_INVALID, "null pointer");

@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 13  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 14  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -113,6 +113,8 @@ _SIGNATURES = {
     "gp_free_device": (_i, [_vp]),
     "gp_malloc_host": (_i, [_c.POINTER(_vp), _sz]),
     "gp_free_host": (_i, [_vp]),
+    "gp_host_register": (_i, [_vp, _sz]),
+    "gp_host_unregister": (_i, [_vp]),
     "gp_memcpy_async": (_i, [_vp, _vp, _sz, _vp]),
     "gp_memset_async": (_i, [_vp, _i, _sz, _vp]),
     "gp_stream_create": (_i, [_c.POINTER(_vp)]),

@@ -47,7 +47,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 13
+#define GP_ABI_VERSION 14
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -420,6 +420,12 @@ int gp_malloc_device_shared(void **ptr, size_t bytes);
 int gp_free_device(void *ptr);
 int gp_malloc_host(void **ptr, size_t bytes); /* pinned (mallocHost) */
 int gp_free_host(void *ptr);
+/* Page-lock an existing host range, and undo it (ABI 14): libgeeps' host-tier
+ * oplogs are shared memory mapped into a same-node peer process as well
+ * (DESIGN.md §4.1); each process registers its own mapping so that copies
+ * between it and HBM run at the pinned PCIe rate.  Unregister before unmapping. */
+int gp_host_register(void *ptr, size_t bytes);
+int gp_host_unregister(void *ptr);
 /* Direction inferred from the pointers (cudaMemcpyDefault in the reference). */
 int gp_memcpy_async(void *dst, const void *src, size_t bytes, gp_stream s);
 int gp_memset_async(void *dst, int value, size_t bytes, gp_stream s);

@@ -1,0 +1,23 @@
+#!/bin/bash
+# r05 dev10: shared host oplogs (a same-node server reads a client's host-tier
+# rows in place): the host tier / IPC recovery tests, the shared-memory
+# checks with page-locking, the timer breakdown shared vs in-frame, then the
+# UBSan build of libgeeps over the same tests.
+cd "$GRAFT_REPO_ROOT"
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r05dev10}; mkdir -p $O
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u -m pytest tests/test_hostshare.py tests/test_abi.py tests/test_libgeeps.py -v -k "hostshare or abi or host_tier or mm_level or ipc_failure" --timeout 150 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc $(tail -n 1 $O/pytest.log)"; grep FAILED $O/pytest.log | head; [ $rc -eq 0 ] || exit $rc
+for share in 1 0; do
+timeout -k 10 200 python -c "
+import json, sys
+sys.path.insert(0, 'scripts')
+import run_clock_bench as m
+r = m.run(2, 476292, 10, 5, 0, 'ipc', timeout=120, extra_env={'CLOCK_BENCH_HOST_TIER_FRAC': '0.5', 'GEEPS_HOST_SHARE': '$share'})
+print(json.dumps({'ms_per_clock': r['ms_per_clock'], 'read_ok': r['read_ok'], 'nr_host_shared': r['nr_host_shared'],
+                  'client': [s['client'] for s in r['stats']], 'servers': [s['servers'] for s in r['stats']]}))
+" > $O/host_tier_share$share.json 2> $O/host_tier_share$share.err; rc=$?
+echo "share=$share rc=$rc $(head -c 300 $O/host_tier_share$share.json)"; [ $rc -eq 0 ] || exit $rc
+done
+GEEPS_SUM_APP=$GRAFT_REPO_ROOT/build/ubsan/geeps_sum_app GEEPS_STRESS_CASES=40 timeout -k 10 600 python -u -m pytest tests/test_libgeeps.py -m gpu -v -k "host_tier or ipc_failure or randomized or rehearsal" --timeout 175 --timeout-method thread > $O/pytest_ubsan.log 2>&1; rc=$?
+echo "ubsan rc=$rc $(tail -n 1 $O/pytest_ubsan.log)"; grep -E "FAILED|runtime error" $O/pytest_ubsan.log | head; exit $rc

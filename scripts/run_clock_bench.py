@@ -132,6 +132,7 @@ def run(P, rows, clocks, warmup, slack=0, transport="ipc", timeout=900, extra_en
         out["nr_refresh_in_place"] = sum(s["client"]["nr_refresh_in_place"] for s in st)
         out["nr_read_direct"] = sum(s["client"]["nr_read_direct"] for s in st)
         out["rows_host_tier"] = sum(s["client"].get("rows_host_tier", 0) for s in st)
+        out["nr_host_shared"] = sum(s["client"].get("nr_host_shared", 0) for s in st)
     return out
 
 

@@ -575,6 +575,8 @@ HOST_TIER_LAYERS = [300, 200, 400, 100]
     (2, 1, 1, 0, "ipc", "int", 0, {}),  # every batch in the host tier
     (2, 0, 1, 0, "ipc", "int", 2, {"GEEPS_TEST_IPC_FAULT": "tag"}),  # NACK: the resend carries both parts
     (3, 1, 1, 0, "ipc", "int", 1, {"GEEPS_TEST_IPC_FAULT": "refuse"}),
+    (2, 0, 1, 0, "ipc", "int", 2, {"GEEPS_HOST_SHARE": "0"}),  # host-tier rows in the frames
+    (3, 0, 1, 0, "ipc", "int", 0, {"GEEPS_TEST_IPC_FAULT": "tag"}),  # no HBM part: a host-only NACK
 ])
 def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mode, gpu_layers, extra):
     """A gpu_memory_capacity that holds only the first `gpu_layers` key
@@ -585,7 +587,10 @@ def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mod
     split back, Reads gather on the host and copy up (clientlib-data.cpp:
     153-189, 280-344, 398-434, 487-509).  Every Read is checked exactly (float
     mode: bit for bit in the server's order; SSP bounds at slack > 0), with
-    read-my-writes, several channels, sockets and staged peers."""
+    read-my-writes, several channels, sockets and staged peers.  Same-node
+    servers read the host-tier rows from the client's shared host oplog
+    (nr_host_shared); a buffer the system refuses to share, or one a server
+    cannot map (NACK), sends those rows in the frame instead."""
     entries = slack + 1 if rmw else 1
     spec = ",".join(str(r) for r in HOST_TIER_LAYERS)
     rows = sum(HOST_TIER_LAYERS)
@@ -602,6 +607,16 @@ def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mod
         # every clock Reads and Updates each host-tier layer once (the setup
         # clock only Updates)
         assert c["nr_read_host"] == 6 * n_host_layers and c["nr_update_host"] == 7 * n_host_layers
+        print("shared host oplog frames / refused:", c["nr_host_shared"], c["nr_host_share_refused"])
+        fault = extra.get("GEEPS_TEST_IPC_FAULT")
+        if P == 1 or transport == "tcp" or extra.get("GEEPS_HOST_SHARE") == "0":
+            assert c["nr_host_shared"] == 0 and c["nr_host_share_refused"] == 0
+        elif fault:
+            # tag: its first shared buffer NACKed by one server (which then gets
+            # the rows in the frame); refuse: its first buffer was private memory
+            assert c["nr_host_share_refused"] == 1
+        else:
+            assert c["nr_host_share_refused"] == 0 and c["nr_host_shared"] >= 6 * (P - 1)
 
 
 @pytest.mark.gpu
