@@ -1629,13 +1629,20 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
   ch0.app_written.record_default();
   GP_CALL(gp_stream_wait_event(ch0.stream->get(), ch0.app_written.get()));
   if (vals) GP_CALL(gp_memcpy_async(cpu_buffer_.data(), pre.buffer.data(), vals * sizeof(float), ch0.stream->get()));
+  // the clock's host oplogs (zeroed when new) while the rows come down
+  std::vector<std::shared_ptr<HostBuf>> oplogs(channels_.size());
+  for (auto &chp : channels_) {
+    std::lock_guard<std::mutex> lk(chp->mu);
+    HostTier &cpu = chp->tables[pre.table_id].cpu;
+    if (cpu.num_rows) oplogs[chp->id] = get_host_oplog(cpu, clock);
+  }
   ch0.stream->sync();
   for (auto &chp : channels_) {
     Channel &ch = *chp;
     std::lock_guard<std::mutex> lk(ch.mu);
     HostTier &cpu = ch.tables[pre.table_id].cpu;
     if (cpu.num_rows == 0) continue;
-    auto oplog = get_host_oplog(cpu, clock);
+    const std::shared_ptr<HostBuf> &oplog = oplogs[ch.id];
     const size_t n = pre.ch_size[ch.id];
     if (!n) continue;
     const gp_double_index *idx = pre.host_index.data() + pre.ch_start[ch.id];
