@@ -1580,11 +1580,29 @@ bool ClientLib::read_batch(RowData **buffer, int handle) {
   return true;
 }
 
+namespace {
+// A host-tier op's rows cross PCIe in pieces of this many rows (16 MiB), so
+// that the CPU's gather or scatter-add of one piece overlaps the copy of the
+// next.
+constexpr size_t kHostPieceRows = (16u << 20) / kRowBytes;
+
+// The entries [lo, hi) of one channel's host DoubleIndex whose op-buffer row
+// (id0) lies in [r0, r1): create_double_index lists them in op-row order.
+std::pair<size_t, size_t> entries_in(const gp_double_index *idx, size_t n, size_t r0, size_t r1) {
+  auto below = [](const gp_double_index &d, size_t r) { return d.id0 < r; };
+  const gp_double_index *lo = std::lower_bound(idx, idx + n, r0, below);
+  const gp_double_index *hi = std::lower_bound(lo, idx + n, r1, below);
+  return {(size_t)(lo - idx), (size_t)(hi - idx)};
+}
+}  // namespace
+
 // A host-tier op's Read: per channel, wait for the data age and gather the
 // op's rows from the host cache into the pinned host buffer (read_batch_cpu,
-// assign_rows_to_double_index_cpu: clientlib-data.cpp:280-302); then one
+// assign_rows_to_double_index_cpu: clientlib-data.cpp:280-302); then the
 // host-to-device copy of num_vals_limit floats into the op buffer in HBM
-// (read_row_batch_param_cache, :233-250).
+// (read_row_batch_param_cache, :233-250).  The last channel gathers piece by
+// piece, and each piece's copy starts as soon as it is gathered (every
+// channel holds its lock for the whole of its gather, as in the reference).
 void ClientLib::read_batch_host(OpInfo &op) {
   const double t0 = now_s();
   const iter_t need = iteration_ - op.slack - 1;
@@ -1601,14 +1619,26 @@ void ClientLib::read_batch_host(OpInfo &op) {
                   << std::endl;
     }
     waited += now_s() - w0;
-    if (op.ch_size[ch.id])
-      GP_CALL(gp_host_gather_rows(cpu_buffer_.data(), pc.cpu.data->data(), op.host_index.data() + op.ch_start[ch.id],
-                                  op.ch_size[ch.id], gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit));
+    const gp_double_index *idx = op.host_index.data() + op.ch_start[ch.id];
+    const size_t n = op.ch_size[ch.id];
+    if (ch.id + 1 < channels_.size()) {
+      if (n)
+        GP_CALL(gp_host_gather_rows(cpu_buffer_.data(), pc.cpu.data->data(), idx, n, gp_double_index{0, 0},
+                                    ROW_DATA_SIZE, op.num_vals_limit));
+      continue;
+    }
+    const size_t vals = std::min(op.num_vals_limit, op.rows.size() * ROW_DATA_SIZE);
+    for (size_t r0 = 0; r0 * ROW_DATA_SIZE < vals; r0 += kHostPieceRows) {
+      const auto e = entries_in(idx, n, r0, r0 + kHostPieceRows);
+      if (e.second > e.first)
+        GP_CALL(gp_host_gather_rows(cpu_buffer_.data(), pc.cpu.data->data(), idx + e.first, e.second - e.first,
+                                    gp_double_index{0, 0}, ROW_DATA_SIZE, op.num_vals_limit));
+      const size_t f0 = r0 * ROW_DATA_SIZE, f1 = std::min(vals, (r0 + kHostPieceRows) * ROW_DATA_SIZE);
+      GP_CALL(gp_memcpy_async(op.buffer.data() + f0, cpu_buffer_.data() + f0, (f1 - f0) * sizeof(float),
+                              channels_[0]->stream->get()));
+    }
   }
-  const size_t vals = std::min(op.num_vals_limit, op.rows.size() * ROW_DATA_SIZE);
-  Channel &ch0 = *channels_[0];
-  if (vals) GP_CALL(gp_memcpy_async(op.buffer.data(), cpu_buffer_.data(), vals * sizeof(float), ch0.stream->get()));
-  ch0.stream->sync();
+  channels_[0]->stream->sync();
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.nr_read++;
   stats_.nr_read_host++;
@@ -1622,13 +1652,23 @@ void ClientLib::read_batch_host(OpInfo &op) {
 // (update_batch_param_cache, clientlib-data.cpp:309-323); then per channel,
 // under its lock, the clock's host oplog (zeroed when created) += the op's
 // rows through the host DoubleIndex, and with read-my-writes the host cache
-// too (update_batch_cpu, :398-434).
+// too (update_batch_cpu, :398-434).  The rows come down piece by piece, and
+// each piece is added as soon as it has landed (a row's adds keep their op
+// order: the pieces go in op-row order).
 void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
   const size_t vals = std::min(pre.num_vals_limit, pre.rows.size() * ROW_DATA_SIZE);
   Channel &ch0 = *channels_[0];
   ch0.app_written.record_default();
   GP_CALL(gp_stream_wait_event(ch0.stream->get(), ch0.app_written.get()));
-  if (vals) GP_CALL(gp_memcpy_async(cpu_buffer_.data(), pre.buffer.data(), vals * sizeof(float), ch0.stream->get()));
+  const size_t piece_vals = kHostPieceRows * ROW_DATA_SIZE;
+  const size_t pieces = (vals + piece_vals - 1) / piece_vals;
+  while (host_events_.size() < pieces) host_events_.push_back(std::make_unique<Event>());
+  for (size_t k = 0; k < pieces; ++k) {
+    const size_t f0 = k * piece_vals, f1 = std::min(vals, f0 + piece_vals);
+    GP_CALL(gp_memcpy_async(cpu_buffer_.data() + f0, pre.buffer.data() + f0, (f1 - f0) * sizeof(float),
+                            ch0.stream->get()));
+    host_events_[k]->record(*ch0.stream);
+  }
   // the clock's host oplogs (zeroed when new) while the rows come down
   std::vector<std::shared_ptr<HostBuf>> oplogs(channels_.size());
   for (auto &chp : channels_) {
@@ -1636,21 +1676,24 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
     HostTier &cpu = chp->tables[pre.table_id].cpu;
     if (cpu.num_rows) oplogs[chp->id] = get_host_oplog(cpu, clock);
   }
-  ch0.stream->sync();
-  for (auto &chp : channels_) {
-    Channel &ch = *chp;
-    std::lock_guard<std::mutex> lk(ch.mu);
-    HostTier &cpu = ch.tables[pre.table_id].cpu;
-    if (cpu.num_rows == 0) continue;
-    const std::shared_ptr<HostBuf> &oplog = oplogs[ch.id];
-    const size_t n = pre.ch_size[ch.id];
-    if (!n) continue;
-    const gp_double_index *idx = pre.host_index.data() + pre.ch_start[ch.id];
-    GP_CALL(gp_host_scatter_add_rows(oplog->data(), cpu_buffer_.data(), idx, n, gp_double_index{0, 0},
-                                     ROW_DATA_SIZE, pre.num_vals_limit));
-    if (config_.read_my_writes)
-      GP_CALL(gp_host_scatter_add_rows(cpu.data->data(), cpu_buffer_.data(), idx, n, gp_double_index{0, 0},
-                                       ROW_DATA_SIZE, pre.num_vals_limit));
+  for (size_t k = 0; k < pieces; ++k) {
+    host_events_[k]->sync();
+    for (auto &chp : channels_) {
+      Channel &ch = *chp;
+      const size_t n = pre.ch_size[ch.id];
+      if (!n || !oplogs[ch.id]) continue;
+      const gp_double_index *idx = pre.host_index.data() + pre.ch_start[ch.id];
+      const auto e = entries_in(idx, n, k * kHostPieceRows, (k + 1) * kHostPieceRows);
+      if (e.second == e.first) continue;
+      std::lock_guard<std::mutex> lk(ch.mu);
+      GP_CALL(gp_host_scatter_add_rows(oplogs[ch.id]->data(), cpu_buffer_.data(), idx + e.first,
+                                       e.second - e.first, gp_double_index{0, 0}, ROW_DATA_SIZE,
+                                       pre.num_vals_limit));
+      if (config_.read_my_writes)
+        GP_CALL(gp_host_scatter_add_rows(ch.tables[pre.table_id].cpu.data->data(), cpu_buffer_.data(),
+                                         idx + e.first, e.second - e.first, gp_double_index{0, 0}, ROW_DATA_SIZE,
+                                         pre.num_vals_limit));
+    }
   }
 }
 

@@ -400,6 +400,7 @@ class ClientLib {
   // the reference's thread cpu_buffer (mallocHost, clientlib-viter.cpp:444-447):
   // host-tier ops' rows on their way to / from the op buffer in HBM
   PinnedArray<float> cpu_buffer_;
+  std::vector<std::unique_ptr<Event>> host_events_;  // the pieces of a host-tier Update's copy
   std::map<std::vector<row_idx_t>, std::unique_ptr<DeviceArray<float>>> local_storage_;
   std::vector<size_t> rows_per_channel_;
   std::vector<std::unique_ptr<Channel>> channels_;

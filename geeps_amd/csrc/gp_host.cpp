@@ -14,13 +14,24 @@
 //     order, from one thread (the reference's loop is one thread; a host tier
 //     of a large table is memory-bound, and one core reads ~10 GB/s).
 //     Threads: GP_HOST_THREADS, else OMP_NUM_THREADS, else the hardware's,
-//     at most 32; calls under 4 MiB of rows stay on the calling thread.
+//     at most 32; calls under 4 MiB of rows stay on the calling thread.  The
+//     helper threads are a persistent pool (a host tier calls these several
+//     times a clock, and starting 15 threads per call cost more than the
+//     copies it overlaps).
+#include <pthread.h>
+
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "gp_reduce.h"
@@ -60,6 +71,89 @@ unsigned host_threads() {
 
 constexpr size_t kParallelBytes = 4u << 20;
 
+// Worker threads shared by every caller (the app thread and libgeeps' reader
+// threads call these concurrently).  A call queues its tasks 1 .. t-1, runs
+// task 0, then runs any of its own tasks no worker has taken yet, and waits
+// for the rest.  Workers start on first need and are never joined (the
+// process's exit ends them); a forked child starts a pool of its own.
+class Pool {
+ public:
+  static Pool &get() {
+    static std::once_flag once;
+    std::call_once(once, [] { pthread_atfork(nullptr, nullptr, [] { instance().store(nullptr); }); });
+    Pool *p = instance().load(std::memory_order_acquire);
+    if (p) return *p;
+    Pool *mine = new Pool();  // (leaked on purpose, see above)
+    if (instance().compare_exchange_strong(p, mine, std::memory_order_acq_rel)) return *mine;
+    delete mine;  // another thread's came first
+    return *p;
+  }
+
+  void run(unsigned t, const std::function<void(unsigned)> &task) {
+    Call c;
+    c.task = &task;
+    c.left = t - 1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while (workers_ < t - 1) {
+        std::thread([this] { work(); }).detach();
+        ++workers_;
+      }
+      for (unsigned k = 1; k < t; ++k) q_.emplace_back(&c, k);
+    }
+    cv_.notify_all();
+    task(0);
+    for (;;) {  // this call's tasks still queued
+      unsigned k = 0;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = std::find_if(q_.begin(), q_.end(), [&](const std::pair<Call *, unsigned> &e) { return e.first == &c; });
+        if (it == q_.end()) break;
+        k = it->second;
+        q_.erase(it);
+      }
+      task(k);
+      finish(&c);
+    }
+    std::unique_lock<std::mutex> lk(c.mu);
+    c.cv.wait(lk, [&] { return c.left == 0; });
+  }
+
+ private:
+  struct Call {
+    const std::function<void(unsigned)> *task = nullptr;
+    unsigned left = 0;  // under mu
+    std::mutex mu;
+    std::condition_variable cv;
+  };
+  static std::atomic<Pool *> &instance() {
+    static std::atomic<Pool *> p{nullptr};
+    return p;
+  }
+  // (under c->mu to the end: the caller may return as soon as it sees 0)
+  static void finish(Call *c) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (--c->left == 0) c->cv.notify_one();
+  }
+  void work() {
+    for (;;) {
+      std::pair<Call *, unsigned> e;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        e = q_.front();
+        q_.pop_front();
+      }
+      (*e.first->task)(e.second);
+      finish(e.first);
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::pair<Call *, unsigned>> q_;
+  unsigned workers_ = 0;
+};
+
 // Runs body(lo, hi) over [0, n) split into contiguous ranges, one per thread
 // (the calling thread takes the first).
 template <typename F>
@@ -69,15 +163,11 @@ void parallel_ranges(size_t n, size_t bytes, F &&body) {
     body((size_t)0, n);
     return;
   }
-  std::vector<std::thread> pool;
-  pool.reserve(t - 1);
   const size_t per = (n + t - 1) / t;
-  for (unsigned k = 1; k < t; ++k) {
+  Pool::get().run(t, [&](unsigned k) {
     const size_t lo = std::min(n, k * per), hi = std::min(n, lo + per);
-    if (lo < hi) pool.emplace_back([&body, lo, hi] { body(lo, hi); });
-  }
-  body((size_t)0, std::min(n, per));
-  for (auto &th : pool) th.join();
+    if (lo < hi) body(lo, hi);
+  });
 }
 
 // The destination rows an index writes, [lo, hi) (offsets applied), for the

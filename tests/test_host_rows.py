@@ -113,3 +113,58 @@ def test_host_row_ops_reject_bad_arguments_and_skip_empty_calls():
     assert L.gp_host_add(4, None, None) == 1
     with pytest.raises(ValueError):
         rowops.add_rows_from_double_index_cpu(y, y.astype(np.float64), np.zeros((1, 2), np.int64))
+
+
+def test_host_row_ops_from_concurrent_callers():
+    """The helper threads are one persistent pool shared by every caller
+    (libgeeps' app thread and its reader threads call these at once): 6
+    threads, each running large scatter-adds on its own rows, all bit-exact."""
+    import threading
+    rng = np.random.default_rng(7)
+    W, n_op, n_cache = 128, 20000, 24000
+    cases = []
+    for _ in range(6):
+        idx = _index(rng, "permuted", n_op, n_cache)
+        x = rng.standard_normal(n_op * W).astype(np.float32)
+        y = rng.standard_normal(n_cache * W).astype(np.float32)
+        e = y.copy()
+        oracle.add_rows_from_double_index(e, x, idx, (0, 0), W, n_op * W)
+        cases.append((idx, x, y, e))
+    errors = []
+
+    def run(c):
+        idx, x, y, e = c
+        try:
+            for _ in range(3):
+                y0 = y.copy()
+                rowops.add_rows_from_double_index_cpu(y0, x, idx, (0, 0), W, n_op * W)
+                assert np.array_equal(bits(y0), bits(e))
+        except Exception as ex:  # noqa: BLE001 (reported below)
+            errors.append(ex)
+    ts = [threading.Thread(target=run, args=(c,)) for c in cases]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors and not any(t.is_alive() for t in ts)
+
+
+def test_host_row_ops_after_fork():
+    """A forked child (the pool's threads are not copied into it) starts a
+    pool of its own instead of waiting on the parent's workers."""
+    import os
+    n = (8 << 20) + 3
+    y = np.ones(n, np.float32)
+    rowops.add_row_batch_cpu(y, np.ones(n, np.float32))  # the parent's pool is up
+    pid = os.fork()
+    if pid == 0:
+        code = 1
+        try:
+            z = np.ones(n, np.float32)
+            rowops.add_row_batch_cpu(z, np.ones(n, np.float32))
+            code = 0 if (z == 2).all() else 2
+        finally:
+            os._exit(code)
+    _, status = os.waitpid(pid, 0)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+    assert (y == 2).all()

@@ -620,6 +620,28 @@ def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mod
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P,channels,rmw,mode,shuffle", [(1, 1, 0, "float", None), (2, 2, 1, "int", "1"),
+                                                         (2, 1, 0, "int", "odd")])
+def test_host_tier_moves_large_ops_in_pieces(dev, P, channels, rmw, mode, shuffle):
+    """Host-tier ops of 40,000 to 90,000 rows (20-45 MB): their Updates come
+    down and are added, and their Reads are gathered and go up, in 16-MiB
+    pieces that overlap the copies with the CPU work.  A row's adds keep their
+    op order across pieces; shuffled update rows spread each piece over the
+    whole host cache.  Every Read is checked exactly (float mode: bit for bit)."""
+    layers = [70000, 40000, 90000]
+    spec = ",".join(str(r) for r in layers)
+    cap = _host_tier_capacity(layers, 1, 1)  # (slack 0: one oplog entry with read-my-writes too)
+    extra = {"GEEPS_TEST_CAPACITY": str(cap)}
+    if shuffle:
+        extra["GEEPS_TEST_SHUFFLE_UPDATES"] = shuffle
+    outs = _run_app_layers(P, sum(layers), spec, clocks=4, slack=0, channels=channels, rmw=rmw, mode=mode,
+                           extra_env=extra, timeout=300)
+    for s in _stats(outs):
+        assert s["client"]["rows_host_tier"] == 130000
+        assert s["client"]["nr_update_host"] == 5 * 2 and s["client"]["nr_read_host"] == 4 * 2
+
+
+@pytest.mark.gpu
 def test_capacity_mm_level_3_refuses_a_host_tier(dev):
     """mm_warning_level 3 keeps all parameter cache in GPU memory: a key batch
     past gpu_memory_capacity fails FinishVirtualIteration, as the reference's
