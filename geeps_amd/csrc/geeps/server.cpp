@@ -224,7 +224,7 @@ void TabletServer::run() {
 
 // A staging bucket no pending bucket references.  At most kMaxPendingBuckets
 // exist per table (the queue is applied when it reaches that many, which
-// frees them all); the client's memory plan counts them (client.cpp,
+// frees them all); the client's memory plan counts them (client_viter.cpp,
 // FinishVirtualIteration).
 std::shared_ptr<DeviceArray<float>> TabletServer::stage_buffer(DataTable &t) {
   for (auto &b : t.stage_pool)

@@ -43,7 +43,7 @@
 // thread may be blocked in a Read of another table waiting on this very
 // server.  A client therefore keeps at most ONE such deferred version per
 // (server, table) -- a Read that would pin a second one gathers instead
-// (client.cpp, read_batch).  Of the clients + 1 versions other than the one
+// (client_data.cpp, read_batch).  Of the clients + 1 versions other than the one
 // being replaced, at most `clients` are then deferred, so at least one is free
 // or held only by readers that will catch up: the wait always ends.
 

@@ -216,7 +216,7 @@ def test_libzmq_client_pushes_to_a_libgeeps_tablet(rows):
 
 def test_non_zmtp_peer_fails_the_handshake_loudly():
     """A peer that is not a ZMTP 3 endpoint ends the handshake with a message
-    naming why (the product aborts with it; GP_CHECK_MSG in client.cpp)."""
+    naming why (the product aborts with it; GP_CHECK_MSG in client_net.cpp)."""
     port = free_port()
     ls = socket.socket()
     ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
