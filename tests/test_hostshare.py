@@ -96,3 +96,17 @@ def test_malformed_handle_is_refused():
         assert rc == 3 and "malformed" in out, out
     finally:
         o.close()
+
+
+@pytest.mark.gpu
+def test_buffers_are_page_locked_on_a_gpu_box():
+    """With a GPU, the owner's buffer is page-locked (gp_host_register, C-ABI
+    14), so the server's host-to-device copy out of it runs at the pinned
+    rate; a peer's mapping of it reads the owner's rows as on the CPU."""
+    o = Owner(1 << 22)
+    try:
+        assert o.pinned == "1"
+        rc, out = _open(o.args())
+        assert (rc, out) == (0, "ok")
+    finally:
+        o.close()
