@@ -35,6 +35,7 @@ std::string ClientStats::to_json() const {
     << ", \"nr_ipc_resent\": " << nr_ipc_resent << ", \"rows_host_tier\": " << rows_host_tier
     << ", \"nr_read_host\": " << nr_read_host << ", \"nr_update_host\": " << nr_update_host
     << ", \"nr_host_shared\": " << nr_host_shared << ", \"nr_host_share_refused\": " << nr_host_share_refused
+    << ", \"nr_update_host_init\": " << nr_update_host_init
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time

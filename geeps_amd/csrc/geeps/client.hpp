@@ -198,6 +198,7 @@ struct ClientStats {
   // server that could not map one: those rows then go in the frame)
   uint64_t rows_host_tier = 0, nr_read_host = 0, nr_update_host = 0;
   uint64_t nr_host_shared = 0, nr_host_share_refused = 0;
+  uint64_t nr_update_host_init = 0;  // host-tier Updates through the fused oplog init
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
 };
@@ -224,6 +225,9 @@ struct Channel {
   // Per table: the clock's update ops write every oplog row of this channel
   // exactly once, so the first touch may be gp_scatter_init_rows (fused zero).
   std::vector<bool> init_ok;
+  // The same for the host tier's oplog (its update ops write every host-tier
+  // row once): gp_host_scatter_init_rows, and the oplog is never zeroed.
+  std::vector<bool> host_init_ok;
   // Two HIP streams per channel: `stream` for the app thread's work (Read
   // gathers, Update scatters, push copies) and `svc_stream` for the service
   // side (this channel's tablet server and its socket reader threads).  Every
@@ -336,7 +340,7 @@ class ClientLib {
   // storage, clientlib-viter.cpp:160-490: GPU local storage + a thread cache
   // of twice the peak op rows), in RowData rows out of ngr_capacity.
   size_t reference_ngr_used(size_t ngr_capacity);
-  std::shared_ptr<HostBuf> get_host_oplog(HostTier &cpu, iter_t clock);
+  std::shared_ptr<HostBuf> get_host_oplog(HostTier &cpu, iter_t clock, bool zero = true);
   void read_batch_host(OpInfo &op);
   void update_batch_host(OpInfo &pre, iter_t clock);
   void reclaim_oplogs(ParamCache &pc, iter_t upto);

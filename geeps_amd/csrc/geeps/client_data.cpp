@@ -197,12 +197,20 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
                             ch0.stream->get()));
     host_events_[k]->record(*ch0.stream);
   }
-  // the clock's host oplogs (zeroed when new) while the rows come down
+  // the clock's host oplogs (zeroed when new, unless this clock's host-tier
+  // update ops write every row once: then each row's first write is the
+  // fused init 0.0f + x) while the rows come down
   std::vector<std::shared_ptr<HostBuf>> oplogs(channels_.size());
+  std::vector<uint8_t> fused(channels_.size(), 0);
   for (auto &chp : channels_) {
     std::lock_guard<std::mutex> lk(chp->mu);
     HostTier &cpu = chp->tables[pre.table_id].cpu;
-    if (cpu.num_rows) oplogs[chp->id] = get_host_oplog(cpu, clock);
+    fused[chp->id] = started_ && chp->host_init_ok[pre.table_id];
+    if (cpu.num_rows) oplogs[chp->id] = get_host_oplog(cpu, clock, /*zero=*/!fused[chp->id]);
+  }
+  if (std::find(fused.begin(), fused.end(), 1) != fused.end()) {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.nr_update_host_init++;
   }
   for (size_t k = 0; k < pieces; ++k) {
     host_events_[k]->sync();
@@ -214,9 +222,9 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
       const auto e = entries_in(idx, n, k * kHostPieceRows, (k + 1) * kHostPieceRows);
       if (e.second == e.first) continue;
       std::lock_guard<std::mutex> lk(ch.mu);
-      GP_CALL(gp_host_scatter_add_rows(oplogs[ch.id]->data(), cpu_buffer_.data(), idx + e.first,
-                                       e.second - e.first, gp_double_index{0, 0}, ROW_DATA_SIZE,
-                                       pre.num_vals_limit));
+      GP_CALL((fused[ch.id] ? gp_host_scatter_init_rows : gp_host_scatter_add_rows)(
+          oplogs[ch.id]->data(), cpu_buffer_.data(), idx + e.first, e.second - e.first, gp_double_index{0, 0},
+          ROW_DATA_SIZE, pre.num_vals_limit));
       if (config_.read_my_writes)
         GP_CALL(gp_host_scatter_add_rows(ch.tables[pre.table_id].cpu.data->data(), cpu_buffer_.data(),
                                          idx + e.first, e.second - e.first, gp_double_index{0, 0}, ROW_DATA_SIZE,
@@ -228,7 +236,7 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
 // create_oplog_entry + zerofy_data_cpu (clientlib-data.cpp:412-417): a pooled
 // host buffer once nothing (a pending push, the in-process server's bucket)
 // references it.
-std::shared_ptr<HostBuf> ClientLib::get_host_oplog(HostTier &cpu, iter_t clock) {
+std::shared_ptr<HostBuf> ClientLib::get_host_oplog(HostTier &cpu, iter_t clock, bool zero) {
   auto it = cpu.oplog.find(clock);
   if (it != cpu.oplog.end()) return it->second;
   std::shared_ptr<HostBuf> buf;
@@ -251,7 +259,7 @@ std::shared_ptr<HostBuf> ClientLib::get_host_oplog(HostTier &cpu, iter_t clock) 
       stats_.nr_host_share_refused++;
     }
   }
-  buf->zero();
+  if (zero) buf->zero();
   cpu.oplog[clock] = buf;
   return buf;
 }

@@ -374,6 +374,7 @@ void ClientLib::decide_fused_init() {
   for (auto &chp : channels_) {
     Channel &ch = *chp;
     ch.init_ok.assign(config_.num_tables, false);
+    ch.host_init_ok.assign(config_.num_tables, false);
     if (clock_handle_ < 0) continue;
     for (uint32_t t = 0; t < config_.num_tables; ++t) {
       const ParamCache &pc = ch.tables[t];
@@ -406,6 +407,25 @@ void ClientLib::decide_fused_init() {
       // so no refresh sees it unwritten: the fused init stays.  With several,
       // a refresh between two of them would: zeroed oplog.
       ch.init_ok[t] = ok && covered == pc.num_rows && (!config_.read_my_writes || writers == 1);
+      // The host tier's oplog, likewise from its own (host-tier) update ops.
+      // Not with read-my-writes: a host-tier Update adds piece by piece, each
+      // under the channel lock, so a refresh between pieces would re-apply
+      // rows not yet written this clock.
+      std::vector<uint8_t> hseen(pc.cpu.num_rows, 0);
+      size_t hcovered = 0;
+      bool hok = pc.cpu.num_rows > 0 && !config_.read_my_writes;
+      for (size_t i = 0; i < end && hok; ++i) {
+        const OpInfo &w = opseq_[i];
+        if (w.type != OpInfo::WRITE || w.local || w.table_id != t || !w.cpu) continue;
+        const OpInfo &pre = opseq_[w.prestep_handle];
+        if (pre.num_vals_limit < pre.rows.size() * ROW_DATA_SIZE) hok = false;
+        for (row_idx_t r : pre.rows) {
+          if (channel_of(t, r) != ch.id) continue;
+          if (hseen[pc.cpu.index.at(r)]++) hok = false;
+          ++hcovered;
+        }
+      }
+      ch.host_init_ok[t] = hok && hcovered == pc.cpu.num_rows;
     }
   }
   // Direct oplog: an update op whose rows are one channel's cache rows in

@@ -1,4 +1,4 @@
-// Host-memory row ops of the C-ABI (include/gp_reduce.h, ABI 13): the
+// Host-memory row ops of the C-ABI (include/gp_reduce.h, ABI 13-15): the
 // reference's CPU twins of the row ops (src/common/row-op-util.hpp:64-139),
 // which libgeeps' host tier runs on the rows a param cache keeps in host
 // memory past `gpu_memory_capacity` (src/client/clientlib-viter.cpp:492-611).
@@ -31,6 +31,7 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -204,6 +205,46 @@ int gp_host_scatter_add_rows(float *y, const float *x, const gp_double_index *in
       float *__restrict__ ys = y + to * row_size;
       // the guard is on the source (x) index, row-op-util.hpp:133-135
       guarded_row(from * row_size, row_size, num_vals_limit, [&](size_t v) { ys[v] += xs[v]; });
+    }
+  });
+  return GP_OK;
+}
+
+int gp_host_scatter_init_rows(float *y, const float *x, const gp_double_index *index, size_t num_rows,
+                              gp_double_index offset, size_t row_size, size_t num_vals_limit) {
+  if (num_rows == 0) return GP_OK;
+  if (!y || !x || !index || row_size == 0) return host_error("gp_host_scatter_init_rows: bad argument");
+  size_t d0 = 0, d1 = 0;
+  const size_t bytes = num_rows * row_size * sizeof(float);
+  dest_span<true>(index, num_rows, offset, &d0, &d1);
+  parallel_ranges(d1 - d0, bytes, [&](size_t lo, size_t hi) {
+    // a destination's first entry initialises it (0.0f + x, 0.0f past the
+    // limit: the zerofied row plus its add), any later one adds, in entry
+    // order: zerofy + add for any index, repeated destinations included
+    const bool dense = hi - lo <= 8 * num_rows + 1024;
+    std::vector<uint8_t> seen(dense ? hi - lo : 0, 0);
+    std::unordered_set<size_t> seen_sparse;
+    for (size_t i = 0; i < num_rows; ++i) {
+      const size_t from = index[i].id0 + offset.id0, to = index[i].id1 + offset.id1;
+      if (to < d0 + lo || to >= d0 + hi) continue;
+      bool first;
+      if (dense) {
+        uint8_t &s = seen[to - d0 - lo];
+        first = !s;
+        s = 1;
+      } else {
+        first = seen_sparse.insert(to).second;
+      }
+      const float *__restrict__ xs = x + from * row_size;
+      float *__restrict__ ys = y + to * row_size;
+      const size_t base = from * row_size;
+      if (!first) {
+        guarded_row(base, row_size, num_vals_limit, [&](size_t v) { ys[v] += xs[v]; });
+      } else if (base + row_size <= num_vals_limit) {
+        for (size_t v = 0; v < row_size; ++v) ys[v] = 0.0f + xs[v];
+      } else {
+        for (size_t v = 0; v < row_size; ++v) ys[v] = base + v < num_vals_limit ? 0.0f + xs[v] : 0.0f;
+      }
     }
   });
   return GP_OK;

@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 14  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 15  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -100,6 +100,7 @@ _SIGNATURES = {
     "gp_bucket_sum_launch_plan": (_i, [_sz, _i, _c.POINTER(SumPlan)]),
     "gp_add": (_i, [_sz, _vp, _vp, _vp, _vp]),
     "gp_host_scatter_add_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz]),
+    "gp_host_scatter_init_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz]),
     "gp_host_gather_rows": (_i, [_vp, _vp, _vp, _sz, DoubleIndex, _sz, _sz]),
     "gp_host_add": (_i, [_sz, _vp, _vp]),
     "gp_host_zero": (_i, [_sz, _vp]),

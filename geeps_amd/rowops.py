@@ -475,6 +475,20 @@ def add_rows_from_double_index_cpu(rows_y, rows_x, index, index_offset=None, row
           "gp_host_scatter_add_rows")
 
 
+def init_rows_from_double_index_cpu(rows_y, rows_x, index, index_offset=None, row_size=ROW_DATA_SIZE,
+                                    num_vals_limit=None) -> None:
+    """``y[(id1+off1)*W + v] = 0.0f + x[(id0+off0)*W + v]`` (0.0f past the limit)
+    in host memory: zerofy_data_cpu of the destination rows + the reference's
+    add (row-op-util.hpp:121-139), fused -- gp_host_scatter_init_rows."""
+    _host_f32(rows_y, "rows_y")
+    _host_f32(rows_x, "rows_x")
+    _host_index(index)
+    limit = (1 << 64) - 1 if num_vals_limit is None else num_vals_limit
+    check(native.lib().gp_host_scatter_init_rows(rows_y.ctypes.data, rows_x.ctypes.data, index.ctypes.data,
+                                                 index.shape[0], _as_offset(index_offset), row_size, limit),
+          "gp_host_scatter_init_rows")
+
+
 def assign_rows_to_double_index_cpu(rows_y, rows_x, index, index_offset=None, row_size=ROW_DATA_SIZE,
                                     num_vals_limit=None) -> None:
     """``y[(id0+off0)*W + v] = x[(id1+off1)*W + v]`` in host memory (reference

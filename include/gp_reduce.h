@@ -47,7 +47,7 @@ extern "C" {
 #define GP_ERR_UNSUPPORTED 3
 
 /* Library ABI version; bumped on any signature change. */
-#define GP_ABI_VERSION 14
+#define GP_ABI_VERSION 15
 
 /* {id0, id1} pair, 16 bytes, identical layout to the reference's
  * `struct DoubleIndex { size_t id0; size_t id1; }`
@@ -390,6 +390,14 @@ int gp_zero(float *y, size_t num_vals, gp_stream s);
  * -- add_rows_from_double_index_cpu (src/common/row-op-util.hpp:121-139). */
 int gp_host_scatter_add_rows(float *y, const float *x, const gp_double_index *index, size_t num_rows,
                              gp_double_index offset, size_t row_size, size_t num_vals_limit);
+/* The fused zerofy + scatter-add (ABI 15): the same bits as zerofy_data_cpu
+ * of the listed destination rows, then add_rows_from_double_index_cpu.  A
+ * destination's first entry writes 0.0f + x[(id0+off0)*W + v] (0.0f where
+ * that x index is at or past the limit), later ones add, in entry order.
+ * libgeeps' host tier uses it when a clock's update ops write every host
+ * oplog row once: the oplog is then never zeroed. */
+int gp_host_scatter_init_rows(float *y, const float *x, const gp_double_index *index, size_t num_rows,
+                              gp_double_index offset, size_t row_size, size_t num_vals_limit);
 /* y[(id0+off0)*W + v] = x[(id1+off1)*W + v] where (id0+off0)*W + v < limit
  * -- assign_rows_to_double_index_cpu (src/common/row-op-util.hpp:81-99). */
 int gp_host_gather_rows(float *y, const float *x, const gp_double_index *index, size_t num_rows,

@@ -204,6 +204,10 @@ static void row_cases(void) {
   oracle_add_rows_from_double_index(want, hx, idx, rows, off0, off1, W, limit);
   expect_same("gp_scatter_init_rows_planned", got, want, y_vals);
   CALL(gp_row_plan_destroy(plan));
+  /* the host-memory fused init (ABI 15) against the same zerofy + add */
+  memcpy(got, hy, y_vals * sizeof(float));
+  CALL(gp_host_scatter_init_rows(got, hx, (const gp_double_index *)idx, rows, off, W, limit));
+  expect_same("gp_host_scatter_init_rows", got, want, y_vals);
 
   /* 4. gather: y[id0 + off0] = x[id1 + off1], the limit on the destination */
   {

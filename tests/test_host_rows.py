@@ -168,3 +168,34 @@ def test_host_row_ops_after_fork():
     _, status = os.waitpid(pid, 0)
     assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
     assert (y == 2).all()
+
+
+@pytest.mark.parametrize("W,limit_frac,off", [(128, 1.0, (0, 0)), (128, 0.61, (0, 0)), (33, 0.5, (2, 3)),
+                                              (1024, 0.93, (0, 0))])
+@pytest.mark.parametrize("threaded", [False, True])
+@pytest.mark.parametrize("kind", ["permuted", "repeated", "sparse"])
+def test_host_init_is_zerofy_then_add(W, limit_frac, off, threaded, kind):
+    """gp_host_scatter_init_rows (ABI 15), the host tier's fused oplog init:
+    bit for bit the oracle's zerofy of the destination rows then its add,
+    -0.0 deltas included (0.0f + -0.0f = +0.0f), and rows wholly or partly
+    past num_vals_limit zero where the add contributed nothing."""
+    rng = np.random.default_rng(11 + W)
+    n_op = (40000 if threaded else 300) if W <= 128 else (5000 if threaded else 40)
+    n_cache = n_op + 17
+    idx = _index(rng, "permuted" if kind == "sparse" else kind, n_op, n_cache)[:n_op].copy()
+    if kind == "repeated":
+        idx[::7, 1] = idx[0, 1]  # one destination listed n_op / 7 times: init, then adds in entry order
+    if kind == "sparse":
+        idx[:, 1] *= 64  # destinations 64 rows apart: the per-thread set, not the bitmap
+        n_cache = int(idx[:, 1].max()) + 1
+    x = rng.standard_normal((n_op + off[0]) * W).astype(np.float32)
+    x[::5] = np.float32(-0.0)
+    limit = int(len(x) * limit_frac)
+    y = np.full((n_cache + off[1]) * W, np.float32(7.25))
+    e = y.copy()
+    rows = np.unique(idx[:, 1]) + off[1]
+    for r in rows:
+        e[r * W:(r + 1) * W] = 0.0
+    oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
+    rowops.init_rows_from_double_index_cpu(y, x, idx, off, W, limit)
+    assert np.array_equal(bits(y), bits(e))

@@ -607,7 +607,12 @@ def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mod
         # every clock Reads and Updates each host-tier layer once (the setup
         # clock only Updates)
         assert c["nr_read_host"] == 6 * n_host_layers and c["nr_update_host"] == 7 * n_host_layers
-        print("shared host oplog frames / refused:", c["nr_host_shared"], c["nr_host_share_refused"])
+        print("shared host oplog frames / refused:", c["nr_host_shared"], c["nr_host_share_refused"],
+              "fused host inits:", c["nr_update_host_init"])
+        # every layer is updated once a clock, so after StartIterations the host
+        # oplog's rows are each written once: the fused init (not with
+        # read-my-writes, whose refreshes could fall between an Update's pieces)
+        assert c["nr_update_host_init"] == (0 if rmw else 6 * n_host_layers)
         fault = extra.get("GEEPS_TEST_IPC_FAULT")
         if P == 1 or transport == "tcp" or extra.get("GEEPS_HOST_SHARE") == "0":
             assert c["nr_host_shared"] == 0 and c["nr_host_share_refused"] == 0
