@@ -30,6 +30,7 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <unordered_set>
 #include <utility>
@@ -96,9 +97,13 @@ class Pool {
     c.left = t - 1;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      while (workers_ < t - 1) {
-        std::thread([this] { work(); }).detach();
-        ++workers_;
+      try {
+        while (workers_ < t - 1) {
+          std::thread([this] { work(); }).detach();
+          ++workers_;
+        }
+      } catch (const std::system_error &) {
+        // (no more threads: the caller runs the tasks no worker takes)
       }
       for (unsigned k = 1; k < t; ++k) q_.emplace_back(&c, k);
     }
