@@ -19,13 +19,14 @@ size_t page_bytes() {
   return p > 0 ? (size_t)p : 4096;
 }
 std::string sys_error(const char *what) { return std::string(what) + ": " + std::strerror(errno); }
+constexpr const char *kMemfdName = "geeps-host-oplog";
 }  // namespace
 
 std::unique_ptr<SharedHostMem> SharedHostMem::create(size_t bytes, std::string *why) {
   const size_t page = page_bytes();
   const size_t data = (bytes + page - 1) / page * page;
   std::unique_ptr<SharedHostMem> m(new SharedHostMem());
-  m->fd_ = memfd_create("geeps-host-oplog", MFD_CLOEXEC);
+  m->fd_ = memfd_create(kMemfdName, MFD_CLOEXEC);
   if (m->fd_ < 0) {
     *why = sys_error("memfd_create");
     return nullptr;
@@ -63,6 +64,17 @@ std::unique_ptr<SharedHostMem> SharedHostMem::open(const HostShareHandle &h, std
     return nullptr;
   }
   const std::string path = "/proc/" + std::to_string(h.pid) + "/fd/" + std::to_string(h.fd);
+  // only ever a libgeeps host oplog: the descriptor must name one of its memfds
+  char target[256] = {};
+  const ssize_t len = readlink(path.c_str(), target, sizeof target - 1);
+  if (len < 0) {
+    *why = sys_error(("open " + path).c_str());
+    return nullptr;
+  }
+  if (std::string(target, (size_t)len).rfind(std::string("/memfd:") + kMemfdName, 0) != 0) {
+    *why = path + " is not a libgeeps host oplog (" + std::string(target, (size_t)len) + ")";
+    return nullptr;
+  }
   const int fd = ::open(path.c_str(), O_RDWR | O_CLOEXEC);
   if (fd < 0) {
     *why = sys_error(("open " + path).c_str());

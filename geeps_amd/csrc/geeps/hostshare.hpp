@@ -9,9 +9,10 @@
 // The buffer is a memfd mapping (no name under /dev/shm to leak), page-locked
 // in every process that maps it (gp_host_register) so that its copies to HBM
 // run at the pinned PCIe rate.  A peer opens it through /proc/<pid>/fd/<fd>.
-// The mapping's last page holds a 16-byte tag, random per buffer, which the
-// peer checks before it trusts a mapping: the descriptor number could name
-// other memory by then, as an IPC handle can (gp_ipc_open_handle's tag).
+// A peer maps only a descriptor that names one of these memfds, whose size is
+// the handle's, and whose last page holds the handle's 16-byte tag (random per
+// buffer): the descriptor number could name other memory by then, as an IPC
+// handle can (gp_ipc_open_handle's tag).
 
 #include <cstddef>
 #include <cstdint>

@@ -73,8 +73,8 @@ def test_wrong_size_and_descriptor_are_refused():
         page = os.sysconf("SC_PAGE_SIZE")
         rc, out = _open(o.args(map_bytes=str(int(o.map_bytes) + page)))
         assert rc == 3 and "not the buffer" in out, out
-        rc, out = _open(o.args(fd="0"))  # the owner's stdin: not this buffer
-        assert rc == 3, out
+        rc, out = _open(o.args(fd="0"))  # the owner's stdin: not a libgeeps memfd
+        assert rc == 3 and "not a libgeeps host oplog" in out, out
         rc, out = _open(o.args(fd="987654"))
         assert rc == 3 and "open" in out, out
     finally:
