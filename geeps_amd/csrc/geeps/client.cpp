@@ -35,7 +35,8 @@ std::string ClientStats::to_json() const {
     << ", \"nr_ipc_resent\": " << nr_ipc_resent << ", \"rows_host_tier\": " << rows_host_tier
     << ", \"nr_read_host\": " << nr_read_host << ", \"nr_update_host\": " << nr_update_host
     << ", \"nr_host_shared\": " << nr_host_shared << ", \"nr_host_share_refused\": " << nr_host_share_refused
-    << ", \"nr_update_host_init\": " << nr_update_host_init
+    << ", \"nr_update_host_init\": " << nr_update_host_init << ", \"nr_read_host_run\": " << nr_read_host_run
+    << ", \"nr_update_host_run\": " << nr_update_host_run
     << ", \"rows_updated\": " << rows_updated
     << ", \"rows_read\": " << rows_read << ", \"bytes_pushed_remote\": " << bytes_pushed_remote
     << ", \"read_wait_time\": " << read_wait_time << ", \"read_time\": " << read_time
@@ -97,6 +98,8 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
   for (uint32_t s = 0; s < num_processes_; ++s)
     same_node_[s] = allow_ipc && num_processes_ > 1 &&
                     norm(config_.host_list[s]) == norm(config_.host_list[process_id_]);
+  const char *runs = std::getenv("GEEPS_HOST_RUNS");
+  host_runs_ = !(runs && std::string(runs) == "0");
   const char *share = std::getenv("GEEPS_HOST_SHARE");
   host_share_ = config_.pinned_cpu_memory != 0 && !(share && std::string(share) == "0");
   bool any_peer = false;

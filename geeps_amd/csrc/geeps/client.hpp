@@ -97,6 +97,12 @@ struct OpInfo {
   // read_batch_cpu, clientlib-data.cpp:280-302, 398-434).
   bool cpu = false;
   std::vector<gp_double_index> host_index;
+  // its rows are one channel's host cache rows [host_run_lo, +rows) in order:
+  // a Read is then one host-to-device copy straight from the host cache, and
+  // an Update whose clock takes the fused init one device-to-host copy
+  // straight into the host oplog (no CPU loop)
+  int host_run_channel = -1;
+  size_t host_run_lo = 0;
 };
 
 // The CPU param cache of one (channel, table): the rows of the key batches
@@ -199,6 +205,8 @@ struct ClientStats {
   uint64_t rows_host_tier = 0, nr_read_host = 0, nr_update_host = 0;
   uint64_t nr_host_shared = 0, nr_host_share_refused = 0;
   uint64_t nr_update_host_init = 0;  // host-tier Updates through the fused oplog init
+  // host-tier Reads / Updates that were one copy (an op's rows one run of host rows)
+  uint64_t nr_read_host_run = 0, nr_update_host_run = 0;
   double read_wait_time = 0, read_time = 0, update_time = 0, push_time = 0, refresh_time = 0;
   std::string to_json() const;
 };
@@ -398,6 +406,7 @@ class ClientLib {
   // host oplogs are shared memory a same-node server maps (pinned_cpu_memory,
   // a same-node peer; GEEPS_HOST_SHARE=0 sends their rows in the frame instead)
   bool host_share_ = false;
+  bool host_runs_ = true;  // GEEPS_HOST_RUNS=0: host-tier ops always run the CPU loops
   std::vector<bool> same_node_;  // peer shares this node: rows move over IPC (xGMI)
 
   std::vector<OpInfo> opseq_;

@@ -149,6 +149,19 @@ void ClientLib::read_batch_host(OpInfo &op) {
     waited += now_s() - w0;
     const gp_double_index *idx = op.host_index.data() + op.ch_start[ch.id];
     const size_t n = op.ch_size[ch.id];
+    if (op.host_run_channel >= 0) {
+      // the op's rows are this channel's host rows [lo, +rows) in order: one
+      // copy straight from the host cache, under the lock a refresh takes
+      if ((int)ch.id != op.host_run_channel) continue;
+      const size_t vals = std::min(op.num_vals_limit, op.rows.size() * ROW_DATA_SIZE);
+      if (vals)
+        GP_CALL(gp_memcpy_async(op.buffer.data(), pc.cpu.data->data() + op.host_run_lo * ROW_DATA_SIZE,
+                                vals * sizeof(float), channels_[0]->stream->get()));
+      channels_[0]->stream->sync();
+      std::lock_guard<std::mutex> slk(stats_mu_);
+      stats_.nr_read_host_run++;
+      continue;
+    }
     if (ch.id + 1 < channels_.size()) {
       if (n)
         GP_CALL(gp_host_gather_rows(cpu_buffer_.data(), pc.cpu.data->data(), idx, n, gp_double_index{0, 0},
@@ -188,6 +201,32 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
   Channel &ch0 = *channels_[0];
   ch0.app_written.record_default();
   GP_CALL(gp_stream_wait_event(ch0.stream->get(), ch0.app_written.get()));
+  // Each row's first write of the clock is the fused init 0.0f + x when this
+  // clock's host-tier update ops write every row once (the oplog is then
+  // never zeroed)
+  std::vector<uint8_t> fused(channels_.size(), 0);
+  for (auto &chp : channels_) fused[chp->id] = started_ && chp->host_init_ok[pre.table_id];
+  const int rc = pre.host_run_channel;
+  if (rc >= 0 && fused[rc] && pre.num_vals_limit >= pre.rows.size() * ROW_DATA_SIZE) {
+    // The op's rows are one channel's host rows [lo, +rows) in order: one copy
+    // straight into the oplog.  It holds x where the init writes 0.0f + x;
+    // they differ only for -0.0, and the server's sum from +0.0 makes both
+    // +0.0 (the HBM tier's direct oplog).
+    Channel &ch = *channels_[rc];
+    std::shared_ptr<HostBuf> oplog;
+    {
+      std::lock_guard<std::mutex> lk(ch.mu);
+      oplog = get_host_oplog(ch.tables[pre.table_id].cpu, clock, /*zero=*/false);
+    }
+    if (vals)
+      GP_CALL(gp_memcpy_async(oplog->data() + pre.host_run_lo * ROW_DATA_SIZE, pre.buffer.data(),
+                              vals * sizeof(float), ch0.stream->get()));
+    ch0.stream->sync();
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.nr_update_host_init++;
+    stats_.nr_update_host_run++;
+    return;
+  }
   const size_t piece_vals = kHostPieceRows * ROW_DATA_SIZE;
   const size_t pieces = (vals + piece_vals - 1) / piece_vals;
   while (host_events_.size() < pieces) host_events_.push_back(std::make_unique<Event>());
@@ -197,15 +236,12 @@ void ClientLib::update_batch_host(OpInfo &pre, iter_t clock) {
                             ch0.stream->get()));
     host_events_[k]->record(*ch0.stream);
   }
-  // the clock's host oplogs (zeroed when new, unless this clock's host-tier
-  // update ops write every row once: then each row's first write is the
-  // fused init 0.0f + x) while the rows come down
+  // the clock's host oplogs (zeroed when new, unless fused) while the rows
+  // come down
   std::vector<std::shared_ptr<HostBuf>> oplogs(channels_.size());
-  std::vector<uint8_t> fused(channels_.size(), 0);
   for (auto &chp : channels_) {
     std::lock_guard<std::mutex> lk(chp->mu);
     HostTier &cpu = chp->tables[pre.table_id].cpu;
-    fused[chp->id] = started_ && chp->host_init_ok[pre.table_id];
     if (cpu.num_rows) oplogs[chp->id] = get_host_oplog(cpu, clock, /*zero=*/!fused[chp->id]);
   }
   if (std::find(fused.begin(), fused.end(), 1) != fused.end()) {

@@ -494,9 +494,22 @@ void ClientLib::create_double_index(OpInfo &op) {
   // allocation.
   if (op.cpu) {
     // a host-tier op: its index stays in host memory (the reference's
-    // row_index_cpu, clientlib-viter.cpp:853-876); no device index or plans
-    op.host_index = std::move(flat);
+    // row_index_cpu, clientlib-viter.cpp:853-876); no device index or plans.
+    // Its rows one channel's host cache rows in order (op row j -> host row
+    // lo + j): its Read and Update copy them whole (read_batch_host)
     op.direct_channel = -1;
+    op.host_run_channel = -1;
+    for (uint32_t c = 0; c < num_channels_ && host_runs_; ++c) {
+      if (per[c].size() != op.rows.size() || op.rows.empty()) continue;
+      bool run = true;
+      for (size_t j = 0; j < per[c].size() && run; ++j)
+        run = per[c][j].id0 == j && per[c][j].id1 == per[c][0].id1 + j;
+      if (run) {
+        op.host_run_channel = (int)c;
+        op.host_run_lo = per[c][0].id1;
+      }
+    }
+    op.host_index = std::move(flat);
     return;
   }
   if (op.type == OpInfo::PRE_WRITE || op.type == OpInfo::READ) {

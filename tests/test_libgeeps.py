@@ -577,6 +577,8 @@ HOST_TIER_LAYERS = [300, 200, 400, 100]
     (3, 1, 1, 0, "ipc", "int", 1, {"GEEPS_TEST_IPC_FAULT": "refuse"}),
     (2, 0, 1, 0, "ipc", "int", 2, {"GEEPS_HOST_SHARE": "0"}),  # host-tier rows in the frames
     (3, 0, 1, 0, "ipc", "int", 0, {"GEEPS_TEST_IPC_FAULT": "tag"}),  # no HBM part: a host-only NACK
+    (1, 0, 1, 0, "ipc", "float", 2, {"GEEPS_HOST_RUNS": "0"}),  # the CPU loops for in-order ops too
+    (2, 0, 1, 0, "ipc", "int", 1, {"GEEPS_TEST_SHUFFLE_UPDATES": "odd"}),  # updates of odd layers: no run
 ])
 def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mode, gpu_layers, extra):
     """A gpu_memory_capacity that holds only the first `gpu_layers` key
@@ -613,6 +615,17 @@ def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mod
         # oplog's rows are each written once: the fused init (not with
         # read-my-writes, whose refreshes could fall between an Update's pieces)
         assert c["nr_update_host_init"] == (0 if rmw else 6 * n_host_layers)
+        # each layer's rows are one run of host rows in order (one channel):
+        # its Read is one copy from the host cache, and its Update (fused
+        # clocks) one copy into the host oplog; shuffled updates are not runs
+        print("host runs (read / update):", c["nr_read_host_run"], c["nr_update_host_run"])
+        if channels == 1 and extra.get("GEEPS_HOST_RUNS") != "0":
+            assert c["nr_read_host_run"] == c["nr_read_host"]
+            shuffled = sum(1 for l in range(gpu_layers, len(HOST_TIER_LAYERS)) if l % 2 == 1) \
+                if extra.get("GEEPS_TEST_SHUFFLE_UPDATES") == "odd" else 0
+            assert c["nr_update_host_run"] == (0 if rmw else 6 * (n_host_layers - shuffled))
+        elif extra.get("GEEPS_HOST_RUNS") == "0":
+            assert c["nr_read_host_run"] == 0 and c["nr_update_host_run"] == 0
         fault = extra.get("GEEPS_TEST_IPC_FAULT")
         if P == 1 or transport == "tcp" or extra.get("GEEPS_HOST_SHARE") == "0":
             assert c["nr_host_shared"] == 0 and c["nr_host_share_refused"] == 0
