@@ -973,11 +973,19 @@ def libgeeps_leg(rows, W, clocks=10, warmup=5, procs=(1, 2)):
     # the client's shared host oplog (nr_host_shared); `_frames`: with
     # GEEPS_HOST_SHARE=0 they travel in the socket frame instead
     host = {"CLOCK_BENCH_HOST_TIER_FRAC": "0.5"}
-    leg("p2_alexnet_host_tier", lambda: run(2, host, ALEXNET_ROWS, 0, info={"host_tier_frac": 0.5},
-                                            keep=("read_ok", "rows_host_tier", "nr_host_shared")))
-    leg("p2_alexnet_host_tier_frames", lambda: run(2, dict(host, GEEPS_HOST_SHARE="0"), ALEXNET_ROWS, 0,
-                                                   info={"host_tier_frac": 0.5},
-                                                   keep=("read_ok", "rows_host_tier", "nr_host_shared")))
+
+    def host_tier(env):
+        d = run(2, env, ALEXNET_ROWS, 0, info={"host_tier_frac": 0.5},
+                keep=("read_ok", "rows_host_tier", "nr_host_shared"))
+        # the host rows cross PCIe four times a clock (Update down, the
+        # server's staging up, the refresh down, Read up), every process's
+        # over this one GPU's link here
+        moved = 4 * d["rows_host_tier"] * 512
+        d["pcie_bytes_per_clock"] = moved
+        d["pcie_GBps"] = round(moved / (d["ms_per_clock"] * 1e-3) / 1e9, 2)
+        return d
+    leg("p2_alexnet_host_tier", lambda: host_tier(host))
+    leg("p2_alexnet_host_tier_frames", lambda: host_tier(dict(host, GEEPS_HOST_SHARE="0")))
     return out
 
 
