@@ -199,3 +199,20 @@ def test_host_init_is_zerofy_then_add(W, limit_frac, off, threaded, kind):
     oracle.add_rows_from_double_index(e, x, idx, off, W, limit)
     rowops.init_rows_from_double_index_cpu(y, x, idx, off, W, limit)
     assert np.array_equal(bits(y), bits(e))
+
+
+def test_host_pool_under_thread_sanitizer():
+    """tests/apps/host_pool_stress.cpp, built with -fsanitize=thread by
+    __graft_entry__.build(): 6 threads run large scatter-adds, fused inits,
+    gathers, adds and zeroes through the shared worker pool, every element
+    checked against a serial loop; ThreadSanitizer reports no race."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "tests",
+                       "host_pool_stress_tsan")
+    if not os.path.exists(exe):
+        pytest.skip("build() first (build/tests/host_pool_stress_tsan)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, GP_HOST_THREADS="8", TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0 and r.stdout.strip() == "ok", (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
