@@ -140,7 +140,7 @@ int gp_scatter_add_rows(float *y, const float *x, const gp_double_index *index,
  * gp_scatter_add_rows (0.0f + x maps -0.0 to +0.0 exactly as the add does).
  * Destinations NOT listed are left untouched (not zeroed): the caller uses it
  * only when the clock's update ops cover every oplog row exactly once
- * (client.cpp, FinishVirtualIteration).  Same index semantics, precondition
+ * (client_viter.cpp, FinishVirtualIteration).  Same index semantics, precondition
  * and large-call planning as gp_scatter_add_rows. */
 int gp_scatter_init_rows(float *y, const float *x, const gp_double_index *index,
                          size_t num_rows, gp_double_index offset,
