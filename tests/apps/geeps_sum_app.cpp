@@ -139,6 +139,7 @@ int main(int argc, char **argv) {
   // GEEPS_TEST_MM_LEVEL=<n>: mm_warning_level (3 refuses a host tier)
   if (const char *cap = std::getenv("GEEPS_TEST_CAPACITY")) cfg.gpu_memory_capacity = std::strtoull(cap, nullptr, 10);
   if (const char *lvl = std::getenv("GEEPS_TEST_MM_LEVEL")) cfg.mm_warning_level = std::atoi(lvl);
+  if (const char *pin = std::getenv("GEEPS_TEST_PINNED")) cfg.pinned_cpu_memory = std::atoi(pin);
   GeePs *ps = new GeePs(pid, cfg);
 
   size_t total = 0;

@@ -579,6 +579,7 @@ HOST_TIER_LAYERS = [300, 200, 400, 100]
     (3, 0, 1, 0, "ipc", "int", 0, {"GEEPS_TEST_IPC_FAULT": "tag"}),  # no HBM part: a host-only NACK
     (1, 0, 1, 0, "ipc", "float", 2, {"GEEPS_HOST_RUNS": "0"}),  # the CPU loops for in-order ops too
     (2, 0, 1, 0, "ipc", "int", 1, {"GEEPS_TEST_SHUFFLE_UPDATES": "odd"}),  # updates of odd layers: no run
+    (2, 1, 1, 0, "ipc", "int", 2, {"GEEPS_TEST_PINNED": "0"}),  # plain host memory, as the reference's
 ])
 def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mode, gpu_layers, extra):
     """A gpu_memory_capacity that holds only the first `gpu_layers` key
@@ -627,7 +628,7 @@ def test_host_tier_splits_the_table(dev, P, slack, channels, rmw, transport, mod
         elif extra.get("GEEPS_HOST_RUNS") == "0":
             assert c["nr_read_host_run"] == 0 and c["nr_update_host_run"] == 0
         fault = extra.get("GEEPS_TEST_IPC_FAULT")
-        if P == 1 or transport == "tcp" or extra.get("GEEPS_HOST_SHARE") == "0":
+        if P == 1 or transport == "tcp" or extra.get("GEEPS_HOST_SHARE") == "0" or extra.get("GEEPS_TEST_PINNED") == "0":
             assert c["nr_host_shared"] == 0 and c["nr_host_share_refused"] == 0
         elif fault:
             # tag: its first shared buffer NACKed by one server (which then gets
