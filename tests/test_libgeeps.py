@@ -813,6 +813,12 @@ def test_randomized_configurations(dev, case):
                                                                3 if local else 0))
     if rng.random() < 0.2:
         extra["GEEPS_TEST_IPC_FAULT"] = rng.choice(["tag", "refuse"])
+    # (late round 5, drawn last) the host tier's own switches: sharing its
+    # oplogs with same-node servers, one-copy runs, page-locked memory
+    if "GEEPS_TEST_CAPACITY" in extra:
+        for k, p in (("GEEPS_HOST_SHARE", 0.2), ("GEEPS_HOST_RUNS", 0.2), ("GEEPS_TEST_PINNED", 0.15)):
+            if rng.random() < p:
+                extra[k] = "0"
     desc = dict(P=P, slack=slack, channels=channels, rmw=rmw, tables=tables, local=local, mode=mode,
                 layers=layers, transport=transport, **extra)
     print("config", desc)
@@ -824,3 +830,6 @@ def test_randomized_configurations(dev, case):
     # what the run recovered from (IPC) and placed on the host, summed over processes
     print("recovered", {k: sum(c[k] for c in st) for k in ("nr_ipc_export_refused", "nr_ipc_nack_sent",
                                                            "nr_ipc_resent", "rows_host_tier")})
+    print("host tier paths", {k: sum(c[k] for c in st) for k in ("nr_host_shared", "nr_host_share_refused",
+                                                                 "nr_update_host_init", "nr_read_host_run",
+                                                                 "nr_update_host_run")})
