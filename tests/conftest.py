@@ -49,7 +49,7 @@ FAMILIES = [
     ("libgeeps end to end (other process / consistency cases)", "test_libgeeps", ("test_",)),
     ("wire path: libgeeps ZMTP/3.0 ROUTER vs a stock libzmq ROUTER (CPU)", "test_zmtp", ("test_",)),
     ("host-tier row ops (a4: add_rows_from_double_index_cpu ...) vs oracle (CPU)", "test_host_rows", ("test_",)),
-    ("host tier's shared oplogs: a peer process maps and checks them (CPU)", "test_hostshare", ("test_",)),
+    ("host tier's shared oplogs: a peer process maps and checks them", "test_hostshare", ("test_",)),
     ("oracle vs golden vectors + layout vs reference headers (CPU)", "", ("test_",)),
 ]
 _family_counts = {}
