@@ -861,6 +861,45 @@ def libgeeps_multi_gpu_leg(n_gpus, rows, W, clocks=5, warmup=2, alex_clocks=10, 
     return out
 
 
+# libgeeps' default across GPUs (GEEPS_STAGE_PEER_UPDATES / _REFRESH unset:
+# client_net.cpp stages a peer on another GPU) and the noise band within which
+# the default counts as no slower than the alternative.
+DEFAULT_PEER_PATH = "staged"
+PEER_PATH_BAND = 0.03
+
+
+def multi_gpu_verdict(multi: dict, default: str = DEFAULT_PEER_PATH, band: float = PEER_PATH_BAND) -> dict:
+    """Top-level scalars that settle libgeeps' cross-GPU default from one
+    `bench.py --gpus N` record, per table of the leg:
+      libgeeps_multi_gpu_<table>_<path>_ms_per_clock  both paths' clocks
+      libgeeps_multi_gpu_<table>_faster_path           the faster one
+      libgeeps_multi_gpu_<table>_default_ok            default <= other x (1 + band)
+    and overall libgeeps_multi_gpu_default_ok (every table measured on both
+    paths, with every Read exact, and the default no slower on each) and
+    libgeeps_multi_gpu_default_path.  A table missing a path (skipped,
+    failed, a Read not exact) makes default_ok null: not decided."""
+    other = "in_place" if default == "staged" else "staged"
+    out = {"libgeeps_multi_gpu_default_path": default}
+    oks = []
+    for table in ("1Mx1024", "alexnet"):
+        ms = {}
+        for path in (default, other):
+            r = multi.get(f"{table}_{path}")
+            if isinstance(r, dict) and "ms_per_clock" in r and r.get("read_ok"):
+                ms[path] = float(r["ms_per_clock"])
+                out[f"libgeeps_multi_gpu_{table}_{path}_ms_per_clock"] = ms[path]
+        if len(ms) < 2:
+            out[f"libgeeps_multi_gpu_{table}_default_ok"] = None
+            oks.append(None)
+            continue
+        ok = ms[default] <= ms[other] * (1.0 + band)
+        out[f"libgeeps_multi_gpu_{table}_faster_path"] = min(ms, key=ms.get)
+        out[f"libgeeps_multi_gpu_{table}_default_ok"] = ok
+        oks.append(ok)
+    out["libgeeps_multi_gpu_default_ok"] = None if (not oks or None in oks) else all(oks)
+    return out
+
+
 def pre_gpu_multi_leg(args, backend):
     """At N > 1 (one rank per GPU under torch.distributed.run): rank 0 runs
     libgeeps_multi_gpu_leg across the N GPUs while the other ranks wait on a
@@ -1306,6 +1345,7 @@ def main(argv=None, backend="nccl", apply_fn=None):
                     rl[f"libgeeps_{k}_ms_per_clock"] = v["ms_per_clock"]
         if multi_e2e:
             line["libgeeps_multi_gpu"] = multi_e2e
+            line.update(multi_gpu_verdict(multi_e2e))
             for k, v in multi_e2e.items():
                 if isinstance(v, dict) and "ms_per_clock" in v:
                     rl[f"libgeeps_{k}_ms_per_clock"] = v["ms_per_clock"]

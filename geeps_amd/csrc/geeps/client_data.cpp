@@ -732,7 +732,7 @@ void ClientLib::push_updates(Channel &ch, iter_t clock, uint32_t table_id) {
         if (ipc_log())
           std::cerr << "libgeeps ipc export oplog: client " << process_id_ << " ch " << ch.id << " server " << s
                     << " buffer " << ref.buffer_id << " at " << static_cast<void *>(oplog->data()) << " bytes "
-                    << oplog->bytes() << "\n";
+                    << oplog->bytes() << ": " << ipc_describe(ref.handle) << "\n";
       }
       const bool with_keys = !(*keys_sent)[s];
       send_to_server(ch, s, {Part{&h, sizeof h},

@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "client.hpp"
@@ -35,6 +36,16 @@ constexpr int kWaitWarnMs = 12000;  // the reference's 12 s timed_wait warnings
 inline bool ipc_log() {
   static const bool on = std::getenv("GEEPS_IPC_LOG") != nullptr;
   return on;
+}
+
+// gp_ipc_describe_handle's line on an exported handle (the exporter's pid,
+// base and size; the process and address the runtime's handle names), for
+// the GEEPS_IPC_LOG lines: a run's log then pairs every mapping with the
+// export it came from.
+inline std::string ipc_describe(const void *handle) {
+  char buf[400];
+  if (gp_ipc_describe_handle(handle, buf, sizeof buf) != GP_OK) return std::string("(") + gp_last_error() + ")";
+  return buf;
 }
 
 struct PinnedPool {

@@ -245,7 +245,8 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
             mapped[ref.buffer_id] = p;
             if (ipc_log())
               std::cerr << "libgeeps ipc map oplog: server " << process_id_ << " ch " << ch.id << " client "
-                        << client_id << " buffer " << ref.buffer_id << " -> " << p << "\n";
+                        << client_id << " buffer " << ref.buffer_id << " -> " << p << ": "
+                        << ipc_describe(ref.handle) << "\n";
           } else {
             std::cerr << "libgeeps: server " << process_id_ << " ch " << ch.id << " could not map oplog buffer "
                       << ref.buffer_id << " of client " << client_id << " (" << gp_last_error()
@@ -587,7 +588,7 @@ void ClientLib::client_reader(Channel &ch, uint32_t server_id, int fd) {
           if (ok && ipc_log())
             std::cerr << "libgeeps ipc map version: client " << process_id_ << " ch " << ch.id << " server "
                       << server_id << " table " << h.table_id << " version " << rv.version << " rows "
-                      << rv.num_rows << " -> " << ptr << "\n";
+                      << rv.num_rows << " -> " << ptr << ": " << ipc_describe(rv.handle) << "\n";
         } else {
           auto it = mapped.find(rv.version);
           GP_CHECK_MSG(it != mapped.end(), "unmapped master version " << rv.version);
@@ -724,7 +725,7 @@ bool ClientLib::ipc_reply(Channel &ch, uint32_t client_id, const RowBatchReply &
     if (ipc_log())
       std::cerr << "libgeeps ipc export version: server " << process_id_ << " ch " << ch.id << " client "
                 << client_id << " table " << r.table_id << " version " << r.version << " rows " << r.num_rows
-                << " at " << r.device_rows << "\n";
+                << " at " << r.device_rows << ": " << ipc_describe(rv.handle) << "\n";
   }
   sc_read_row_batch_msg_t h{};
   h.cmd = READ_ROW_BATCH;

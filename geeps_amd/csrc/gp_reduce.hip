@@ -2110,8 +2110,13 @@ struct CachedPlan {
   // The streams this entry's calls ran on, each with an event recorded after
   // the call's last launch (mark_used): what the device may still be doing
   // with the entry's buffers when the host drops it.
+  // `unrecorded`: some call's event could not be created or recorded (e.g. a
+  // stream of another device than the current one): its launches are not
+  // covered by `uses` (a never-recorded event queries as passed), so the drop
+  // waits for the device instead.
   std::mutex use_mu;
   std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+  bool unrecorded = false;
   void mark_used(hipStream_t s) {
     std::lock_guard<std::mutex> lk(use_mu);
     hipEvent_t ev = nullptr;
@@ -2120,11 +2125,15 @@ struct CachedPlan {
     if (!ev) {
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
         (void)hipGetLastError();
+        unrecorded = true;
         return;
       }
       uses.emplace_back(s, ev);
     }
-    (void)hipEventRecord(ev, s);
+    if (hipEventRecord(ev, s) != hipSuccess) {
+      (void)hipGetLastError();
+      unrecorded = true;
+    }
   }
   ~CachedPlan();
 };
@@ -2176,7 +2185,7 @@ CachedPlan::~CachedPlan() {
   if (!ready) return;
   // every call that used the entry already done (the usual case when the
   // host drops it: an idle device): free now, as the member destructors do
-  bool passed = !uses.empty();
+  bool passed = !uses.empty() && !unrecorded;
   for (auto &u : uses)
     if (passed && hipEventQuery(u.second) != hipSuccess) {
       (void)hipGetLastError();
@@ -2195,7 +2204,7 @@ CachedPlan::~CachedPlan() {
     if (*b) g.bufs.push_back(std::move(*b));
   for (auto *w : {&changed, &compact_broken})
     if (*w) g.words.push_back(std::move(*w));
-  if (g.events.empty()) {  // no call recorded its launches (a failed build): wait for the device
+  if (g.events.empty() || unrecorded) {  // launches no event covers (a failed build, a failed record): wait for the device
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != key.device) (void)hipSetDevice(key.device);
@@ -3056,340 +3065,12 @@ int gp_zero(float *y, size_t num_vals, gp_stream s) {
   return GP_OK;
 }
 
-// ---- runtime helpers -------------------------------------------------------
-
-int gp_device_count(int *count) {
-  if (!count) return set_error(GP_ERR_INVALID, "null pointer");
-  GP_HIP_TRY(hipGetDeviceCount(count));
-  return GP_OK;
-}
-
-int gp_set_device(int device) {
-  GP_HIP_TRY(hipSetDevice(device));
-  return GP_OK;
-}
-
-int gp_get_device(int *device) {
-  if (!device) return set_error(GP_ERR_INVALID, "null pointer");
-  GP_HIP_TRY(hipGetDevice(device));
-  return GP_OK;
-}
-
-// Large buffers (libgeeps' oplogs, master versions, staging buckets, caches)
-// are asked for physically contiguous first: over 8 fresh 36-GiB arenas after
-// random spacers the 8-way sweep sum ran 84.5-86.8 % of 8 TB/s (mean 86.0 %)
-// contiguous against 83.1-87.1 % (mean 85.3 %) from plain hipMalloc
-// (scripts/tune/contig_tune.hip, profiles/r02/tune/contig_tune.txt).  When the
-// device has no contiguous range left, plain hipMalloc.
-constexpr size_t kContiguousMin = 64u << 20;
-
-int gp_malloc_device(void **ptr, size_t bytes) {
-  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
-  *ptr = nullptr;
-  if (bytes == 0) return GP_OK;
-  if (bytes >= kContiguousMin &&
-      hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocContiguous) == hipSuccess && *ptr)
-    return GP_OK;
-  (void)hipGetLastError();  // a failed contiguous request is not this call's error
-  *ptr = nullptr;
-  GP_HIP_TRY(hipMalloc(ptr, bytes));
-  return GP_OK;
-}
-
-// A buffer meant for IPC (gp_ipc_get_handle) is an allocation of its own,
-// rounded up to a multiple of 2 MiB, whose last kIpcTagBytes hold a tag that
-// the export writes and every mapping checks.  On MI355X (ROCm 7.2,
-// scripts/probes/ipc_probe.py) a process's FIRST device allocation could not
-// always be exported: in some runs hipIpcGetMemHandle refused it ("invalid
-// argument", persistently), in one run the export succeeded and the peer's
-// mapping held other memory, not the exported bytes; every later allocation
-// exported and mapped correctly in thousands of tries.  libgeeps' one failure
-// of this kind (ROCr "IPC Attach: Invalid IPC handle! X and Y", round 3) was
-// on the mapping side.  The tag turns a mapping of the wrong memory into a
-// loud error instead of silently wrong rows.
-constexpr size_t kIpcBlock = 2u << 20;
-constexpr size_t kIpcTagBytes = 256;  // the tag's slot at the end of the allocation
-
-static std::mutex g_ipc_prime_mu;
-static bool g_ipc_primed[kMaxDevices];   // g_ipc_prime_mu
-static void *g_ipc_primer[kMaxDevices];  // g_ipc_prime_mu: kept for the process's lifetime
-
-int gp_malloc_device_shared(void **ptr, size_t bytes) {
-  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
-  *ptr = nullptr;
-  if (bytes == 0) return GP_OK;
-  // Before a device's first shareable buffer: one throwaway export, so no
-  // real buffer is the process's first export -- the buffer the probe saw
-  // fail.  The throwaway stays allocated for the process's lifetime, as in the
-  // probe's "primed" scenario (scripts/probes/ipc_probe.py): freed, its range
-  // could go to the next real buffer, the freed-and-reused case that fails
-  // too.  A precaution; what guarantees no wrong rows is the
-  // tag check, and a refused export or a failed mapping now costs a resend
-  // over the socket, not the job (libgeeps' NACKs, wire.hpp).
-  int dev = 0;
-  GP_HIP_TRY(hipGetDevice(&dev));
-  if (dev >= 0 && dev < kMaxDevices) {
-    std::lock_guard<std::mutex> lk(g_ipc_prime_mu);
-    if (!g_ipc_primed[dev]) {
-      g_ipc_primed[dev] = true;
-      void *d = nullptr;
-      if (hipMalloc(&d, kIpcBlock) == hipSuccess) {
-        hipIpcMemHandle_t h;
-        (void)hipIpcGetMemHandle(&h, d);
-        g_ipc_primer[dev] = d;
-      }
-      (void)hipGetLastError();  // a refused throwaway export is expected, not this call's error
-    }
-  }
-  return gp_malloc_device(ptr, (bytes + kIpcTagBytes + kIpcBlock - 1) / kIpcBlock * kIpcBlock);
-}
-
-int gp_free_device(void *ptr) {
-  if (ptr) GP_HIP_TRY(hipFree(ptr));
-  return GP_OK;
-}
-
-int gp_malloc_host(void **ptr, size_t bytes) {
-  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
-  *ptr = nullptr;
-  if (bytes == 0) return GP_OK;
-  GP_HIP_TRY(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
-  return GP_OK;
-}
-
-int gp_free_host(void *ptr) {
-  if (ptr) GP_HIP_TRY(hipHostFree(ptr));
-  return GP_OK;
-}
-
-int gp_host_register(void *ptr, size_t bytes) {
-  if (!ptr) return set_error(GP_ERR_INVALID, "null pointer");
-  if (bytes == 0) return GP_OK;
-  GP_HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
-  return GP_OK;
-}
-
-int gp_host_unregister(void *ptr) {
-  if (ptr) GP_HIP_TRY(hipHostUnregister(ptr));
-  return GP_OK;
-}
-
-int gp_memcpy_async(void *dst, const void *src, size_t bytes, gp_stream s) {
-  if (bytes == 0) return GP_OK;
-  if (!dst || !src) return set_error(GP_ERR_INVALID, "null pointer");
-  GP_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)s));
-  return GP_OK;
-}
-
-int gp_memset_async(void *dst, int value, size_t bytes, gp_stream s) {
-  if (bytes == 0) return GP_OK;
-  if (!dst) return set_error(GP_ERR_INVALID, "null pointer");
-  GP_HIP_TRY(hipMemsetAsync(dst, value, bytes, (hipStream_t)s));
-  return GP_OK;
-}
-
-int gp_stream_create(gp_stream *s) {
-  if (!s) return set_error(GP_ERR_INVALID, "null pointer");
-  hipStream_t st = nullptr;
-  GP_HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  *s = (gp_stream)st;
-  return GP_OK;
-}
-
-int gp_stream_destroy(gp_stream s) {
-  if (s) GP_HIP_TRY(hipStreamDestroy((hipStream_t)s));
-  return GP_OK;
-}
-
-int gp_stream_synchronize(gp_stream s) {
-  GP_HIP_TRY(hipStreamSynchronize((hipStream_t)s));
-  return GP_OK;
-}
-
-int gp_device_synchronize(void) {
-  GP_HIP_TRY(hipDeviceSynchronize());
-  return GP_OK;
-}
-
-int gp_event_create(gp_event *e) {
-  if (!e) return set_error(GP_ERR_INVALID, "null pointer");
-  hipEvent_t ev = nullptr;
-  GP_HIP_TRY(hipEventCreate(&ev));
-  *e = (gp_event)ev;
-  return GP_OK;
-}
-
-int gp_event_destroy(gp_event e) {
-  if (e) GP_HIP_TRY(hipEventDestroy((hipEvent_t)e));
-  return GP_OK;
-}
-
-int gp_event_record(gp_event e, gp_stream s) {
-  GP_HIP_TRY(hipEventRecord((hipEvent_t)e, (hipStream_t)s));
-  return GP_OK;
-}
-
-int gp_event_synchronize(gp_event e) {
-  GP_HIP_TRY(hipEventSynchronize((hipEvent_t)e));
-  return GP_OK;
-}
-
-int gp_event_elapsed_ms(float *ms, gp_event start, gp_event stop) {
-  if (!ms) return set_error(GP_ERR_INVALID, "null pointer");
-  GP_HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
-  return GP_OK;
-}
-
-int gp_stream_wait_event(gp_stream s, gp_event e) {
-  if (!e) return set_error(GP_ERR_INVALID, "null event");
-  GP_HIP_TRY(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0));
-  return GP_OK;
-}
-
-int gp_device_pci_bus_id(int device, char *buf, int len) {
-  if (!buf || len < 2) return set_error(GP_ERR_INVALID, "null or short buffer");
-  GP_HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
-  buf[len - 1] = 0;
-  return GP_OK;
-}
-
-// The handle as it crosses the C-ABI: the runtime's handle, then where the
-// allocation's tag lies (bytes from its base) and the tag itself.
-struct IpcHandleOut {
-  hipIpcMemHandle_t h;
-  uint64_t tag_offset;
-  uint64_t tag[2];
-};
-static_assert(sizeof(IpcHandleOut) <= GP_IPC_HANDLE_BYTES, "IPC handle size");
-constexpr uint64_t kIpcTagMagic = 0x6770495043746167ull;  // "gpIPCtag"
-
-// One process's IPC calls run one at a time (libgeeps exports and maps from
-// several threads: server threads export master versions, reader threads map
-// a peer's versions and oplogs); they run once per buffer.
-static std::mutex g_ipc_mu;
-static hipStream_t g_ipc_stream[kMaxDevices];  // g_ipc_mu: the tag copies' stream per device
-
-static int ipc_stream(hipStream_t *s) {
-  int dev = 0;
-  GP_HIP_TRY(hipGetDevice(&dev));
-  if (dev < 0 || dev >= kMaxDevices) return set_error(GP_ERR_INVALID, "device id out of range");
-  if (!g_ipc_stream[dev]) GP_HIP_TRY(hipStreamCreateWithFlags(&g_ipc_stream[dev], hipStreamNonBlocking));
-  *s = g_ipc_stream[dev];
-  return GP_OK;
-}
-
-// The allocation's tag: the same for every export of it, distinct per process,
-// allocation and size.
-static void ipc_tag(const void *base, size_t bytes, uint64_t tag[2]) {
-  static const uint64_t salt = [] {
-    uint64_t x = (uint64_t)getpid() * 0x9e3779b97f4a7c15ull;
-    x ^= (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
-    return x;
-  }();
-  uint64_t h = salt ^ (reinterpret_cast<uintptr_t>(base) * 0xbf58476d1ce4e5b9ull) ^ (bytes * 0x94d049bb133111ebull);
-  h ^= h >> 31;
-  tag[0] = kIpcTagMagic;
-  tag[1] = h;
-}
-
-int gp_ipc_get_handle(void *handle_out, void *device_base) {
-  if (!handle_out || !device_base) return set_error(GP_ERR_INVALID, "null pointer");
-  std::lock_guard<std::mutex> lk(g_ipc_mu);
-  // a handle names a whole allocation: an interior pointer would map the
-  // allocation's base in the peer, at the wrong rows
-  void *base = nullptr;
-  size_t bytes = 0;
-  GP_HIP_TRY(hipMemGetAddressRange(&base, &bytes, device_base));
-  if (base != device_base || bytes < kIpcBlock || bytes % kIpcBlock) {
-    char msg[200];
-    std::snprintf(msg, sizeof msg,
-                  "IPC export of %p: %s (allocation %p, %zu B); allocate it with gp_malloc_device_shared",
-                  device_base, base != device_base ? "not an allocation base" : "not a gp_malloc_device_shared buffer",
-                  base, bytes);
-    return set_error(GP_ERR_INVALID, msg);
-  }
-  IpcHandleOut out{};
-  out.tag_offset = bytes - kIpcTagBytes;
-  ipc_tag(base, bytes, out.tag);
-  hipStream_t s = nullptr;
-  if (const int rc = ipc_stream(&s); rc != GP_OK) return rc;
-  GP_HIP_TRY(hipMemcpyAsync(static_cast<char *>(base) + out.tag_offset, out.tag, sizeof out.tag,
-                            hipMemcpyHostToDevice, s));
-  GP_HIP_TRY(hipStreamSynchronize(s));
-  GP_HIP_TRY(hipIpcGetMemHandle(&out.h, device_base));
-  std::memset(handle_out, 0, GP_IPC_HANDLE_BYTES);
-  std::memcpy(handle_out, &out, sizeof out);
-  return GP_OK;
-}
-
-static std::mutex g_ipc_leak_mu;
-static std::vector<void *> g_ipc_leaked;  // g_ipc_leak_mu: mappings refused as mis-mapped, never closed
-
-int gp_ipc_open_handle(void **device_ptr, const void *handle) {
-  if (!device_ptr || !handle) return set_error(GP_ERR_INVALID, "null pointer");
-  IpcHandleOut in;
-  std::memcpy(&in, handle, sizeof in);
-  if (in.tag[0] != kIpcTagMagic) return set_error(GP_ERR_INVALID, "not a gp_ipc_get_handle handle");
-  std::lock_guard<std::mutex> lk(g_ipc_mu);
-  void *p = nullptr;
-  GP_HIP_TRY(hipIpcOpenMemHandle(&p, in.h, hipIpcMemLazyEnablePeerAccess));
-  // the mapping must span the tag (else it is not the exported allocation:
-  // refused without reading past it) and hold the exporter's tag there
-  uint64_t got[2] = {0, 0};
-  hipStream_t s = nullptr;
-  int rc = ipc_stream(&s);
-  void *mbase = nullptr;
-  size_t mbytes = 0;
-  const bool ranged = hipMemGetAddressRange(&mbase, &mbytes, p) == hipSuccess;
-  if (!ranged) (void)hipGetLastError();  // no range for this mapping: the tag check below still runs
-  const uintptr_t from_base = reinterpret_cast<uintptr_t>(p) - reinterpret_cast<uintptr_t>(mbase);
-  if (rc == GP_OK && ranged && (from_base > mbytes || mbytes - from_base < in.tag_offset + sizeof got)) {
-    char msg[200];
-    std::snprintf(msg, sizeof msg,
-                  "IPC mapping %p spans %zu B from %p, short of the exporter's tag at +%llu: the runtime mapped "
-                  "other memory than the exported buffer",
-                  p, mbytes, mbase, (unsigned long long)in.tag_offset);
-    rc = set_error(GP_ERR_HIP, msg);
-  }
-  if (rc == GP_OK && (hipMemcpyAsync(got, static_cast<char *>(p) + in.tag_offset, sizeof got, hipMemcpyDeviceToHost,
-                                     s) != hipSuccess ||
-                      hipStreamSynchronize(s) != hipSuccess))
-    rc = set_error(GP_ERR_HIP, "reading the IPC mapping's tag failed");
-  if (rc == GP_OK && (got[0] != in.tag[0] || got[1] != in.tag[1])) {
-    char msg[240];
-    std::snprintf(msg, sizeof msg,
-                  "IPC mapping %p does not hold the exporter's tag at +%llu (read %016llx %016llx, expected "
-                  "%016llx %016llx): the runtime mapped other memory than the exported buffer",
-                  p, (unsigned long long)in.tag_offset, (unsigned long long)got[0], (unsigned long long)got[1],
-                  (unsigned long long)in.tag[0], (unsigned long long)in.tag[1]);
-    rc = set_error(GP_ERR_HIP, msg);
-  }
-  if (rc != GP_OK) {
-    // A mapping of the wrong memory is left mapped, never closed: round 5's
-    // randomized runs saw the runtime hand out, for one exporter's handle, a
-    // mapping of ANOTHER exporter's buffer that this process had already
-    // mapped (the tag read was that buffer's).  Whether closing it would
-    // also tear down the live mapping of that buffer is the runtime's
-    // business; a leaked mapping costs address space only.
-    std::lock_guard<std::mutex> lk2(g_ipc_leak_mu);
-    g_ipc_leaked.push_back(p);
-    (void)hipGetLastError();  // no failed call's error may linger into a later launch check
-    return rc;
-  }
-  *device_ptr = p;
-  return GP_OK;
-}
-
-int gp_ipc_close_handle(void *device_ptr) {
-  std::lock_guard<std::mutex> lk(g_ipc_mu);
-  if (device_ptr) GP_HIP_TRY(hipIpcCloseMemHandle(device_ptr));
-  return GP_OK;
-}
 
 }  // extern "C"
 
-// The thread's gp_last_error message, for the C-ABI's host-memory functions
-// (gp_host.cpp, another translation unit of the library).
+// The thread's gp_last_error message, for the C-ABI functions of the library's
+// other translation units (gp_host.cpp: host-memory row ops; gp_runtime.hip:
+// memory, streams, events, IPC).
 namespace gp_internal {
 int set_error(int code, const char *msg) { return ::set_error(code, msg); }
 }  // namespace gp_internal

@@ -20,7 +20,7 @@ GP_ERR_INVALID = 1
 GP_ERR_HIP = 2
 
 
-ABI_VERSION = 15  # GP_ABI_VERSION in include/gp_reduce.h
+ABI_VERSION = 16  # GP_ABI_VERSION in include/gp_reduce.h
 
 
 class GpError(RuntimeError):
@@ -132,6 +132,8 @@ _SIGNATURES = {
     "gp_ipc_get_handle": (_i, [_vp, _vp]),
     "gp_ipc_open_handle": (_i, [_c.POINTER(_vp), _vp]),
     "gp_ipc_close_handle": (_i, [_vp]),
+    "gp_ipc_describe_handle": (_i, [_vp, _c.c_char_p, _i]),
+    "gp_ipc_mismaps": (_i, [_c.POINTER(_i), _c.POINTER(_i)]),
 }
 
 _lock = threading.Lock()

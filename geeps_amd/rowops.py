@@ -462,6 +462,52 @@ def _host_index(index):
         raise ValueError("index must be a contiguous (n, 2) int64 numpy array")
 
 
+def _host_bounds(kind, y, x, index, off, row_size, limit) -> None:
+    """The host twins' bounds check, as _validate_bounds for the device ops:
+    every element the C-ABI call will touch must lie inside the numpy arrays
+    (the C code trusts its pointers: an id past the end would write the
+    Python process's heap).  Negative ids and offsets are refused, as are ids
+    whose element index could not be formed in 63 bits; the guarded side
+    (the source of add / init, the destination of the gather) is touched only
+    below ``limit``, rows wholly past it not at all."""
+    import numpy as np
+    if row_size <= 0:
+        raise ValueError("row_size must be positive")
+    if limit < 0:
+        raise ValueError("num_vals_limit must not be negative")
+    if off.id0 < 0 or off.id1 < 0:  # (a ctypes c_uint64 wraps a negative int: caught by the size test below)
+        raise ValueError("negative index offset")
+    if index.shape[0] == 0:
+        return
+    if index.dtype == np.int64 and int(index.min()) < 0:
+        raise ValueError("negative row id in DoubleIndex")
+    ids = index.view(np.uint64)
+    top = int(ids.max()) + max(int(off.id0), int(off.id1))
+    if (top + 1) * row_size >= 1 << 63:
+        raise ValueError(f"row id {top} out of range for any array of {row_size}-float rows")
+    r0 = ids[:, 0] + np.uint64(off.id0)
+    r1 = ids[:, 1] + np.uint64(off.id1)
+    if kind == "gather":   # y[id0] = x[id1], guard on y
+        x_rows, y_rows, guarded = r1, r0, r0
+    else:                  # y[id1] (+)= x[id0], guard on x
+        x_rows, y_rows, guarded = r0, r1, r0
+    if limit < (1 << 63):
+        active = guarded * np.uint64(row_size) < np.uint64(limit)  # the row touches >= 1 element
+        if not bool(active.any()):
+            return
+        x_rows, y_rows = x_rows[active], y_rows[active]
+    x_max, y_max = int(x_rows.max()), int(y_rows.max())
+    x_need, y_need = (x_max + 1) * row_size, (y_max + 1) * row_size
+    if kind == "gather":
+        y_need = min(y_need, limit)
+    else:
+        x_need = min(x_need, limit)
+    if x_need > x.size:
+        raise ValueError(f"source row {x_max} out of range for rows_x")
+    if y_need > y.size:
+        raise ValueError(f"destination row {y_max} out of range for rows_y")
+
+
 def add_rows_from_double_index_cpu(rows_y, rows_x, index, index_offset=None, row_size=ROW_DATA_SIZE,
                                    num_vals_limit=None) -> None:
     """``y[(id1+off1)*W + v] += x[(id0+off0)*W + v]`` in host memory, entries in
@@ -470,6 +516,7 @@ def add_rows_from_double_index_cpu(rows_y, rows_x, index, index_offset=None, row
     _host_f32(rows_x, "rows_x")
     _host_index(index)
     limit = (1 << 64) - 1 if num_vals_limit is None else num_vals_limit
+    _host_bounds("add", rows_y, rows_x, index, _as_offset(index_offset), row_size, limit)
     check(native.lib().gp_host_scatter_add_rows(rows_y.ctypes.data, rows_x.ctypes.data, index.ctypes.data,
                                                 index.shape[0], _as_offset(index_offset), row_size, limit),
           "gp_host_scatter_add_rows")
@@ -484,6 +531,7 @@ def init_rows_from_double_index_cpu(rows_y, rows_x, index, index_offset=None, ro
     _host_f32(rows_x, "rows_x")
     _host_index(index)
     limit = (1 << 64) - 1 if num_vals_limit is None else num_vals_limit
+    _host_bounds("init", rows_y, rows_x, index, _as_offset(index_offset), row_size, limit)
     check(native.lib().gp_host_scatter_init_rows(rows_y.ctypes.data, rows_x.ctypes.data, index.ctypes.data,
                                                  index.shape[0], _as_offset(index_offset), row_size, limit),
           "gp_host_scatter_init_rows")
@@ -497,6 +545,7 @@ def assign_rows_to_double_index_cpu(rows_y, rows_x, index, index_offset=None, ro
     _host_f32(rows_x, "rows_x")
     _host_index(index)
     limit = (1 << 64) - 1 if num_vals_limit is None else num_vals_limit
+    _host_bounds("gather", rows_y, rows_x, index, _as_offset(index_offset), row_size, limit)
     check(native.lib().gp_host_gather_rows(rows_y.ctypes.data, rows_x.ctypes.data, index.ctypes.data,
                                            index.shape[0], _as_offset(index_offset), row_size, limit),
           "gp_host_gather_rows")

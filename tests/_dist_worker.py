@@ -51,6 +51,44 @@ def run_shard(rank, world, port, num_rows, W, num_clients, exchange, steps, out_
         dist.destroy_process_group()
 
 
+def run_rehearsal(rank, world, port, num_rows, W, num_clients, exchange, steps, out_dir, apply="hip"):
+    """configs[2]'s flow at its own rank count on one box (tests/test_rccl.py):
+    `steps` clocks of ShardedReducer.step over gloo ranks with the oracle's
+    seeded deltas, then bench.exchange_check -- the check `bench.py --gpus N`
+    runs on its RCCL ranks -- on the same reducer.  Rank 0 saves its refreshed
+    table; every rank writes a digest of its own and the check's result."""
+    import hashlib
+    import json
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from geeps_amd.shard import ShardedReducer
+        red = ShardedReducer(num_rows, W, num_clients, device="cpu", exchange=exchange,
+                             apply_fn=oracle_apply if apply == "oracle" else hip_apply)
+        for step in range(steps):
+            deltas = [full_delta(c + 100 * step, num_rows, W) for c in red.hosted]
+            table = red.step(deltas)
+            del deltas
+            if exchange == "rs":  # the buckets gloo's reduce-scatter delivered to this shard, per slot
+                for j, r in enumerate(red.recv):
+                    np.save(os.path.join(out_dir, f"rs_{rank}_{step}_{j}.npy"), r[:red.layout.local_vals].numpy())
+        table = table.numpy()[:num_rows * W]
+        if rank == 0:
+            np.save(os.path.join(out_dir, "table_0.npy"), table)
+        digest = hashlib.sha256(table.tobytes()).hexdigest()
+        del table
+        cpu = torch.device("cpu")
+        bdeltas, _ = bench.make_deltas(red.hosted, num_rows * W, cpu, "separate")
+        chk = bench.exchange_check(red, bdeltas, num_rows, W, num_clients, cpu, world, exchange)
+        with open(os.path.join(out_dir, f"rank_{rank}.json"), "w") as f:
+            json.dump({"rank": rank, "hosted": red.hosted, "digest": digest, "check": chk,
+                       "shard": [red.layout.row_start, red.layout.local_rows]}, f)
+    finally:
+        dist.destroy_process_group()
+
+
 def run_bench(rank, world, port, argv, out_dir):
     """bench.py's multi-rank flow on gloo CPU ranks (oracle as the apply step)."""
     import json

@@ -31,7 +31,7 @@ def main():
     role, d, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
     L = native.lib()
     if role == "export":
-        bufs = []
+        bufs, bases, described = [], [], []
         for k in range(n):
             p = ctypes.c_void_p()
             native.check(L.gp_malloc_device_shared(ctypes.byref(p), SIZE), "gp_malloc_device_shared")
@@ -39,7 +39,11 @@ def main():
             native.check(L.gp_device_synchronize(), "sync")
             h = (ctypes.c_ubyte * HANDLE)()
             native.check(L.gp_ipc_get_handle(h, p), "gp_ipc_get_handle")
+            line = ctypes.create_string_buffer(400)
+            native.check(L.gp_ipc_describe_handle(h, line, 400), "gp_ipc_describe_handle")
+            described.append(line.value.decode())
             bufs.append(p)
+            bases.append(p.value)
             tmp = os.path.join(d, f"h{k}.tmp")
             with open(tmp, "wb") as f:
                 f.write(bytes(h))
@@ -50,7 +54,8 @@ def main():
         h = (ctypes.c_ubyte * HANDLE)()
         refused = L.gp_ipc_get_handle(h, q) == native.GP_ERR_INVALID
         wait_for(os.path.join(d, "done"), 120)
-        print(json.dumps({"role": "export", "plain_refused": refused}))
+        print(json.dumps({"role": "export", "plain_refused": refused, "pid": os.getpid(), "bases": bases,
+                          "described": described}))
         return
     corrupt = len(sys.argv) > 4 and sys.argv[4] == "corrupt"
     res = []
@@ -71,9 +76,12 @@ def main():
         native.check(L.gp_device_synchronize(), "sync")
         res.append({"k": k, "ok": all(b == 1 + k for b in got), "err": ""})
         native.check(L.gp_ipc_close_handle(p), "gp_ipc_close_handle")
+    closed, kept = ctypes.c_int(), ctypes.c_int()
+    native.check(L.gp_ipc_mismaps(ctypes.byref(closed), ctypes.byref(kept)), "gp_ipc_mismaps")
     with open(os.path.join(d, "done"), "w") as f:
         f.write("1")
-    print(json.dumps({"role": "import", "results": res}))
+    print(json.dumps({"role": "import", "results": res, "mismaps_closed": closed.value,
+                      "mismaps_kept": kept.value}))
 
 
 if __name__ == "__main__":

@@ -24,8 +24,10 @@ FAMILIES = [
      ("test_full_size_config1_two_clients",)),
     ("configs[2] rehearsal: libgeeps one process per GPU, cross-GPU paths forced, on one GPU",
      "test_libgeeps", ("test_one_process_per_gpu_rehearsal",)),
-    ("configs[2] 8 shards on real ranks: RCCL exchange + HIP sum (nccl, >= 2 GPUs; gloo-exchange "
-     "rehearsal on one GPU)", "test_rccl", ("test_",)),
+    ("configs[2] on real ranks: RCCL exchange + HIP sum (nccl ranks; skips below 2 GPUs)", "test_rccl",
+     ("test_rccl_",)),
+    ("configs[2] rehearsal, NOT RCCL: gloo exchange at 2/8 ranks around the HIP sum on one GPU "
+     "(+ bench.exchange_check on the ranks; oracle-apply cases on CPU)", "test_rccl", ("test_gloo_",)),
     ("configs[2] 8 shards: RCCL-shaped exchange (gloo ranks) + one process per GPU", "",
      ("test_sharded_reduction", "test_bench_multirank_flow", "test_one_process_per_gpu",
       "test_world_one_is_local", "test_hosting_requires_divisible_clients",

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = native.lib()
-    assert L.gp_abi_version() == native.ABI_VERSION == 15
+    assert L.gp_abi_version() == native.ABI_VERSION == 16
     assert isinstance(L.gp_last_error(), bytes)
 
 

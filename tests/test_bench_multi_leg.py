@@ -122,3 +122,33 @@ def test_leg_stops_at_its_first_failure(monkeypatch):
     assert len(fake.calls) == 1 and "fake failure" in out["1Mx1024_staged"]["error"]
     assert all("after 1Mx1024_staged failed" in out[k]["skipped"]
                for k in ("alexnet_staged", "1Mx1024_in_place", "alexnet_in_place"))
+
+
+def test_multi_gpu_verdict_settles_the_default_from_one_record():
+    """the leg's record alone says whether libgeeps'
+    cross-GPU default (staged) is no slower than in place, per table and
+    overall, as top-level scalars."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    def rec(ms, ok=True):
+        return {"ms_per_clock": ms, "read_ok": ok}
+    multi = {"1Mx1024_staged": rec(19.0), "1Mx1024_in_place": rec(25.0),
+             "alexnet_staged": rec(2.0), "alexnet_in_place": rec(1.96)}  # within the 3 % band
+    v = bench.multi_gpu_verdict(multi)
+    assert v["libgeeps_multi_gpu_default_path"] == "staged"
+    assert v["libgeeps_multi_gpu_1Mx1024_staged_ms_per_clock"] == 19.0
+    assert v["libgeeps_multi_gpu_1Mx1024_in_place_ms_per_clock"] == 25.0
+    assert v["libgeeps_multi_gpu_1Mx1024_faster_path"] == "staged"
+    assert v["libgeeps_multi_gpu_alexnet_faster_path"] == "in_place"
+    assert v["libgeeps_multi_gpu_alexnet_default_ok"] is True
+    assert v["libgeeps_multi_gpu_default_ok"] is True
+    assert all(not isinstance(x, (dict, list)) for x in v.values())  # scalars only
+    multi["1Mx1024_staged"] = rec(30.0)
+    v = bench.multi_gpu_verdict(multi)
+    assert v["libgeeps_multi_gpu_1Mx1024_default_ok"] is False and v["libgeeps_multi_gpu_default_ok"] is False
+    # a path not measured (skipped, failed, a Read not exact): not decided
+    for broken in ({"skipped": "budget"}, {"error": "x"}, rec(1.0, ok=False)):
+        m = dict(multi, alexnet_in_place=broken)
+        v = bench.multi_gpu_verdict(m)
+        assert v["libgeeps_multi_gpu_alexnet_default_ok"] is None and v["libgeeps_multi_gpu_default_ok"] is None

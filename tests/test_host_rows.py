@@ -115,6 +115,41 @@ def test_host_row_ops_reject_bad_arguments_and_skip_empty_calls():
         rowops.add_rows_from_double_index_cpu(y, y.astype(np.float64), np.zeros((1, 2), np.int64))
 
 
+@pytest.mark.parametrize("op", ["add", "init", "gather"])
+def test_host_row_ops_refuse_rows_outside_the_arrays(op):
+    """the host wrappers check every touched row against
+    the numpy arrays before the C-ABI call (which trusts its pointers), as the
+    device wrappers do; rows wholly past num_vals_limit on the guarded side are
+    skipped, not refused."""
+    fn = {"add": rowops.add_rows_from_double_index_cpu, "init": rowops.init_rows_from_double_index_cpu,
+          "gather": rowops.assign_rows_to_double_index_cpu}[op]
+    W = 4
+    x = np.ones(3 * W, np.float32)
+    y = np.zeros(5 * W, np.float32)
+    # (source side, destination side) of an entry: add / init read x[id0] and
+    # write y[id1]; the gather writes y[id0] from x[id1]
+    def entry(src, dst):
+        return np.array([[dst, src]] if op == "gather" else [[src, dst]], np.int64)
+    fn(y, x, entry(2, 4), row_size=W)                      # in range
+    for src, dst in ((3, 0), (0, 5), (0, 1 << 62)):
+        with pytest.raises(ValueError, match="out of range"):
+            fn(y, x, entry(src, dst), row_size=W)
+    with pytest.raises(ValueError, match="negative"):
+        fn(y, x, entry(-1, 0), row_size=W)
+    with pytest.raises(ValueError, match="out of range"):  # a wrapped negative offset
+        fn(y, x, entry(0, 0), index_offset=(0, -1), row_size=W)
+    with pytest.raises(ValueError, match="out of range"):
+        fn(y, x, entry(0, 0), index_offset=(3, 0) if op != "gather" else (0, 3), row_size=W)
+    # the guarded side's rows past the limit are skipped (the reference's
+    # guard), so an out-of-range row there is no error ...
+    guarded_big = entry(7, 0) if op != "gather" else entry(0, 7)
+    fn(y, x, guarded_big, row_size=W, num_vals_limit=3 * W)
+    # ... but a row the limit lets in is checked
+    with pytest.raises(ValueError, match="out of range"):
+        fn(y, x, guarded_big, row_size=W, num_vals_limit=8 * W)
+    assert np.array_equal(y[4 * W:], np.ones(W, np.float32))
+
+
 def test_host_row_ops_from_concurrent_callers():
     """The helper threads are one persistent pool shared by every caller
     (libgeeps' app thread and its reader threads call these at once): 6

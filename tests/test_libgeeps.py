@@ -159,6 +159,13 @@ def _collect(procs, timeout):
             streams.append(f.read())
             f.close()
         outs.append((pr.returncode, streams[0], streams[1]))
+    log_dir = os.environ.get("GEEPS_TEST_LOG_DIR")
+    if log_dir:  # every process's whole output (e.g. GEEPS_IPC_LOG audits), not just a failure's tail
+        os.makedirs(log_dir, exist_ok=True)
+        tag = os.environ.get("PYTEST_CURRENT_TEST", "run").split(" ")[0].replace("/", "_").replace("::", "-")
+        for p, (rc, o, e) in enumerate(outs):
+            with open(os.path.join(log_dir, f"{tag}_p{p}.log"), "w") as f:
+                f.write(f"rc={rc}\n--- stdout\n{o}\n--- stderr\n{e}")
     failed = hung or any(rc != 0 or not o.startswith("OK") for rc, o, _ in outs)
     if failed:
         report = [f"hung (killed after {timeout} s): {hung}"] if hung else []

@@ -16,6 +16,17 @@ client, src/server/tablet-server.cpp:136-163).
   so the multi-rank partition / order / refresh logic runs around the real
   kernel on a one-GPU box; bit-exact against the oracle (a2a; rs at 2 ranks is a
   two-term sum per shard, pinned against its own association).
+* test_gloo_rehearsal_at_configs2_shape: configs[2]'s
+  own shape -- 8 ranks, 8 (or 16) clients, uneven row counts, 1024- and
+  128-wide rows, both exchanges -- on gloo CPU ranks sharing cuda:0 for the HIP
+  sum, then bench.exchange_check on the same ranks.  A rehearsal of the
+  partition, a2a split, all-gather unpacking and the on-rank check around the
+  real kernel, NOT RCCL evidence: the exchange is gloo's (tests/conftest.py
+  files it under its own label).  a2a is bit-exact against the oracle in
+  client order; rs bit-exact against the HIP-apply of the buckets gloo itself
+  delivered (each checked against the client-order sum within rs_tolerance):
+  gloo's reduce-scatter association is not one fixed order at this size
+  (expected_table), so it is captured, not restated.
 """
 import json
 import os
@@ -90,3 +101,81 @@ def test_gloo_exchange_hip_sum_one_gpu(dev, tmp_path, num_rows, W, clients, exch
         else:  # each shard's reduce-scatter adds the two ranks' slot-j deltas first
             oracle.apply_updates(m, [d[2 * j] + d[2 * j + 1] for j in range(clients // 2)])
     assert np.array_equal(tables[0].view(np.uint32), m.view(np.uint32))
+
+
+def expected_table(tmp_path, num_rows, W, clients, world, exchange, steps):
+    """The refreshed table.  a2a: the oracle's client-order apply.  rs: each
+    shard's master = the oracle's apply, in slot order, of the buckets gloo's
+    reduce-scatter delivered to that shard (saved by the ranks: gloo's own
+    association, which is not one fixed order -- at 8 ranks and 8.4 M floats
+    per shard it is ((x[s-1] + x[s-2]) + ...) + x[s] for all but a few dozen
+    leading elements of each shard, which get the rank-order sum); each such
+    bucket is first checked to be the sum of the right clients' slices, within
+    bench.rs_tolerance of their client-order sum."""
+    import bench
+    from oracle import oracle
+    from geeps_amd.shard import server_partition
+    starts, counts = server_partition(num_rows, world)
+    m = np.zeros(num_rows * W, np.float32)
+    for step in range(steps):
+        d = [oracle.synthetic_delta(c + 100 * step, num_rows * W) for c in range(clients)]
+        if exchange == "a2a":
+            oracle.apply_updates(m, d)
+            continue
+        for s_, (a, c) in enumerate(zip(starts, counts)):
+            sl = slice(a * W, (a + c) * W)
+            buckets = []
+            for j in range(clients // world):
+                b = np.load(tmp_path / f"rs_{s_}_{step}_{j}.npy")
+                exact = np.zeros(c * W, np.float32)
+                for r in range(world):
+                    exact = exact + d[j * world + r][sl]
+                assert b.shape == exact.shape
+                assert float(np.abs(b - exact).max()) <= bench.rs_tolerance(world), (s_, step, j)
+                buckets.append(b)
+            shard = np.ascontiguousarray(m[sl])
+            oracle.apply_updates(shard, buckets)
+            m[sl] = shard
+        del d
+    return m
+
+REHEARSAL = [
+    # (rows, W, clients, exchange, steps, apply); uneven: 65539 = 8 x 8192 + 3
+    pytest.param(65539, 1024, 8, "a2a", 2, "hip", marks=pytest.mark.gpu),
+    pytest.param(65539, 1024, 8, "rs", 1, "hip", marks=pytest.mark.gpu),
+    pytest.param(8197, 128, 16, "a2a", 2, "hip", marks=pytest.mark.gpu),   # 2 client slots per rank
+    pytest.param(8197, 128, 16, "rs", 2, "hip", marks=pytest.mark.gpu),
+    # CPU: the same ranks with the oracle as the apply, pinning the expected
+    # tables (and gloo's rs association) without a GPU
+    pytest.param(1029, 64, 16, "rs", 2, "oracle"),
+    pytest.param(1029, 64, 8, "a2a", 2, "oracle"),
+]
+
+
+@pytest.mark.parametrize("num_rows,W,clients,exchange,steps,apply", REHEARSAL)
+def test_gloo_rehearsal_at_configs2_shape(request, tmp_path, num_rows, W, clients, exchange, steps, apply):
+    import torch.multiprocessing as mp
+    if apply == "hip":
+        request.getfixturevalue("dev")  # a HIP device, and the library loaded
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _dist_worker
+    world = 8
+    mp.spawn(_dist_worker.run_rehearsal,
+             args=(world, _free_port(), num_rows, W, clients, exchange, steps, str(tmp_path), apply),
+             nprocs=world, join=True)
+    ranks = [json.loads((tmp_path / f"rank_{r}.json").read_text()) for r in range(world)]
+    # every rank refreshed the same table; the shards are the reference partition
+    assert len({r["digest"] for r in ranks}) == 1
+    from geeps_amd.shard import server_partition
+    starts, counts = server_partition(num_rows, world)
+    assert [r["shard"] for r in ranks] == [[a, c] for a, c in zip(starts, counts)]
+    assert sorted(c for r in ranks for c in r["hosted"]) == list(range(clients))
+    table = np.load(tmp_path / "table_0.npy")
+    exp = expected_table(tmp_path, num_rows, W, clients, world, exchange, steps)
+    assert np.array_equal(table.view(np.uint32), exp.view(np.uint32))
+    # bench.exchange_check, on the same ranks: all agree it passed
+    for r in ranks:
+        chk = r["check"]
+        assert chk["ok"] and chk["ranks"] == world and chk["elements_checked"] == num_rows * W, chk
+        if exchange == "a2a":
+            assert chk["max_abs_err"] == 0.0, chk
