@@ -30,7 +30,18 @@
 //    scatter-add, ZIN for the fused init, NB = 0 for the gather), the other
 //    rows to the row kernels in destination order.
 //
-// Wave64 throughout: 256-thread workgroups = 4 waves, one per SIMD.
+//  * the unplanned calls' device planning ("Device-built plans" below): the
+//    reference binding's calls pass a device index every call; large calls
+//    scan it on the device, build an inverse map / sorted residual / ranges
+//    plan once, and from the second call on check the index on the device and
+//    run the cached plan with no host round trip (the plan cache, its gated
+//    launches and stream-ordered retirement).
+//
+//  * the C-ABI entry points (the `extern "C"` block at the end).
+//
+// The library's other translation units: gp_sort.hip (hipCUB radix sort),
+// gp_runtime.hip (runtime helpers and IPC, no kernels), gp_host.cpp (the host
+// row ops).  Wave64 throughout: 256-thread workgroups = 4 waves, one per SIMD.
 
 #include <hip/hip_runtime.h>
 #include <unistd.h>
