@@ -15,6 +15,8 @@
 //   r6_multichunk_tune [rounds]      (1M x 1024 fp32 shard; NB = 2 and 8)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include \
 //   scripts/tune/r6_multichunk_tune.hip geeps_amd/csrc/gp_sort.hip -o build/probe/r6_multichunk_tune
+// (-DR6_CHUNK_SIZES: the second pass, one chunk per launch at other chunk
+// sizes, i.e. register tile counts).
 #include "../../geeps_amd/csrc/gp_reduce.hip"
 
 #include <algorithm>
@@ -136,6 +138,21 @@ int main(int argc, char **argv) {
     BucketPtrs b = {};
     for (int k = 0; k < NB; ++k) b.p[k] = reinterpret_cast<const float *>(bk[k]);
     std::vector<Variant> vs;
+#ifdef R6_CHUNK_SIZES
+    // round 6, second pass: one chunk per launch, chunk size by register tiles
+    if (NB == 2) {
+      vs.push_back(make<2, 7, 1, 8, 1>("prod shape"));
+      vs.push_back(make<2, 3, 1, 8, 1>("64 MiB"));
+      vs.push_back(make<2, 9, 1, 8, 1>("112 MiB"));
+      vs.push_back(make<2, 11, 1, 8, 1>("128 MiB"));
+      vs.push_back(make<2, 13, 1, 8, 1>("144 MiB"));
+    } else {
+      vs.push_back(make<8, 7, 1, 8, 1>("prod shape"));
+      vs.push_back(make<8, 8, 1, 8, 1>("104 MiB"));
+      vs.push_back(make<8, 9, 1, 8, 1>("112 MiB"));
+      vs.push_back(make<8, 11, 1, 8, 1>("128 MiB"));
+    }
+#else
     if (NB == 2) {
       vs.push_back(make<2, 7, 1, 8, 1>("prod shape"));
       vs.push_back(make<2, 7, 1, 8, 2>("prod shape"));
@@ -148,6 +165,7 @@ int main(int argc, char **argv) {
       vs.push_back(make<8, 7, 1, 8, 2>("prod shape"));
       vs.push_back(make<8, 7, 1, 8, 3>("prod shape"));
     }
+#endif
     // bit check against production (gp_bucket_sum_into over the same prefix)
     for (auto &v : vs) {
       const size_t launches = n4 / v.chunk_f4, covered = launches * v.chunk_f4;
