@@ -124,6 +124,7 @@ ClientLib::ClientLib(uint32_t process_id, const GeePsConfig &config)
     for (uint32_t s = 0; s < num_processes_; ++s)
       ch->client_send_mu.push_back(std::make_unique<std::mutex>());
     ch->ipc_oplogs.resize(num_processes_);
+    ch->ipc_parked.resize(num_processes_);
     ch->host_oplogs.resize(num_processes_);
     ch->host_share_off.assign(num_processes_, 0);
     ch->ipc_client.assign(num_processes_, 0);
@@ -239,6 +240,8 @@ void ClientLib::shutdown() {
     chp->server->stop();
     for (auto &m : chp->ipc_oplogs)
       for (auto &kv : m) gp_ipc_close_handle(kv.second);
+    for (auto &parked : chp->ipc_parked)
+      for (void *p : parked) gp_ipc_close_handle(p);
     for (auto &pc : chp->tables)
       for (auto &per_server : pc.server_versions)
         for (auto &kv : per_server) gp_ipc_close_handle(kv.second);

@@ -273,6 +273,13 @@ struct Channel {
   // takes refreshes in place (its ZMTP READY said so), and which master versions'
   // IPC handles it already has
   std::vector<std::map<uint64_t, void *>> ipc_oplogs;    // [client][buffer id]
+  // mappings of oplog buffers a client has since replaced: kept mapped until
+  // Shutdown, so that their addresses are never reused by this process's own
+  // buffers while peers may still open handles to those (the runtime resolves
+  // a handle by (pid, address) at open time and was seen to hand out stale
+  // memory for addresses that had held a closed mapping: DESIGN.md §4).  Per
+  // client, as ipc_oplogs: only that client's reader thread touches its entry.
+  std::vector<std::vector<void *>> ipc_parked;  // [client]
   // same-node clients' shared host oplogs (a table with a host tier)
   std::vector<std::map<uint64_t, std::shared_ptr<SharedHostMem>>> host_oplogs;  // [client][buffer id]
   // client side, [server]: it could not map a shared host oplog (its NACK),

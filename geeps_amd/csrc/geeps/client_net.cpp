@@ -236,7 +236,7 @@ void ClientLib::server_reader(Channel &ch, uint32_t client_id, int fd) {
         if (ref.has_handle) {
           auto old = mapped.find(ref.buffer_id);
           if (old != mapped.end()) {
-            GP_CALL(gp_ipc_close_handle(old->second));
+            ch.ipc_parked[client_id].push_back(old->second);  // closed at Shutdown (client.hpp)
             mapped.erase(old);
           }
           void *p = nullptr;

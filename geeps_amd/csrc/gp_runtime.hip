@@ -114,14 +114,15 @@ struct LiveMapping {
 };
 std::map<void *, LiveMapping> g_ipc_live;
 
-// Mis-mappings: closed ones (a fresh mapping of the wrong memory: nothing else
-// uses it) and kept ones (the runtime returned an address this process already
-// maps for another handle: closing it could tear that live mapping down).  Past
-// kIpcMaxMismaps of either, every later open is refused (libgeeps then moves
-// the rows by socket): a runtime that keeps mis-mapping is not retried forever.
+// Mis-mappings stay mapped (never used): unmapped, their address would go to
+// this process's next allocation, and a handle to a buffer at an address that
+// had held a closed mapping is what the runtime was seen to resolve to stale
+// memory (round 6 audit).  Counted (gp_ipc_mismaps); past
+// kIpcMaxMismaps every
+// later open is refused (libgeeps then moves the rows by socket): a runtime
+// that keeps mis-mapping is not retried forever.
 constexpr int kIpcMaxMismaps = 16;
-int g_ipc_mismaps_closed = 0;  // g_ipc_mu
-int g_ipc_mismaps_kept = 0;    // g_ipc_mu
+int g_ipc_mismaps = 0;  // g_ipc_mu
 
 int ipc_stream(hipStream_t *s) {
   int dev = 0;
@@ -428,13 +429,12 @@ int gp_ipc_open_handle(void **device_ptr, const void *handle) {
   std::memcpy(&in, handle, sizeof in);
   if ((uint32_t)(in.tag[0] >> 32) != kIpcTagMagic) return set_error(GP_ERR_INVALID, "not a gp_ipc_get_handle handle");
   std::lock_guard<std::mutex> lk(g_ipc_mu);
-  if (g_ipc_mismaps_closed + g_ipc_mismaps_kept >= kIpcMaxMismaps) {
+  if (g_ipc_mismaps >= kIpcMaxMismaps) {
     char msg[160];
     std::snprintf(msg, sizeof msg,
-                  "IPC mapping refused: the runtime mis-mapped %d handles in this process (%d closed, %d kept "
-                  "as aliases of live mappings); the limit is %d",
-                  g_ipc_mismaps_closed + g_ipc_mismaps_kept, g_ipc_mismaps_closed, g_ipc_mismaps_kept,
-                  kIpcMaxMismaps);
+                  "IPC mapping refused: the runtime mis-mapped %d handles in this process (kept mapped, unused); "
+                  "the limit is %d",
+                  g_ipc_mismaps, kIpcMaxMismaps);
     return set_error(GP_ERR_HIP, msg);
   }
   void *p = nullptr;
@@ -489,17 +489,9 @@ int gp_ipc_open_handle(void **device_ptr, const void *handle) {
     why += "; " + describe(in);
     if (read) why += "; " + describe_read(got, p);
     why += "; runtime handle " + hex_bytes(&in.h, sizeof in.h);
-    if (g_ipc_live.count(p)) {
-      // a second reference to a live mapping: closing it could unmap that
-      // one; kept (counted, bounded)
-      ++g_ipc_mismaps_kept;
-      why += "; kept mapped";
-    } else {
-      // a fresh mapping of the wrong memory, used by nothing: unmapped again
-      const bool closed = hipIpcCloseMemHandle(p) == hipSuccess;
-      ++g_ipc_mismaps_closed;
-      why += closed ? "; unmapped" : "; unmapping it failed";
-    }
+    // kept mapped, never used (above); counted and bounded
+    ++g_ipc_mismaps;
+    why += "; kept mapped, unused";
     (void)hipGetLastError();  // no failed call's error may linger into a later launch check
     return set_error(GP_ERR_HIP, why);
   }
@@ -526,11 +518,10 @@ int gp_ipc_describe_handle(const void *handle, char *buf, int len) {
   return GP_OK;
 }
 
-int gp_ipc_mismaps(int *closed, int *kept) {
-  if (!closed || !kept) return set_error(GP_ERR_INVALID, "null pointer");
+int gp_ipc_mismaps(int *count) {
+  if (!count) return set_error(GP_ERR_INVALID, "null pointer");
   std::lock_guard<std::mutex> lk(g_ipc_mu);
-  *closed = g_ipc_mismaps_closed;
-  *kept = g_ipc_mismaps_kept;
+  *count = g_ipc_mismaps;
   return GP_OK;
 }
 

@@ -133,7 +133,7 @@ _SIGNATURES = {
     "gp_ipc_open_handle": (_i, [_c.POINTER(_vp), _vp]),
     "gp_ipc_close_handle": (_i, [_vp]),
     "gp_ipc_describe_handle": (_i, [_vp, _c.c_char_p, _i]),
-    "gp_ipc_mismaps": (_i, [_c.POINTER(_i), _c.POINTER(_i)]),
+    "gp_ipc_mismaps": (_i, [_c.POINTER(_i)]),
 }
 
 _lock = threading.Lock()

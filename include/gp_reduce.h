@@ -462,20 +462,20 @@ int gp_device_pci_bus_id(int device, char *buf, int len);
  * GP_ERR_HIP instead of handing out wrong rows. */
 #define GP_IPC_HANDLE_BYTES 96
 int gp_ipc_get_handle(void *handle_out, void *device_base);
-/* ABI 16: a mapping that fails the tag check is unmapped again (or, when the
- * runtime returned the address of a mapping this process already holds, left
- * as it is), and the error names what the handle names, what the mapping held
- * and the raw runtime handle; after 16 such mis-mappings in one process every
- * later open is refused (GP_ERR_HIP). */
+/* ABI 16: a mapping that fails the tag check is left mapped and never used
+ * (unmapped, its address could go to a buffer this process exports later,
+ * which the runtime may then resolve to stale memory: DESIGN.md §4), and the
+ * error names what the handle names, what the mapping held and the raw
+ * runtime handle; after 16 such mis-mappings in one process every later open
+ * is refused (GP_ERR_HIP). */
 int gp_ipc_open_handle(void **device_ptr, const void *handle);
 int gp_ipc_close_handle(void *device_ptr);
 /* ABI 16: one line on a handle (NUL-terminated in buf[len]): the exporter's
  * pid, buffer base and size as libgeeps recorded them, the process and
  * address the runtime's handle names, and whether the two agree. */
 int gp_ipc_describe_handle(const void *handle, char *buf, int len);
-/* ABI 16: this process's mis-mapped opens so far (closed: unmapped again;
- * kept: aliases of a live mapping). */
-int gp_ipc_mismaps(int *closed, int *kept);
+/* ABI 16: this process's mis-mapped opens so far (each left mapped, unused). */
+int gp_ipc_mismaps(int *count);
 
 #ifdef __cplusplus
 }  /* extern "C" */
