@@ -20,8 +20,9 @@
 // strtoull + a map lookup + sendmsg(SCM_RIGHTS) in the server thread).  So a
 // handle is only as good as the exporter's address map at open time; libgeeps
 // never frees an exported buffer while it runs (oplogs are retired, master
-// versions kept: DESIGN.md §4), and every mapping is checked against a tag
-// before any of its bytes is used.
+// versions kept), never unmaps a mapping before Shutdown (an address that had
+// held a closed mapping was what the runtime misresolved: DESIGN.md §4), and
+// checks every mapping against a tag before any of its bytes is used.
 
 #include <hip/hip_runtime.h>
 #include <unistd.h>
