@@ -1,7 +1,8 @@
 """geeps_amd — MI355X-native GeePS gradient-update reduction path.
 
 Product code:
-  * geeps_amd/csrc/gp_reduce.hip   HIP kernels + C-ABI (include/gp_reduce.h)
+  * geeps_amd/csrc/gp_kernels.hpp  HIP kernels (gfx950); gp_reduce.hip, gp_unplanned.hip,
+                                   gp_runtime.hip, gp_host.cpp: the C-ABI (include/gp_reduce.h)
   * geeps_amd/csrc/geeps/          C++ drop-in libgeeps (include/geeps.hpp)
   * geeps_amd/native.py            ctypes binding of the C-ABI
   * geeps_amd/rowops.py            reference-named row ops / N-way sum on tensors

@@ -394,7 +394,7 @@ def test_c_abi_consumer_builds_as_c99(tmp_path):
 
 def test_sweep_shapes_and_plan_cover_every_headline_shard():
     """For 1-8 buckets and the 1/2/4/8-GPU shards of the 1M x 1024 table, the
-    launch plan uses the documented sweep shapes (gp_reduce.hip SweepShape:
+    launch plan uses the documented sweep shapes (gp_kernels.hpp SweepShape:
     32-KiB tiles, bursts of 1 at 2-8 buckets; 16-KiB tiles, bursts of 8 at 1)
     and its chunks never overrun the shard (96-MiB chunks, then 64-MiB ones at
     3-8 buckets, on 256 CUs without a device)."""

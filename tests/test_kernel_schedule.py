@@ -2,7 +2,7 @@
 burst's loads issued together, then waited on with counted vmcnt(N).  One
 compiler choice regrouped the register tiles' adds into load -> vmcnt(0) ->
 add chains (117-224 full drains per chunk, 8.3 instead of 6.5 ms at 8 buckets;
-profiles/r01b/sweep_ab.txt).  This compiles the product kernel file to gfx950
+profiles/r01b/sweep_ab.txt).  This compiles the product kernel translation units to gfx950
 assembly (no GPU needed) and fails if that comes back."""
 import os
 import re
@@ -20,12 +20,20 @@ HIPCC = "/opt/rocm/bin/hipcc"
 def asm(tmp_path_factory):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not installed")
-    out = tmp_path_factory.mktemp("asm") / "gp_reduce.s"
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I",
-                    os.path.join(REPO, "include"), "--cuda-device-only", "-S", "-o", str(out),
-                    os.path.join(REPO, "geeps_amd", "csrc", "gp_reduce.hip")],
-                   check=True, capture_output=True, cwd=str(out.parent))
-    return out.read_text()
+    # both translation units over gp_kernels.hpp: gp_reduce.hip launches the
+    # plain forms (bucket sums, row plans), gp_unplanned.hip the GATED ones
+    # (the unplanned calls' steady state); each instantiates its own copy
+    # (compiled side by side)
+    d = tmp_path_factory.mktemp("asm")
+    tus = ("gp_unplanned", "gp_reduce")
+    procs = [subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I",
+                               os.path.join(REPO, "include"), "--cuda-device-only", "-S", "-o", str(d / f"{tu}.s"),
+                               os.path.join(REPO, "geeps_amd", "csrc", f"{tu}.hip")],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, cwd=str(d)) for tu in tus]
+    for p in procs:
+        _, err = p.communicate()
+        assert p.returncode == 0, err.decode()[-2000:]
+    return "".join((d / f"{tu}.s").read_text() for tu in tus)
 
 
 def _kernel(asm, pattern):
@@ -36,7 +44,7 @@ def _kernel(asm, pattern):
 
 
 # (buckets, register tiles, tiles per burst, zero-input, 4-KiB block-strides
-# per tile): every production instantiation (gp_reduce.hip: SweepShape's
+# per tile): every production instantiation (gp_kernels.hpp: SweepShape's
 # 96-MiB chunks, the 64-MiB chunks after them, the zero-input form)
 SWEEP_SHAPES = ([(1, 14, 8, 0, 4)] + [(nb, 7, 1, 0, 8) for nb in range(2, 9)]
                 + [(nb, 6, 4, 0, 4) for nb in range(3, 9)] + [(1, 6, 4, 1, 4)])
@@ -79,7 +87,7 @@ def test_wave_kernels_fit_their_occupancy(asm):
 
 @pytest.mark.parametrize("rt,tg,zin", [(14, 8, 0), (6, 4, 1), (6, 4, 0)])
 def test_gated_sweep_kernel_keeps_burst_schedule(asm, rt, tg, zin):
-    """The GATED = true forms (the unplanned calls' steady state, gp_reduce.hip
+    """The GATED = true forms (the unplanned calls' steady state, gp_unplanned.hip
     "Device-built plans") run the gate test, then the same body: the same
     loads, and no more full drains than the plain form."""
     plain = _kernel(asm, rf"_ZN12_GLOBAL__N_123bucket_sum_sweep_kernelILi1ELi{rt}ELi{tg}ELb{zin}ELi4ELb0EE")
