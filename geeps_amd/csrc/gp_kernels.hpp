@@ -97,11 +97,11 @@ struct BucketPtrs {
 };
 
 // A launch that runs or exits at its start by a device word an earlier launch
-// on the same stream wrote: the unplanned calls' steady state (§ "Device-built
-// plans" below) launches both the cached plan and the op-order fallback right
-// behind the index check, and exactly one of them does any work, with no host
-// round trip.  `word` holds the generation of the last call whose check found
-// the index changed; this call's generation is `gen`.  A kernel's GATED = true
+// on the same stream wrote: the unplanned calls' steady state ("Device-built
+// plans", gp_unplanned.hip) launches both the cached plan and the op-order
+// fallback right behind the index check, and exactly one of them does any
+// work, with no host round trip.  `word` holds the generation of the last call
+// whose check found the index changed; this call's generation is `gen`.  A kernel's GATED = true
 // instantiation runs this test first and takes the Gate as its last argument;
 // GATED = false (the default, every other launch) compiles to the same code as
 // without it (tests/test_kernel_schedule.py checks the sweep kernel's schedule).
@@ -1220,36 +1220,11 @@ int launch_row_op_seg(float *flat_ptr, const gp_row_segments *t,
   return GP_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Row plans: a scatter DoubleIndex compiled once (libgeeps' indexes are fixed
-// at FinishVirtualIteration, clientlib-viter.cpp:817-883).
-//
-// The plan visits the rows in destination (id1) order, offsets applied.  That
-// is bit-neutral because destinations are distinct: every destination row
-// receives exactly the same adds whatever order the rows are visited in.
-//  * Dense runs: maximal runs in which id0 and id1 both step by one and every
-//    row is clear of num_vals_limit are plain ranges y[y0 .. y0 + L*W) (+)=
-//    x[x0 .. x0 + L*W).  Runs of at least kDenseRunBytes go to the phase-
-//    separated sum kernels (one bucket; the fused init through their ZIN
-//    form), which read no index and, unlike any single-pass form, keep their
-//    rate on every allocation: over 10 fresh allocations the add ran 76.5-
-//    80.9 % of 8 TB/s this way against 63-80 % through the wave-map kernel,
-//    which fell to 63-69 % on 7 of them (profiles/r02/tune/rowop_alloc*.txt).
-//    libgeeps assigns cache rows in first-access order, so an op's rows are
-//    typically one run per channel.
-//  * The other rows keep a device index, sorted by id1, for the wave-map
-//    kernel with non-temporal oplog accesses and one resident round of blocks:
-//    the read-modify-write side walks the oplog front to back like the
-//    gather's write side: 77-79 % for a random permutation, against 63-65 %
-//    for the same index in op order through row_op_kernel (plan_tune*.txt).
-// ---------------------------------------------------------------------------
+// Dense id0 / id1 runs (row plans, gp_reduce.hip; the unplanned calls' scan,
+// gp_unplanned.hip) of at least this many bytes go to the sum kernels above.
 // A dense run launches 1-3 kernels; below 4 MiB (the phased form's smallest
 // shard) the row kernel moves it without the launches.
 constexpr size_t kDenseRunBytes = 4u << 20;
-
-struct RowRun {
-  uint64_t x_row, y_row, rows;  // offsets applied
-};
 
 }  // namespace
 

@@ -59,6 +59,37 @@ __global__ __launch_bounds__(kBlock) void hbm_read_probe_kernel(const f4 *__rest
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// Row plans: a scatter DoubleIndex compiled once (libgeeps' indexes are fixed
+// at FinishVirtualIteration, clientlib-viter.cpp:817-883).
+//
+// The plan visits the rows in destination (id1) order, offsets applied.  That
+// is bit-neutral because destinations are distinct: every destination row
+// receives exactly the same adds whatever order the rows are visited in.
+//  * Dense runs: maximal runs in which id0 and id1 both step by one and every
+//    row is clear of num_vals_limit are plain ranges y[y0 .. y0 + L*W) (+)=
+//    x[x0 .. x0 + L*W).  Runs of at least kDenseRunBytes go to the phase-
+//    separated sum kernels (one bucket; the fused init through their ZIN
+//    form), which read no index and, unlike any single-pass form, keep their
+//    rate on every allocation: over 10 fresh allocations the add ran 76.5-
+//    80.9 % of 8 TB/s this way against 63-80 % through the wave-map kernel,
+//    which fell to 63-69 % on 7 of them (profiles/r02/tune/rowop_alloc*.txt).
+//    libgeeps assigns cache rows in first-access order, so an op's rows are
+//    typically one run per channel.
+//  * The other rows keep a device index, sorted by id1, for the wave-map
+//    kernel with non-temporal oplog accesses and one resident round of blocks:
+//    the read-modify-write side walks the oplog front to back like the
+//    gather's write side: 77-79 % for a random permutation, against 63-65 %
+//    for the same index in op order through row_op_kernel (plan_tune*.txt).
+// ---------------------------------------------------------------------------
+namespace {
+
+struct RowRun {
+  uint64_t x_row, y_row, rows;  // offsets applied
+};
+
+}  // namespace
+
 struct gp_row_plan_s {
   size_t num_rows = 0, row_size = 0, limit = 0;
   bool gather = false;  // a gather plan (y[id0] = x[id1]); else a scatter plan
