@@ -147,7 +147,16 @@ def test_host_row_ops_refuse_rows_outside_the_arrays(op):
     # ... but a row the limit lets in is checked
     with pytest.raises(ValueError, match="out of range"):
         fn(y, x, guarded_big, row_size=W, num_vals_limit=8 * W)
-    assert np.array_equal(y[4 * W:], np.ones(W, np.float32))
+    # an unsigned index (the reference's size_t ids) is checked the same way,
+    # including ids past 2^63 that a signed view would read as negative
+    fn(y, x, entry(2, 4).astype(np.uint64), row_size=W)
+    huge = entry(0, 0).astype(np.uint64)
+    huge[0, 1 if op != "gather" else 0] = np.uint64(1 << 63)
+    with pytest.raises(ValueError, match="out of range"):
+        fn(y, x, huge, row_size=W)
+    # the two in-range calls ran (the add twice), nothing else touched y
+    assert np.array_equal(y[4 * W:], np.full(W, 2.0 if op == "add" else 1.0, np.float32))
+    assert not y[:4 * W].any()
 
 
 def test_host_row_ops_from_concurrent_callers():
