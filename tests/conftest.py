@@ -48,6 +48,8 @@ FAMILIES = [
      ("test_row_plan", "test_gather_plan")),
     ("C-ABI from C99 vs oracle", "test_gpu_parity", ("test_c_abi_consumer",)),
     ("IPC buffers between processes through the C-ABI (tagged mappings)", "test_ipc", ("test_",)),
+    ("IPC audit: the runtime's mis-mappings re-derived from the committed round-6 logs (CPU)", "test_ipc_audit",
+     ("test_",)),
     ("libgeeps end to end (other process / consistency cases)", "test_libgeeps", ("test_",)),
     ("wire path: libgeeps ZMTP/3.0 ROUTER vs a stock libzmq ROUTER (CPU)", "test_zmtp", ("test_",)),
     ("host-tier row ops (a4: add_rows_from_double_index_cpu ...) vs oracle (CPU)", "test_host_rows", ("test_",)),
