@@ -9,7 +9,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 O=$GRAFT_REPO_ROOT/gpurun_out/r06/tsan; mkdir -p $O
 export PYTHONUNBUFFERED=1
-export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 report_signal_unsafe=0"
+export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 report_signal_unsafe=0 suppressions=$GRAFT_REPO_ROOT/scripts/tsan.supp"
 APP=$GRAFT_REPO_ROOT/build/tsan/geeps_sum_app
 GEEPS_SUM_APP=$APP timeout -k 10 240 python -u -m pytest tests/test_libgeeps.py -m gpu -v -x \
   -k "test_two_processes_loopback_bsp" --timeout 200 --timeout-method thread > $O/pytest_first.log 2>&1
