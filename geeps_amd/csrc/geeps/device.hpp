@@ -17,6 +17,37 @@
 
 namespace geeps {
 
+// Page-locked host memory through the C-ABI.  In a ThreadSanitizer build
+// (scripts/build_tsan.sh) the HIP runtime's allocator is not instrumented:
+// TSan cannot see that a block one thread freed and another thread got back
+// from the runtime was ordered by the runtime's own locking, and reports the
+// two threads' accesses to it as a race.  The free releases and the
+// allocation acquires on the block's address, stating that edge.
+#if defined(__has_feature)
+#if __has_feature(thread_sanitizer)
+extern "C" void __tsan_acquire(void *addr);
+extern "C" void __tsan_release(void *addr);
+#define GEEPS_TSAN_ACQUIRE(p) __tsan_acquire(p)
+#define GEEPS_TSAN_RELEASE(p) __tsan_release(p)
+#endif
+#endif
+#ifndef GEEPS_TSAN_ACQUIRE
+#define GEEPS_TSAN_ACQUIRE(p) ((void)(p))
+#define GEEPS_TSAN_RELEASE(p) ((void)(p))
+#endif
+
+inline void *pinned_alloc(size_t bytes) {
+  void *p = nullptr;
+  GP_CALL(gp_malloc_host(&p, bytes));
+  GEEPS_TSAN_ACQUIRE(p);
+  return p;
+}
+
+inline int pinned_free(void *p) {
+  GEEPS_TSAN_RELEASE(p);
+  return gp_free_host(p);
+}
+
 class Stream {
  public:
   Stream() { GP_CALL(gp_stream_create(&s_)); }
@@ -116,15 +147,11 @@ class PinnedArray {
   PinnedArray &operator=(const PinnedArray &) = delete;
   void resize(size_t n) {
     release();
-    if (n) {
-      void *p = nullptr;
-      GP_CALL(gp_malloc_host(&p, n * sizeof(T)));
-      p_ = static_cast<T *>(p);
-    }
+    if (n) p_ = static_cast<T *>(pinned_alloc(n * sizeof(T)));
     n_ = n;
   }
   void release() {
-    if (p_) GP_CALL(gp_free_host(p_));
+    if (p_) GP_CALL(pinned_free(p_));
     p_ = nullptr;
     n_ = 0;
   }
@@ -157,9 +184,7 @@ class HostBuf {
                 << "); this host oplog's rows go to same-node servers by socket\n";
     }
     if (pinned) {
-      void *p = nullptr;
-      GP_CALL(gp_malloc_host(&p, n * sizeof(float)));
-      p_ = static_cast<float *>(p);
+      p_ = static_cast<float *>(pinned_alloc(n * sizeof(float)));
     } else {
       p_ = new float[n];
     }
@@ -167,7 +192,7 @@ class HostBuf {
   ~HostBuf() {
     if (!p_ || shm_) return;  // (shm_ unmaps itself)
     if (pinned_)
-      gp_free_host(p_);
+      pinned_free(p_);
     else
       delete[] p_;
   }
