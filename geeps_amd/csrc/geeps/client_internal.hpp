@@ -5,6 +5,7 @@
 // client_data.cpp, client_net.cpp): not part of libgeeps' interface.
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <memory>
@@ -48,11 +49,18 @@ inline std::string ipc_describe(const void *handle) {
   return buf;
 }
 
+// A reader thread's pinned receive buffers: one is reused once no batch holds
+// it.  use_count() is a relaxed load; the acquire fence after it pairs with the
+// release in the last holder's decrement (another thread: the server, done
+// with the rows), so this thread's next writes follow that holder's use.
 struct PinnedPool {
   std::vector<std::shared_ptr<PinnedArray<float>>> bufs;
   std::shared_ptr<PinnedArray<float>> get(size_t floats) {
     for (auto &b : bufs)
-      if (b.use_count() == 1 && b->size() >= floats) return b;
+      if (b.use_count() == 1 && b->size() >= floats) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return b;
+      }
     bufs.push_back(std::make_shared<PinnedArray<float>>(std::max<size_t>(floats, 1)));
     return bufs.back();
   }
